@@ -1,0 +1,212 @@
+"""CPU oracle for the GP posterior update -- TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product. Only ``tests/``,
+``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py`` may
+import it. The product path (``mfgp_coverage_amd``) never imports it and fails
+loudly when its HIP library is missing.
+
+It restates, in NumPy, the single hot path of MSU-dcypherlab/mfgp-coverage
+(``/root/reference``):
+
+* ``se_kernel``        <- ``SFGP.kernel`` gaussian_process.py:66-79
+                          (``MFGP.kernel`` gaussian_process.py:329-342 is identical)
+* ``sf_faithful``      <- ``SFGP.updt_info`` gp:229-255 + ``SFGP.predict`` gp:121-148,
+                          same op sequence (dense K(X*,X*), four ``np.linalg.solve``,
+                          dense ``psi @ beta``), returns ``diag`` of the covariance.
+* ``mf_faithful``      <- ``MFGP.updt_info`` gp:493-529 + ``MFGP.predict`` gp:401-438.
+* ``sf_diag``/``mf_diag`` -- the same math with a Cholesky, two triangular solves
+                          and a row-sum of squares (no M x M matrices). This is the
+                          semantic spec of the HIP kernels and the stronger CPU
+                          baseline.
+
+Pinning: ``tests/test_oracle.py`` checks this module
+against golden vectors produced by importing the reference itself in the build
+container (``tests/golden/make_golden.py``), against the reference's own logged
+runs (``Data/*_agent.csv`` VarMax / Var0 replays), and against closed forms.
+
+Hyperparameter layouts (log-scaled, simulator.py:53-56, 83-84):
+  SF: [mu, s^2, L, noise]
+  MF: [mu_lo, s^2_lo, L_lo, mu_hi, s^2_hi, L_hi, rho, noise_lo, noise_hi]
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.linalg as sla
+
+JITTER = 1e-8  # gaussian_process.py:42 (SF) and :298 (MF)
+
+
+def se_kernel(x, xp, log_s2, log_l):
+    """Squared-exponential kernel, gaussian_process.py:66-79.
+
+    Scales before subtracting (``x/l - xp/l``, gp:77-78); ``s`` and ``l`` are the
+    exponentiated log hyperparameters (gp:75-76).
+    """
+    output_scale = np.exp(log_s2)
+    lengthscale = np.exp(log_l)
+    diffs = np.expand_dims(x / lengthscale, 1) - np.expand_dims(xp / lengthscale, 0)
+    return output_scale * np.exp(-0.5 * np.sum(diffs ** 2, axis=2))
+
+
+# ---------------------------------------------------------------------------
+# Reference-faithful restatements (same op sequence, dense covariance)
+# ---------------------------------------------------------------------------
+
+def sf_faithful(X, y, hyp, Xs, jitter=JITTER, return_cov=False):
+    """SFGP.updt_info (gp:229-255) then SFGP.predict (gp:121-148)."""
+    X = np.asarray(X, dtype=np.float64).reshape(-1, 2)
+    y = np.asarray(y, dtype=np.float64).reshape(-1, 1)
+    hyp = np.asarray(hyp, dtype=np.float64)
+    N = y.shape[0]
+    sigma_n = np.exp(hyp[-1])                                        # gp:248-249
+    K = se_kernel(X, X, hyp[1], hyp[2]) + np.eye(N) * sigma_n        # gp:253
+    L = np.linalg.cholesky(K + np.eye(N) * jitter)                  # gp:254
+    mean = np.exp(hyp[0])                                            # gp:132
+    yc = y - mean                                                    # gp:133
+    psi = se_kernel(Xs, X, hyp[1], hyp[2])                           # gp:139
+    alpha = np.linalg.solve(np.transpose(L), np.linalg.solve(L, yc))  # gp:141
+    mu = np.matmul(psi, alpha) + mean                                # gp:142-143
+    beta = np.linalg.solve(np.transpose(L), np.linalg.solve(L, psi.T))  # gp:145
+    cov = se_kernel(Xs, Xs, hyp[1], hyp[2]) - np.matmul(psi, beta)   # gp:146
+    if return_cov:
+        return mu[:, 0], cov
+    return mu[:, 0], np.diag(cov).copy()
+
+
+def _mf_parts(hyp):
+    hyp = np.asarray(hyp, dtype=np.float64)
+    theta_L, theta_H = hyp[0:3], hyp[3:6]                            # gp:310-313
+    rho = np.exp(hyp[-3])                                            # gp:414
+    mean_L = np.exp(theta_L[0])                                      # gp:415
+    mean_H = rho * mean_L + np.exp(theta_H[0])                       # gp:416
+    return theta_L, theta_H, rho, mean_L, mean_H
+
+
+def mf_K(XL, XH, hyp, jitter=JITTER):
+    """Block covariance of MFGP.updt_info, gp:510-529 (jitter included)."""
+    theta_L, theta_H, rho, _, _ = _mf_parts(hyp)
+    sigma_n_L = np.exp(hyp[-2])
+    sigma_n_H = np.exp(hyp[-1])
+    NL, NH = XL.shape[0], XH.shape[0]
+    K_LL = se_kernel(XL, XL, theta_L[1], theta_L[2]) + np.eye(NL) * sigma_n_L   # gp:523
+    K_LH = rho * se_kernel(XL, XH, theta_L[1], theta_L[2])                     # gp:524
+    K_HH = rho ** 2 * se_kernel(XH, XH, theta_L[1], theta_L[2]) + \
+        se_kernel(XH, XH, theta_H[1], theta_H[2]) + np.eye(NH) * sigma_n_H     # gp:525-526
+    K = np.vstack((np.hstack((K_LL, K_LH)), np.hstack((K_LH.T, K_HH))))       # gp:527-528
+    return K + np.eye(NL + NH) * jitter
+
+
+def mf_psi(Xs, XL, XH, hyp):
+    """Cross covariance of MFGP.predict, gp:426-429."""
+    theta_L, theta_H, rho, _, _ = _mf_parts(hyp)
+    psi1 = rho * se_kernel(Xs, XL, theta_L[1], theta_L[2])
+    psi2 = rho ** 2 * se_kernel(Xs, XH, theta_L[1], theta_L[2]) + \
+        se_kernel(Xs, XH, theta_H[1], theta_H[2])
+    return np.hstack((psi1, psi2))
+
+
+def mf_faithful(XL, yL, XH, yH, hyp, Xs, jitter=JITTER, return_cov=False):
+    """MFGP.updt_info (gp:493-529) then MFGP.predict (gp:401-438)."""
+    XL = np.asarray(XL, dtype=np.float64).reshape(-1, 2)
+    XH = np.asarray(XH, dtype=np.float64).reshape(-1, 2)
+    yL = np.asarray(yL, dtype=np.float64).reshape(-1, 1)
+    yH = np.asarray(yH, dtype=np.float64).reshape(-1, 1)
+    theta_L, theta_H, rho, mean_L, mean_H = _mf_parts(hyp)
+    L = np.linalg.cholesky(mf_K(XL, XH, hyp, jitter))                # gp:529
+    y = np.vstack((yL - mean_L, yH - mean_H))                        # gp:419-424
+    psi = mf_psi(Xs, XL, XH, hyp)                                    # gp:426-429
+    alpha = np.linalg.solve(np.transpose(L), np.linalg.solve(L, y))  # gp:431
+    mu = mean_H + np.matmul(psi, alpha)                              # gp:432
+    beta = np.linalg.solve(np.transpose(L), np.linalg.solve(L, psi.T))  # gp:434
+    cov = rho ** 2 * se_kernel(Xs, Xs, theta_L[1], theta_L[2]) + \
+        se_kernel(Xs, Xs, theta_H[1], theta_H[2]) - np.matmul(psi, beta)  # gp:435-436
+    if return_cov:
+        return mu[:, 0], cov
+    return mu[:, 0], np.diag(cov).copy()
+
+
+# ---------------------------------------------------------------------------
+# Diag-only restatements (semantic spec of the kernels; scalable CPU baseline)
+# ---------------------------------------------------------------------------
+
+def _diag_solve(K, psi, r, kss, mean):
+    N = K.shape[0]
+    if N == 0:
+        M = psi.shape[0]
+        return np.full(M, mean, dtype=np.float64), np.full(M, kss, dtype=np.float64)
+    L = np.linalg.cholesky(K)
+    V = sla.solve_triangular(L, psi.T, lower=True, check_finite=False)   # V = L^-1 psi^T
+    z = sla.solve_triangular(L, r, lower=True, check_finite=False)       # z = L^-1 (y - m)
+    mu = mean + V.T @ z                       # psi alpha = psi L^-T L^-1 r = V^T z
+    var = kss - np.einsum("ij,ij->j", V, V)   # diag(k** - psi K^-1 psi^T)
+    return mu, var
+
+
+def sf_diag(X, y, hyp, Xs, jitter=JITTER):
+    """Posterior mean and diagonal variance of SFGP (gp:229-255, 121-148)."""
+    X = np.asarray(X, dtype=np.float64).reshape(-1, 2)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    hyp = np.asarray(hyp, dtype=np.float64)
+    N = X.shape[0]
+    K = se_kernel(X, X, hyp[1], hyp[2]) + np.eye(N) * np.exp(hyp[-1])
+    K = K + np.eye(N) * jitter
+    psi = se_kernel(Xs, X, hyp[1], hyp[2])
+    mean = np.exp(hyp[0])
+    kss = np.exp(hyp[1])            # kernel(X*,X*) diagonal = s * exp(0)
+    return _diag_solve(K, psi, y - mean, kss, mean)
+
+
+def mf_diag(XL, yL, XH, yH, hyp, Xs, jitter=JITTER):
+    """Posterior mean and diagonal variance of MFGP (gp:493-529, 401-438)."""
+    XL = np.asarray(XL, dtype=np.float64).reshape(-1, 2)
+    XH = np.asarray(XH, dtype=np.float64).reshape(-1, 2)
+    yL = np.asarray(yL, dtype=np.float64).reshape(-1)
+    yH = np.asarray(yH, dtype=np.float64).reshape(-1)
+    theta_L, theta_H, rho, mean_L, mean_H = _mf_parts(hyp)
+    K = mf_K(XL, XH, hyp, jitter)
+    psi = mf_psi(Xs, XL, XH, hyp)
+    r = np.concatenate((yL - mean_L, yH - mean_H))
+    kss = rho ** 2 * np.exp(theta_L[1]) + np.exp(theta_H[1])
+    return _diag_solve(K, psi, r, kss, mean_H)
+
+
+def prior_variance(hyp):
+    """Known-answer Var0: variance of the empty GP."""
+    hyp = np.asarray(hyp, dtype=np.float64)
+    if hyp.shape[0] == 4:
+        return np.exp(hyp[1])
+    rho = np.exp(hyp[6])
+    return rho ** 2 * np.exp(hyp[1]) + np.exp(hyp[4])
+
+
+def prior_mean(hyp):
+    hyp = np.asarray(hyp, dtype=np.float64)
+    if hyp.shape[0] == 4:
+        return np.exp(hyp[0])
+    return _mf_parts(hyp)[4]
+
+
+# ---------------------------------------------------------------------------
+# Tolerance policy (BASELINE.json north_star "1e-6 rel fp64")
+# ---------------------------------------------------------------------------
+
+def parity_errors(mu, var, mu_ref, var_ref, kss):
+    """Return (mu_rel, var_floored_rel).
+
+    mu:  max |d| / |ref|.
+    var: max |d| / max(|ref|, 1e-6 * k**) -- posterior variance next to data is
+         ~1e-9 against a prior of ~0.06, i.e. pure catastrophic cancellation in
+         k** - sum(V^2); the reference's own rounding is larger than 1e-6 * 1e-9
+         there, so the relative bound is floored at 1e-6 * k**.
+    """
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    var = np.asarray(var, dtype=np.float64).reshape(-1)
+    mu_ref = np.asarray(mu_ref, dtype=np.float64).reshape(-1)
+    var_ref = np.asarray(var_ref, dtype=np.float64).reshape(-1)
+    mu_err = np.max(np.abs(mu - mu_ref) / np.maximum(np.abs(mu_ref), 1e-300)) if mu.size else 0.0
+    den = np.maximum(np.abs(var_ref), 1e-6 * kss)
+    var_err = np.max(np.abs(var - var_ref) / den) if var.size else 0.0
+    return float(mu_err), float(var_err)
+
+
+PARITY_TOL = 1e-6

@@ -1,0 +1,160 @@
+"""Generate the golden fixtures under tests/golden/ -- BUILD CONTAINER ONLY.
+
+Two kinds of fixtures, both plain data (.npz, no pickles):
+
+1. ``atc_reference.npz``: outputs of the reference's OWN ``gaussian_process.py``
+   (``/root/reference``, imported here with a pass-through ``autograd`` shim:
+   ``autograd.numpy`` is NumPy for non-traced calls, gp:16-17; ``value_and_grad``
+   is only used by ``train``, gp:117/397, which is never called) on the
+   ``anti_two_corners`` data (``Data/anti_two_corners_*``): SF and MF, the native
+   51x51 grid and a 32x32 grid, N in {0, 9, 50, 130, 260}, plus append sequences
+   (``updt`` / ``updt_hifi`` in chunks of 4, and an empty append).
+   Stored: inputs (hyp, training data, grids) and ``mu``, ``diag(cov)``,
+   ``amax(cov)``.
+
+2. ``replay_*.npz``: the reference's own logged runs (``Data/<run>_sample.csv``
+   and ``Data/<run>_agent.csv``), reduced to what the GP path determines: the
+   sample sequence per iteration and the per-iteration max of the logged
+   ``VarMax`` (max posterior variance per Voronoi cell, simulator.py:286-323; the
+   max over cells is the max over the grid) plus ``Var0`` (simulator.py:841-842).
+   No reference code is involved in (2): it is a CSV extraction.
+
+Run: ``python tests/golden/make_golden.py`` (needs /root/reference; the GPU box
+never runs this -- it only reads the committed .npz files).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import pandas as pd
+
+REF = "/root/reference"
+DATA = os.path.join(REF, "Data")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference():
+    shim = types.ModuleType("autograd")
+    shim.numpy = np
+    shim.value_and_grad = None
+    sys.modules.setdefault("autograd", shim)
+    sys.modules.setdefault("autograd.numpy", np)
+    sys.path.insert(0, REF)
+    import gaussian_process as gp  # noqa: E402  (the reference module)
+    return gp
+
+
+def _csv(name):
+    return pd.read_csv(os.path.join(DATA, name)).values.astype(np.float64)
+
+
+def grid32():
+    g = np.linspace(0.0, 1.0, 32)
+    # x-outer row-major order, distribution.py:86-88
+    return np.array([(a, b) for a in g for b in g], dtype=np.float64)
+
+
+def make_reference_fixture(gp):
+    hyp_sf = _csv("anti_two_corners_sf_hyp.csv")[0]
+    hyp_mf = _csv("anti_two_corners_mf_hyp.csv")[0]
+    truth = _csv("anti_two_corners_hifi.csv")
+    train = _csv("anti_two_corners_hifi_train.csv")
+    prior = _csv("anti_two_corners_prior.csv")
+    grids = {"g51": truth[:, :2].copy(), "g32": grid32()}
+    out = {"hyp_sf": hyp_sf, "hyp_mf": hyp_mf, "train": train, "prior": prior,
+           "grid_g51": grids["g51"], "grid_g32": grids["g32"]}
+    e2, e1 = np.empty((0, 2)), np.empty((0, 1))
+
+    def pred(model, gname):
+        mu, cov = model.predict(grids[gname])
+        return mu[:, 0].copy(), np.diag(cov).copy(), float(np.amax(cov))
+
+    for gname in grids:
+        for N in (0, 9, 50, 130, 260):
+            X, y = train[:N, :2].copy(), train[:N, 2:3].copy()
+            # SF: SFGP(X, y, len) then .hyp = ... then updt_info (simulator.py:78-102, 676-678)
+            m = gp.SFGP(X, y, 1)
+            m.hyp = hyp_sf.copy()
+            if N > 0:
+                m.updt_info(m.X, m.y)
+            mu, var, vmax = pred(m, gname)
+            key = f"sf_{gname}_n{N}"
+            out[key + "_mu"], out[key + "_var"], out[key + "_amax"] = mu, var, np.array(vmax)
+            # MF: lofi = prior (simulator.py:59-63), hifi = first N training rows
+            m = gp.MFGP(prior[:, :2].copy(), prior[:, 2:3].copy(), X, y, 1, 1)
+            m.hyp = hyp_mf.copy()
+            m.updt_info(m.X_L, m.y_L, m.X_H, m.y_H)
+            mu, var, vmax = pred(m, gname)
+            key = f"mf_{gname}_n{N}"
+            out[key + "_mu"], out[key + "_var"], out[key + "_amax"] = mu, var, np.array(vmax)
+        # fully empty MF (null prior): the Var0 path (simulator.py:829-842)
+        m = gp.MFGP(e2.copy(), e1.copy(), e2.copy(), e1.copy(), 1, 1)
+        m.hyp = hyp_mf.copy()
+        mu, var, vmax = pred(m, gname)
+        key = f"mfempty_{gname}"
+        out[key + "_mu"], out[key + "_var"], out[key + "_amax"] = mu, var, np.array(vmax)
+
+    # append sequences on the native grid: updt / updt_hifi (gp:257-268, 531-542)
+    chunks = [4, 4, 0, 4, 4, 1]
+    sf = gp.SFGP(prior[:, :2].copy(), prior[:, 2:3].copy(), 1)
+    sf.hyp = hyp_sf.copy()
+    sf.updt_info(sf.X, sf.y)
+    mf = gp.MFGP(prior[:, :2].copy(), prior[:, 2:3].copy(), e2.copy(), e1.copy(), 1, 1)
+    mf.hyp = hyp_mf.copy()
+    mf.updt_info(mf.X_L, mf.y_L, mf.X_H, mf.y_H)
+    pos = 0
+    for s, k in enumerate(chunks):
+        xa, ya = train[pos:pos + k, :2].copy(), train[pos:pos + k, 2:3].copy()
+        pos += k
+        sf.updt(xa, ya)
+        mf.updt_hifi(xa, ya)
+        for name, model in (("sfseq", sf), ("mfseq", mf)):
+            mu, var, vmax = pred(model, "g51")
+            key = f"{name}_s{s}"
+            out[key + "_mu"], out[key + "_var"], out[key + "_amax"] = mu, var, np.array(vmax)
+    out["seq_chunks"] = np.array(chunks, dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, "atc_reference.npz"), **out)
+    print("wrote atc_reference.npz with", len(out), "arrays")
+
+
+# run name -> (truth/grid data prefix, hyp file, prior file or None)
+REPLAYS = {
+    "atc24_todescato_nsf": ("anti_two_corners", "anti_two_corners_sf_hyp.csv", None, (0, 1)),
+    "atc24_todescato_hsf": ("anti_two_corners", "anti_two_corners_sf_hyp.csv", "anti_two_corners_prior.csv", (0, 1)),
+    "atc24_todescato_hmf": ("anti_two_corners", "anti_two_corners_mf_hyp.csv", "anti_two_corners_prior.csv", (0, 1)),
+    "atc24_choi_hmf": ("anti_two_corners", "anti_two_corners_mf_hyp.csv", "anti_two_corners_prior.csv", (0,)),
+    "atc248_todescato_hmf": ("anti_two_corners", "anti_two_corners_mf_hyp.csv", "anti_two_corners_prior.csv", (3,)),
+    "australia6_todescato_nsf": ("australia6", "australia6_sf_hyp.csv", None, (0,)),
+    "australia6_todescato_hmf": ("australia6", "australia6_mf_hyp.csv", "australia6_prior.csv", (0,)),
+}
+
+
+def make_replay_fixtures():
+    for run, (data, hypf, priorf, sims) in REPLAYS.items():
+        agent = pd.read_csv(os.path.join(DATA, run + "_agent.csv"))
+        sample = pd.read_csv(os.path.join(DATA, run + "_sample.csv"))
+        out = {"hyp": _csv(hypf)[0], "grid": _csv(data + "_hifi.csv")[:, :2].copy(),
+               "sims": np.array(sims, dtype=np.int64)}
+        if priorf is not None:
+            out["prior"] = _csv(priorf)
+        for sim in sims:
+            a = agent[agent.SimNum == sim]
+            s = sample[sample.SimNum == sim]
+            its = np.sort(a.Iteration.unique())
+            out[f"s{sim}_iters"] = its.astype(np.int64)
+            out[f"s{sim}_varmax"] = a.groupby("Iteration").VarMax.max().loc[its].values.astype(np.float64)
+            out[f"s{sim}_var0"] = np.array(a.Var0.iloc[0], dtype=np.float64)
+            out[f"s{sim}_sample_iter"] = s.Iteration.values.astype(np.int64)
+            out[f"s{sim}_sample_xy"] = s[["X", "Y"]].values.astype(np.float64)
+            out[f"s{sim}_sample_y"] = s.Sample.values.astype(np.float64)
+        np.savez_compressed(os.path.join(OUT, f"replay_{run}.npz"), **out)
+        print("wrote replay", run)
+
+
+if __name__ == "__main__":
+    gp = _import_reference()
+    make_reference_fixture(gp)
+    make_replay_fixtures()

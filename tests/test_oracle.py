@@ -1,0 +1,116 @@
+"""Pin the CPU oracle (oracle/gp_oracle.py) against the reference (no GPU).
+
+* golden vectors produced by the reference's own gaussian_process.py
+  (tests/golden/make_golden.py, anti_two_corners, SF + MF, 51x51 and 32x32);
+* the reference's own logged runs (Data/*_agent.csv VarMax, Var0);
+* closed forms (empty GP, single observation).
+"""
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as O
+from tests import _fixtures as F
+
+
+@pytest.fixture(scope="module")
+def atc():
+    return F.atc()
+
+
+@pytest.mark.parametrize("grid", F.GRIDS)
+@pytest.mark.parametrize("N", F.NS)
+def test_sf_oracle_vs_reference(atc, grid, N):
+    X, y = atc["train"][:N, :2], atc["train"][:N, 2]
+    Xs = atc[f"grid_{grid}"]
+    key = f"sf_{grid}_n{N}"
+    mu_f, var_f = O.sf_faithful(X, y, atc["hyp_sf"], Xs)
+    np.testing.assert_allclose(mu_f, atc[key + "_mu"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(var_f, atc[key + "_var"], rtol=1e-10, atol=1e-20)
+    mu_d, var_d = O.sf_diag(X, y, atc["hyp_sf"], Xs)
+    e_mu, e_var = O.parity_errors(mu_d, var_d, atc[key + "_mu"], atc[key + "_var"], O.prior_variance(atc["hyp_sf"]))
+    assert e_mu < O.PARITY_TOL and e_var < O.PARITY_TOL, (e_mu, e_var)
+
+
+@pytest.mark.parametrize("grid", F.GRIDS)
+@pytest.mark.parametrize("N", F.NS)
+def test_mf_oracle_vs_reference(atc, grid, N):
+    P = atc["prior"]
+    X, y = atc["train"][:N, :2], atc["train"][:N, 2]
+    Xs = atc[f"grid_{grid}"]
+    key = f"mf_{grid}_n{N}"
+    mu_f, var_f = O.mf_faithful(P[:, :2], P[:, 2], X, y, atc["hyp_mf"], Xs)
+    np.testing.assert_allclose(mu_f, atc[key + "_mu"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(var_f, atc[key + "_var"], rtol=1e-10, atol=1e-20)
+    mu_d, var_d = O.mf_diag(P[:, :2], P[:, 2], X, y, atc["hyp_mf"], Xs)
+    e_mu, e_var = O.parity_errors(mu_d, var_d, atc[key + "_mu"], atc[key + "_var"], O.prior_variance(atc["hyp_mf"]))
+    assert e_mu < O.PARITY_TOL and e_var < O.PARITY_TOL, (e_mu, e_var)
+
+
+@pytest.mark.parametrize("grid", F.GRIDS)
+def test_empty_gp_closed_form(atc, grid):
+    Xs = atc[f"grid_{grid}"]
+    e = np.empty((0, 2))
+    for hyp, key in ((atc["hyp_sf"], f"sf_{grid}_n0"), (atc["hyp_mf"], f"mfempty_{grid}")):
+        mu, var = (O.sf_diag(e, e[:, 0], hyp, Xs) if hyp.shape[0] == 4
+                   else O.mf_diag(e, e[:, 0], e, e[:, 0], hyp, Xs))
+        assert np.all(mu == O.prior_mean(hyp)) and np.all(var == O.prior_variance(hyp))
+        np.testing.assert_allclose(mu, atc[key + "_mu"], rtol=1e-15)
+        np.testing.assert_allclose(var, atc[key + "_var"], rtol=1e-15)
+
+
+def test_single_observation_closed_form(atc):
+    hyp = atc["hyp_sf"]
+    x0 = np.array([[0.3, 0.7]])
+    s = np.exp(hyp[1])
+    _, var = O.sf_diag(x0, np.array([0.5]), hyp, x0)
+    expect = s - s * s / (s + np.exp(hyp[3]) + O.JITTER)
+    np.testing.assert_allclose(var[0], expect, rtol=1e-6)
+
+
+def test_append_sequence_oracle(atc):
+    P, T = atc["prior"], atc["train"]
+    Xs = atc["grid_g51"]
+    pos = 0
+    for s, k in enumerate(atc["seq_chunks"]):
+        pos += int(k)
+        X = np.vstack([P[:, :2], T[:pos, :2]])
+        y = np.concatenate([P[:, 2], T[:pos, 2]])
+        mu, var = O.sf_diag(X, y, atc["hyp_sf"], Xs)
+        e = O.parity_errors(mu, var, atc[f"sfseq_s{s}_mu"], atc[f"sfseq_s{s}_var"], O.prior_variance(atc["hyp_sf"]))
+        assert max(e) < O.PARITY_TOL, e
+        mu, var = O.mf_diag(P[:, :2], P[:, 2], T[:pos, :2], T[:pos, 2], atc["hyp_mf"], Xs)
+        e = O.parity_errors(mu, var, atc[f"mfseq_s{s}_mu"], atc[f"mfseq_s{s}_var"], O.prior_variance(atc["hyp_mf"]))
+        assert max(e) < O.PARITY_TOL, e
+
+
+class _OracleModel:
+    def __init__(self, hyp, prior, grid):
+        self.hyp, self.grid = hyp, grid
+        self.mf = hyp.shape[0] == 9
+        e = np.empty((0, 2))
+        self.XL = prior[:, :2] if (prior is not None and self.mf) else e
+        self.yL = prior[:, 2] if (prior is not None and self.mf) else np.empty(0)
+        self.X = prior[:, :2] if (prior is not None and not self.mf) else e
+        self.y = prior[:, 2] if (prior is not None and not self.mf) else np.empty(0)
+
+    def append(self, X, y):
+        self.X = np.vstack([self.X, X])
+        self.y = np.concatenate([self.y, y.reshape(-1)])
+
+    def var(self):
+        if self.mf:
+            return O.mf_diag(self.XL, self.yL, self.X, self.y, self.hyp, self.grid)[1]
+        return O.sf_diag(self.X, self.y, self.hyp, self.grid)[1]
+
+
+@pytest.mark.parametrize("run", F.REPLAY_RUNS)
+def test_oracle_replays_logged_runs(run):
+    fx = F.replay(run)
+    for sim in fx["sims"]:
+        np.testing.assert_allclose(O.prior_variance(fx["hyp"]), fx[f"s{sim}_var0"], rtol=1e-13)
+        logged, got = F.replay_run(
+            fx, sim,
+            make_model=lambda hyp, prior: _OracleModel(hyp, prior, fx["grid"]),
+            append=lambda m, X, y: m.append(X, y),
+            predict_var=lambda m: m.var())
+        np.testing.assert_allclose(got, logged, rtol=1e-9)
