@@ -1,0 +1,114 @@
+/*
+ * mfgp_hip.h -- C ABI of the MI355X GP posterior engine (libmfgp_hip.so).
+ *
+ * Drop-in boundary for the hot path of MSU-dcypherlab/mfgp-coverage: the
+ * reference has no FFI layer, its boundary is the Python class API of
+ * gaussian_process.py (imported at simulator.py:25). Each entry point below
+ * replaces one reference method; the Python mirror
+ * (mfgp_coverage_amd/gaussian_process.py) binds them with ctypes
+ * (see INTEGRATION.md).
+ *
+ * Conventions
+ *   - plain pointers and sizes; no torch / HIP types in the signatures
+ *     (streams are passed as void*, i.e. a hipStream_t).
+ *   - coordinates are row-major [n,2] float64, values [n] float64.
+ *   - every data pointer may be host or device memory (detected with
+ *     hipPointerGetAttributes); inputs are borrowed for the call and copied,
+ *     outputs are written into caller buffers.
+ *   - return 0 on success, else an MFGP_ERR_* code; mfgp_last_error() gives a
+ *     thread-local message.
+ */
+#ifndef MFGP_HIP_H
+#define MFGP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MFGP_OK 0
+#define MFGP_ERR_NOT_PD 1   /* Cholesky pivot <= 0: numpy.linalg.LinAlgError (gp:254, gp:529) */
+#define MFGP_ERR_ARG 2      /* bad argument: TypeError/ValueError (simulator.py:366, 652)     */
+#define MFGP_ERR_DEVICE 3   /* HIP runtime error: RuntimeError                                */
+
+#define MFGP_SF 0           /* SFGP, gaussian_process.py:23-268, hyp [mu, s2, L, noise]              */
+#define MFGP_MF 1           /* MFGP, gaussian_process.py:271-578, hyp [mu_lo,s2_lo,L_lo,mu_hi,s2_hi,
+                               L_hi,rho,noise_lo,noise_hi] (all log-scaled, simulator.py:53-56)     */
+#define MFGP_F64 0
+#define MFGP_F32 1          /* reserved (config 5); not accepted yet */
+
+#define MFGP_ASYNC 1        /* batch flag: do not synchronise; status via mfgp_ctx_synchronize */
+
+typedef struct mfgp_ctx mfgp_ctx;
+typedef struct mfgp_model mfgp_model;
+
+/* One context per host thread: owns a HIP stream and a scratch workspace. */
+int mfgp_ctx_create(int device, mfgp_ctx** out);
+void mfgp_ctx_destroy(mfgp_ctx* ctx);
+/* Launch on a caller stream (hipStream_t) instead of the context's own. NULL restores it. */
+int mfgp_ctx_set_stream(mfgp_ctx* ctx, void* hip_stream);
+void* mfgp_ctx_get_stream(mfgp_ctx* ctx);
+/* Wait for all work; returns MFGP_ERR_NOT_PD if an ASYNC batch hit a non-PD factor. */
+int mfgp_ctx_synchronize(mfgp_ctx* ctx);
+/* Kernel timing (HIP events around every launch of the fused predict kernel). */
+int mfgp_ctx_enable_timing(mfgp_ctx* ctx, int enable);
+/* Sum of predict-kernel durations (ms) and launch count since the last reset;
+ * also the same for the factor stage (assemble + blocked Cholesky). */
+int mfgp_ctx_get_timing(mfgp_ctx* ctx, double* predict_ms, int64_t* predict_launches,
+                        double* factor_ms, int64_t* factor_calls);
+int mfgp_ctx_reset_timing(mfgp_ctx* ctx);
+
+/* SFGP.__init__ (gp:28-64) / MFGP.__init__ (gp:276-327) with the caller's
+ * hyperparameters (the simulator overwrites .hyp right after construction,
+ * simulator.py:72-73, 99-100). nhyp = 4 (SF) or 9 (MF). jitter = 1e-8 in the
+ * reference (gp:42, gp:298). */
+int mfgp_model_create(mfgp_ctx* ctx, int kind, int dtype, const double* hyp, int nhyp,
+                      double jitter, mfgp_model** out);
+void mfgp_model_destroy(mfgp_model* m);
+/* copy.deepcopy(model) (simulator.py:339). */
+int mfgp_clone(const mfgp_model* src, mfgp_model** out);
+/* Writes to .hyp / .jitter; they take effect at the next factorisation. */
+int mfgp_model_set_hyp(mfgp_model* m, const double* hyp, int nhyp, double jitter);
+
+/* The grid X* of predict(X_star) (gp:121 / gp:401), [M,2]. Cached on the device. */
+int mfgp_set_grid(mfgp_model* m, const double* xstar, int64_t M);
+
+/* updt_info (gp:229-255 / gp:493-529): replace the training set and refactor.
+ * SF uses only the H slots (XL/yL must be NULL/0). Returns MFGP_ERR_NOT_PD like
+ * np.linalg.cholesky raising LinAlgError. */
+int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL,
+                  const double* XH, const double* yH, int64_t NH);
+
+/* updt (gp:257-268) / updt_hifi (gp:531-542): append k >= 0 rows and refactor. */
+int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k);
+
+/* predict (gp:121-148 / gp:401-438): posterior mean and the diagonal of the
+ * posterior covariance at every grid cell (the only part the callers use,
+ * simulator.py:301, 341, 672, 685, 842, 855, 1014). mu, var: [M]. */
+int mfgp_predict(mfgp_model* m, double* mu, double* var);
+
+/* Sizes and state readers (the Python mirror's .X/.L attributes). */
+int64_t mfgp_model_n(const mfgp_model* m);      /* N = NL + NH */
+int64_t mfgp_model_nl(const mfgp_model* m);
+int64_t mfgp_model_m(const mfgp_model* m);
+/* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
+int mfgp_get_factor(mfgp_model* m, double* L_out);
+
+/* Batched update + predict over `count` independent GPs (Monte-Carlo seeds):
+ * for model i append k[i] rows (rows of X/y, concatenated in model order),
+ * refactor, and predict into mu + i*M_i, var + i*M_i (concatenated in model
+ * order). One set of launches serves the whole batch. flags: MFGP_ASYNC. */
+int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y,
+                              const int64_t* k, double* mu, double* var, int flags);
+/* Drop the last `k` hifi rows of each model without refactoring (benchmark reset). */
+int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi);
+
+const char* mfgp_last_error(void);
+const char* mfgp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MFGP_HIP_H */

@@ -1,0 +1,232 @@
+"""ctypes binding of libmfgp_hip.so (C ABI declared in include/mfgp_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU
+is visible, every entry point raises instead of computing on the host.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmfgp_hip.so")
+
+OK, ERR_NOT_PD, ERR_ARG, ERR_DEVICE = 0, 1, 2, 3
+SF, MF = 0, 1
+F64, F32 = 0, 1
+ASYNC = 1
+
+_c_double_p = ctypes.POINTER(ctypes.c_double)
+_c_int64_p = ctypes.POINTER(ctypes.c_int64)
+
+# name -> (restype, argtypes); every symbol declared in include/mfgp_hip.h
+SIGNATURES = {
+    "mfgp_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "mfgp_ctx_destroy": (None, [ctypes.c_void_p]),
+    "mfgp_ctx_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "mfgp_ctx_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "mfgp_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mfgp_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int64_p, _c_double_p, _c_int64_p]),
+    "mfgp_ctx_reset_timing": (ctypes.c_int, [ctypes.c_void_p]),
+    "mfgp_model_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
+    "mfgp_model_destroy": (None, [ctypes.c_void_p]),
+    "mfgp_clone": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "mfgp_model_set_hyp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]),
+    "mfgp_set_grid": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "mfgp_set_data": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "mfgp_append": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "mfgp_predict": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mfgp_model_n": (ctypes.c_int64, [ctypes.c_void_p]),
+    "mfgp_model_nl": (ctypes.c_int64, [ctypes.c_void_p]),
+    "mfgp_model_m": (ctypes.c_int64, [ctypes.c_void_p]),
+    "mfgp_get_factor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "mfgp_batch_append_predict": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p,
+                                                 ctypes.c_void_p, _c_int64_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_int]),
+    "mfgp_truncate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "mfgp_last_error": (ctypes.c_char_p, []),
+    "mfgp_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib():
+    """Load libmfgp_hip.so (once). Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+            h = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                f = getattr(h, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = h
+    return _lib
+
+
+def check(rc):
+    if rc == OK:
+        return
+    msg = lib().mfgp_last_error().decode(errors="replace")
+    if rc == ERR_NOT_PD:
+        raise np.linalg.LinAlgError(msg)
+    if rc == ERR_ARG:
+        if "Hyperparameters must be" in msg:
+            raise TypeError(msg)
+        raise ValueError(msg)
+    raise RuntimeError(f"libmfgp_hip: {msg}")
+
+
+def ptr(a):
+    """Host pointer of a C-contiguous float64 ndarray (None for empty)."""
+    if a is None or a.size == 0:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One HIP stream + workspace (mfgp_ctx)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(lib().mfgp_ctx_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.mfgp_ctx_destroy(h)
+            self.handle = None
+
+    def synchronize(self):
+        check(lib().mfgp_ctx_synchronize(self.handle))
+
+    def set_stream(self, stream_ptr):
+        check(lib().mfgp_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
+
+    def enable_timing(self, on=True):
+        check(lib().mfgp_ctx_enable_timing(self.handle, 1 if on else 0))
+
+    def reset_timing(self):
+        check(lib().mfgp_ctx_reset_timing(self.handle))
+
+    def timing(self):
+        pm, fm = ctypes.c_double(), ctypes.c_double()
+        pn, fn = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().mfgp_ctx_get_timing(self.handle, ctypes.byref(pm), ctypes.byref(pn),
+                                        ctypes.byref(fm), ctypes.byref(fn)))
+        return {"predict_ms": pm.value, "predict_launches": pn.value,
+                "factor_ms": fm.value, "factor_calls": fn.value}
+
+
+_tls = threading.local()
+_default_device = int(os.environ.get("MFGP_DEVICE", "0"))
+
+
+def set_device(device):
+    """Device used by models created afterwards in this process (one process per GPU)."""
+    global _default_device
+    _default_device = int(device)
+
+
+def context(device=None):
+    """The calling thread's context for `device` (one stream per host thread)."""
+    dev = _default_device if device is None else int(device)
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    if dev not in ctxs:
+        ctxs[dev] = Context(dev)
+    return ctxs[dev]
+
+
+class Model:
+    """Owning handle of one device-resident GP (mfgp_model)."""
+
+    def __init__(self, ctx, kind, hyp, jitter, handle=None):
+        self.ctx = ctx
+        self.kind = kind
+        if handle is None:
+            hyp = np.ascontiguousarray(hyp, dtype=np.float64)
+            h = ctypes.c_void_p()
+            check(lib().mfgp_model_create(ctx.handle, kind, F64, ptr(hyp), int(hyp.shape[0]),
+                                          float(jitter), ctypes.byref(h)))
+            handle = h
+        self.handle = handle
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.mfgp_model_destroy(h)
+            self.handle = None
+
+    def clone(self):
+        h = ctypes.c_void_p()
+        check(lib().mfgp_clone(self.handle, ctypes.byref(h)))
+        return Model(self.ctx, self.kind, None, None, handle=h)
+
+    def set_hyp(self, hyp, jitter):
+        hyp = np.ascontiguousarray(hyp, dtype=np.float64).reshape(-1)
+        check(lib().mfgp_model_set_hyp(self.handle, ptr(hyp), int(hyp.shape[0]), float(jitter)))
+
+    def set_grid(self, xs):
+        xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1, 2)
+        check(lib().mfgp_set_grid(self.handle, ptr(xs), xs.shape[0]))
+
+    def set_data(self, XL, yL, XH, yH):
+        XL, yL, XH, yH = (np.ascontiguousarray(a, dtype=np.float64) for a in (XL, yL, XH, yH))
+        check(lib().mfgp_set_data(self.handle, ptr(XL), ptr(yL), XL.size // 2, ptr(XH), ptr(yH), XH.size // 2))
+
+    def append(self, X, y):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        check(lib().mfgp_append(self.handle, ptr(X), ptr(y), X.size // 2))
+
+    def predict(self):
+        M = lib().mfgp_model_m(self.handle)
+        mu = np.empty(M, dtype=np.float64)
+        var = np.empty(M, dtype=np.float64)
+        check(lib().mfgp_predict(self.handle, ptr(mu) if M else None, ptr(var) if M else None))
+        return mu, var
+
+    def factor(self):
+        n = lib().mfgp_model_n(self.handle)
+        L = np.zeros((n, n), dtype=np.float64)
+        if n:
+            check(lib().mfgp_get_factor(self.handle, ptr(L)))
+        return L
+
+    @property
+    def n(self):
+        return lib().mfgp_model_n(self.handle)
+
+    def truncate(self, n_keep_hifi):
+        check(lib().mfgp_truncate(self.handle, int(n_keep_hifi)))
+
+
+def batch_append_predict(models, X, y, k, mu_ptr, var_ptr, asynchronous=False):
+    """Batched update+predict over device-resident models.
+
+    X, y: integer device (or host) addresses of the concatenated new rows;
+    k: per-model row counts; mu_ptr/var_ptr: device addresses of [sum M] outputs.
+    """
+    n = len(models)
+    arr = (ctypes.c_void_p * n)(*[m.handle.value for m in models])
+    ks = (ctypes.c_int64 * n)(*[int(v) for v in k])
+    rc = lib().mfgp_batch_append_predict(arr, n, ctypes.c_void_p(X), ctypes.c_void_p(y), ks,
+                                         ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
+                                         ASYNC if asynchronous else 0)
+    check(rc)

@@ -1,0 +1,704 @@
+// C ABI of libmfgp_hip.so (declared in include/mfgp_hip.h).
+//
+// Host-side state management for the GP posterior engine: contexts (one HIP
+// stream + workspace each), models (device-resident training set, factor and
+// grid), the batched update+predict driver, timing and error reporting.
+// Mirrors the reference methods cited in include/mfgp_hip.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mfgp_hip.h"
+#include "mfgp_internal.h"
+
+using namespace mfgp;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) return set_err(MFGP_ERR_DEVICE, "%s: %s (%s:%d)", #expr,         \
+                                         hipGetErrorString(e_), __FILE__, __LINE__);       \
+  } while (0)
+
+constexpr int RING = 64;       // descriptor upload slots
+constexpr int MAXB = 256;      // GPs per launch
+
+struct EvPair {
+  hipEvent_t a, b;
+  int kind;  // 0 predict, 1 factor
+};
+
+}  // namespace
+
+struct mfgp_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  // descriptor ring
+  GPDesc* h_ring = nullptr;  // pinned [RING][MAXB]
+  GPDesc* d_ring = nullptr;  // device [RING][MAXB]
+  hipEvent_t ring_ev[RING];
+  bool ring_used[RING];
+  int ring_pos = 0;
+  // workspace (V scratch + device outputs for host-pointer calls)
+  double* ws = nullptr;
+  size_t ws_bytes = 0;
+  // timing
+  bool timing = false;
+  std::vector<EvPair> pending;
+  std::vector<hipEvent_t> pool;
+  double t_predict = 0.0, t_factor = 0.0;
+  int64_t n_predict = 0, n_factor = 0;
+  // deferred status words of ASYNC batches
+  std::vector<int*> async_status;
+};
+
+struct mfgp_model {
+  mfgp_ctx* ctx = nullptr;
+  int kind = MFGP_SF;
+  int nhyp = 4;
+  double hyp[9] = {0};
+  double jitter = 1e-8;
+  // training set (device)
+  int64_t NL = 0, NH = 0, cap = 0;
+  double* X = nullptr;  // [cap,2]
+  double* y = nullptr;  // [cap]
+  // factor (device)
+  int64_t ld = 0;
+  double* A = nullptr;     // [ld,ld]
+  double* Linv = nullptr;  // [ld/NB][TILE]
+  int* status = nullptr;
+  bool factored = false;
+  int64_t factor_N = -1;
+  double factor_hyp[9] = {0};
+  double factor_jitter = 0.0;
+  // grid (device)
+  int64_t M = 0, Mcap = 0;
+  double* grid = nullptr;
+};
+
+namespace {
+
+Hyp derive_hyp(int kind, const double* hyp, double jitter) {
+  Hyp h{};
+  h.kind = kind;
+  h.jitter = jitter;
+  if (kind == MFGP_SF) {
+    // [mu, s^2, L, noise]  (gp:75-76, gp:132, gp:248-249)
+    h.sL = std::exp(hyp[1]);
+    h.lL = std::exp(hyp[2]);
+    h.sH = h.sL;
+    h.lH = h.lL;
+    h.rho = 1.0;
+    h.rho2 = 1.0;
+    h.noiseL = h.noiseH = std::exp(hyp[3]);
+    h.meanL = h.meanH = std::exp(hyp[0]);
+    h.kss = h.sL;  // kernel(X*,X*) diagonal = s * exp(0)
+  } else {
+    // [mu_lo, s^2_lo, L_lo, mu_hi, s^2_hi, L_hi, rho, noise_lo, noise_hi]  (gp:510-514, 414-416)
+    h.sL = std::exp(hyp[1]);
+    h.lL = std::exp(hyp[2]);
+    h.sH = std::exp(hyp[4]);
+    h.lH = std::exp(hyp[5]);
+    h.rho = std::exp(hyp[6]);
+    h.rho2 = h.rho * h.rho;
+    h.noiseL = std::exp(hyp[7]);
+    h.noiseH = std::exp(hyp[8]);
+    h.meanL = std::exp(hyp[0]);
+    h.meanH = h.rho * h.meanL + std::exp(hyp[3]);
+    h.kss = h.rho2 * h.sL + h.sH;  // gp:435-436 diagonal
+  }
+  return h;
+}
+
+int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+hipEvent_t ev_get(mfgp_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+int ev_begin(mfgp_ctx* c, EvPair& p, int kind) {
+  if (!c->timing) return MFGP_OK;
+  p.a = ev_get(c);
+  p.b = ev_get(c);
+  p.kind = kind;
+  HIP_TRY(hipEventRecord(p.a, c->stream));
+  return MFGP_OK;
+}
+
+int ev_end(mfgp_ctx* c, EvPair& p) {
+  if (!c->timing) return MFGP_OK;
+  HIP_TRY(hipEventRecord(p.b, c->stream));
+  c->pending.push_back(p);
+  return MFGP_OK;
+}
+
+int drain_timing(mfgp_ctx* c) {
+  for (auto& p : c->pending) {
+    HIP_TRY(hipEventSynchronize(p.b));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
+    if (p.kind == 0) {
+      c->t_predict += ms;
+      c->n_predict += 1;
+    } else {
+      c->t_factor += ms;
+      c->n_factor += 1;
+    }
+    c->pool.push_back(p.a);
+    c->pool.push_back(p.b);
+  }
+  c->pending.clear();
+  return MFGP_OK;
+}
+
+int ensure_ws(mfgp_ctx* c, size_t bytes) {
+  if (bytes <= c->ws_bytes) return MFGP_OK;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->ws) HIP_TRY(hipFree(c->ws));
+  c->ws = nullptr;
+  c->ws_bytes = 0;
+  size_t want = std::max(bytes, c->ws_bytes + c->ws_bytes / 2);
+  HIP_TRY(hipMalloc(&c->ws, want));
+  c->ws_bytes = want;
+  return MFGP_OK;
+}
+
+// Grow the training capacity of m to hold `need` rows (keeps X/y contents).
+int ensure_cap(mfgp_model* m, int64_t need) {
+  if (need <= m->cap && m->A) return MFGP_OK;
+  mfgp_ctx* c = m->ctx;
+  int64_t cap = std::max<int64_t>({need, m->cap + m->cap / 2, 63});
+  int64_t ld = round_up(cap + 1, NB);
+  cap = ld - 1;
+  double *X = nullptr, *y = nullptr, *A = nullptr, *Li = nullptr;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMalloc(&X, sizeof(double) * 2 * cap));
+  HIP_TRY(hipMalloc(&y, sizeof(double) * cap));
+  HIP_TRY(hipMalloc(&A, sizeof(double) * ld * ld));
+  HIP_TRY(hipMalloc(&Li, sizeof(double) * (ld / NB) * TILE));
+  const int64_t n = m->NL + m->NH;
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(X, m->X, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(y, m->y, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (m->X) HIP_TRY(hipFree(m->X));
+  if (m->y) HIP_TRY(hipFree(m->y));
+  if (m->A) HIP_TRY(hipFree(m->A));
+  if (m->Linv) HIP_TRY(hipFree(m->Linv));
+  m->X = X;
+  m->y = y;
+  m->A = A;
+  m->Linv = Li;
+  m->cap = cap;
+  m->ld = ld;
+  m->factored = false;
+  return MFGP_OK;
+}
+
+int check_model(const mfgp_model* m) {
+  if (!m || !m->ctx) return set_err(MFGP_ERR_ARG, "null model");
+  return MFGP_OK;
+}
+
+GPDesc* acquire_slot(mfgp_ctx* c, int& slot, int& rc) {
+  slot = c->ring_pos;
+  c->ring_pos = (c->ring_pos + 1) % RING;
+  rc = MFGP_OK;
+  if (c->ring_used[slot]) {
+    hipError_t e = hipEventSynchronize(c->ring_ev[slot]);
+    if (e != hipSuccess) {
+      rc = set_err(MFGP_ERR_DEVICE, "hipEventSynchronize: %s", hipGetErrorString(e));
+      return nullptr;
+    }
+  }
+  return c->h_ring + (size_t)slot * MAXB;
+}
+
+int upload_slot(mfgp_ctx* c, int slot, int count, const GPDesc** dptr) {
+  HIP_TRY(hipMemcpyAsync(c->d_ring + (size_t)slot * MAXB, c->h_ring + (size_t)slot * MAXB,
+                         sizeof(GPDesc) * count, hipMemcpyHostToDevice, c->stream));
+  *dptr = c->d_ring + (size_t)slot * MAXB;
+  return MFGP_OK;
+}
+
+int release_slot(mfgp_ctx* c, int slot) {
+  HIP_TRY(hipEventRecord(c->ring_ev[slot], c->stream));
+  c->ring_used[slot] = true;
+  return MFGP_OK;
+}
+
+void fill_desc(GPDesc& d, mfgp_model* m) {
+  d.X = m->X;
+  d.y = m->y;
+  d.A = m->A;
+  d.Linv = m->Linv;
+  d.grid = m->grid;
+  d.V = nullptr;
+  d.mu = nullptr;
+  d.var = nullptr;
+  d.status = m->status;
+  d.ld = m->ld;
+  d.N = m->NL + m->NH;
+  d.NL = m->NL;
+  d.M = m->M;
+  d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
+  d.hp = d.hf;
+}
+
+// Enqueue assembly + blocked Cholesky for `count` models (descriptors already uploaded).
+int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
+  int64_t max_nb = 0, max_tiles = 0;
+  for (int i = 0; i < count; ++i) {
+    const int64_t nb = nblocks_factor(hd[i].N);
+    max_nb = std::max(max_nb, nb);
+    max_tiles = std::max(max_tiles, nb * (nb + 1) / 2);
+  }
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 1);
+  if (rc) return rc;
+  HIP_TRY(launch_assemble(dd, count, max_tiles, c->stream));
+  for (int kb = 0; kb < max_nb; ++kb) {
+    HIP_TRY(launch_potrf_diag(dd, count, kb, c->stream));
+    const int64_t below = max_nb - kb - 1;
+    if (below > 0) {
+      HIP_TRY(launch_panel(dd, count, kb, below, c->stream));
+      HIP_TRY(launch_syrk(dd, count, kb, below * (below + 1) / 2, c->stream));
+    }
+  }
+  return ev_end(c, ev);
+}
+
+int enqueue_predict(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
+  int64_t max_ct = 0;
+  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_grid(hd[i].M));
+  if (max_ct == 0) return MFGP_OK;
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 0);
+  if (rc) return rc;
+  HIP_TRY(launch_predict(dd, count, max_ct, c->stream));
+  return ev_end(c, ev);
+}
+
+size_t v_bytes(int64_t M, int64_t N) {
+  return sizeof(double) * (size_t)ntiles_grid(M) * (size_t)nblocks_rows(N) * TILE;
+}
+
+int read_status(mfgp_model* m) {
+  int st = INT_MAX;
+  HIP_TRY(hipMemcpy(&st, m->status, sizeof(int), hipMemcpyDeviceToHost));
+  if (st != INT_MAX)
+    return set_err(MFGP_ERR_NOT_PD, "Matrix is not positive definite (leading minor of order %d)", st);
+  return MFGP_OK;
+}
+
+// Factor one model now (synchronous, status checked).
+int factor_one(mfgp_model* m) {
+  mfgp_ctx* c = m->ctx;
+  int rc = ensure_cap(m, m->NL + m->NH);
+  if (rc) return rc;
+  int slot;
+  GPDesc* hd = acquire_slot(c, slot, rc);
+  if (!hd) return rc;
+  fill_desc(hd[0], m);
+  const GPDesc* dd = nullptr;
+  if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
+  if ((rc = enqueue_factor(c, dd, hd, 1))) return rc;
+  if ((rc = release_slot(c, slot))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  m->factor_N = m->NL + m->NH;
+  std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
+  m->factor_jitter = m->jitter;
+  rc = read_status(m);
+  m->factored = (rc == MFGP_OK);
+  return rc;
+}
+
+bool factor_current(const mfgp_model* m) {
+  return m->factored && m->factor_N == m->NL + m->NH && m->factor_jitter == m->jitter &&
+         std::memcmp(m->factor_hyp, m->hyp, sizeof(m->hyp)) == 0;
+}
+
+int copy_rows(mfgp_model* m, int64_t at, const double* X, const double* y, int64_t k) {
+  if (k <= 0) return MFGP_OK;
+  if (!X || !y) return set_err(MFGP_ERR_ARG, "null data pointer with k=%lld", (long long)k);
+  HIP_TRY(hipMemcpyAsync(m->X + 2 * at, X, sizeof(double) * 2 * k, hipMemcpyDefault, m->ctx->stream));
+  HIP_TRY(hipMemcpyAsync(m->y + at, y, sizeof(double) * k, hipMemcpyDefault, m->ctx->stream));
+  return MFGP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mfgp_last_error(void) { return g_err.c_str(); }
+const char* mfgp_version(void) { return "mfgp_hip 0.1 gfx950 f64"; }
+
+int mfgp_ctx_create(int device, mfgp_ctx** out) {
+  if (!out) return set_err(MFGP_ERR_ARG, "null out");
+  *out = nullptr;
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return set_err(MFGP_ERR_ARG, "device %d out of range (%d devices)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  mfgp_ctx* c = new mfgp_ctx();
+  c->device = device;
+  HIP_TRY(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+  c->stream = c->own;
+  HIP_TRY(hipHostMalloc(&c->h_ring, sizeof(GPDesc) * RING * MAXB, hipHostMallocDefault));
+  HIP_TRY(hipMalloc(&c->d_ring, sizeof(GPDesc) * RING * MAXB));
+  for (int i = 0; i < RING; ++i) {
+    HIP_TRY(hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming));
+    c->ring_used[i] = false;
+  }
+  *out = c;
+  return MFGP_OK;
+}
+
+void mfgp_ctx_destroy(mfgp_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  (void)drain_timing(c);
+  for (auto e : c->pool) (void)hipEventDestroy(e);
+  for (int i = 0; i < RING; ++i) (void)hipEventDestroy(c->ring_ev[i]);
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->d_ring) (void)hipFree(c->d_ring);
+  if (c->h_ring) (void)hipHostFree(c->h_ring);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+int mfgp_ctx_set_stream(mfgp_ctx* c, void* s) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->stream = s ? (hipStream_t)s : c->own;
+  return MFGP_OK;
+}
+
+void* mfgp_ctx_get_stream(mfgp_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int mfgp_ctx_synchronize(mfgp_ctx* c) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  int rc = MFGP_OK;
+  for (int* s : c->async_status) {
+    int st = INT_MAX;
+    HIP_TRY(hipMemcpy(&st, s, sizeof(int), hipMemcpyDeviceToHost));
+    if (st != INT_MAX && rc == MFGP_OK)
+      rc = set_err(MFGP_ERR_NOT_PD, "Matrix is not positive definite (leading minor of order %d)", st);
+  }
+  c->async_status.clear();
+  return rc;
+}
+
+int mfgp_ctx_enable_timing(mfgp_ctx* c, int enable) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  c->timing = enable != 0;
+  return MFGP_OK;
+}
+
+int mfgp_ctx_get_timing(mfgp_ctx* c, double* pm, int64_t* pn, double* fm, int64_t* fn) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  int rc = drain_timing(c);
+  if (rc) return rc;
+  if (pm) *pm = c->t_predict;
+  if (pn) *pn = c->n_predict;
+  if (fm) *fm = c->t_factor;
+  if (fn) *fn = c->n_factor;
+  return MFGP_OK;
+}
+
+int mfgp_ctx_reset_timing(mfgp_ctx* c) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  int rc = drain_timing(c);
+  c->t_predict = c->t_factor = 0.0;
+  c->n_predict = c->n_factor = 0;
+  return rc;
+}
+
+int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int nhyp, double jitter,
+                      mfgp_model** out) {
+  if (!c || !out) return set_err(MFGP_ERR_ARG, "null ctx/out");
+  *out = nullptr;
+  if (kind != MFGP_SF && kind != MFGP_MF) return set_err(MFGP_ERR_ARG, "kind must be MFGP_SF or MFGP_MF");
+  if (dtype != MFGP_F64) return set_err(MFGP_ERR_ARG, "only MFGP_F64 is implemented");
+  const int want = kind == MFGP_SF ? 4 : 9;
+  if (!hyp || nhyp != want)
+    return set_err(MFGP_ERR_ARG, "Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)");
+  HIP_TRY(hipSetDevice(c->device));
+  mfgp_model* m = new mfgp_model();
+  m->ctx = c;
+  m->kind = kind;
+  m->nhyp = nhyp;
+  std::memcpy(m->hyp, hyp, sizeof(double) * nhyp);
+  m->jitter = jitter;
+  HIP_TRY(hipMalloc(&m->status, sizeof(int)));
+  int rc = ensure_cap(m, 63);
+  if (rc) {
+    mfgp_model_destroy(m);
+    return rc;
+  }
+  *out = m;
+  return MFGP_OK;
+}
+
+void mfgp_model_destroy(mfgp_model* m) {
+  if (!m) return;
+  if (m->ctx) (void)hipStreamSynchronize(m->ctx->stream);
+  if (m->X) (void)hipFree(m->X);
+  if (m->y) (void)hipFree(m->y);
+  if (m->A) (void)hipFree(m->A);
+  if (m->Linv) (void)hipFree(m->Linv);
+  if (m->status) (void)hipFree(m->status);
+  if (m->grid) (void)hipFree(m->grid);
+  delete m;
+}
+
+int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
+  int rc = check_model(src);
+  if (rc) return rc;
+  if (!out) return set_err(MFGP_ERR_ARG, "null out");
+  mfgp_ctx* c = src->ctx;
+  mfgp_model* m = nullptr;
+  if ((rc = mfgp_model_create(c, src->kind, MFGP_F64, src->hyp, src->nhyp, src->jitter, &m))) return rc;
+  if ((rc = ensure_cap(m, src->cap))) {
+    mfgp_model_destroy(m);
+    return rc;
+  }
+  // same capacity => same ld: the factor copies verbatim
+  const int64_t n = src->NL + src->NH;
+  m->NL = src->NL;
+  m->NH = src->NH;
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(m->X, src->X, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(m->y, src->y, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (src->factored && src->ld == m->ld) {
+    HIP_TRY(hipMemcpyAsync(m->A, src->A, sizeof(double) * src->ld * src->ld, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(m->Linv, src->Linv, sizeof(double) * (src->ld / NB) * TILE, hipMemcpyDeviceToDevice,
+                           c->stream));
+    m->factored = true;
+    m->factor_N = src->factor_N;
+    std::memcpy(m->factor_hyp, src->factor_hyp, sizeof(m->factor_hyp));
+    m->factor_jitter = src->factor_jitter;
+  }
+  if (src->M > 0) {
+    HIP_TRY(hipMalloc(&m->grid, sizeof(double) * 2 * src->M));
+    HIP_TRY(hipMemcpyAsync(m->grid, src->grid, sizeof(double) * 2 * src->M, hipMemcpyDeviceToDevice, c->stream));
+    m->M = m->Mcap = src->M;
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  *out = m;
+  return MFGP_OK;
+}
+
+int mfgp_model_set_hyp(mfgp_model* m, const double* hyp, int nhyp, double jitter) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (!hyp || nhyp != m->nhyp)
+    return set_err(MFGP_ERR_ARG, "Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)");
+  std::memcpy(m->hyp, hyp, sizeof(double) * nhyp);
+  m->jitter = jitter;
+  return MFGP_OK;
+}
+
+int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (M < 0 || (M > 0 && !xs)) return set_err(MFGP_ERR_ARG, "bad grid");
+  mfgp_ctx* c = m->ctx;
+  if (M > m->Mcap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (m->grid) HIP_TRY(hipFree(m->grid));
+    m->grid = nullptr;
+    HIP_TRY(hipMalloc(&m->grid, sizeof(double) * 2 * M));
+    m->Mcap = M;
+  }
+  m->M = M;
+  if (M > 0) HIP_TRY(hipMemcpyAsync(m->grid, xs, sizeof(double) * 2 * M, hipMemcpyDefault, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MFGP_OK;
+}
+
+int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL, const double* XH,
+                  const double* yH, int64_t NH) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (NL < 0 || NH < 0) return set_err(MFGP_ERR_ARG, "negative sizes");
+  if (m->kind == MFGP_SF && NL != 0) return set_err(MFGP_ERR_ARG, "SF model takes its data in the H slots");
+  if ((rc = ensure_cap(m, NL + NH))) return rc;
+  m->NL = NL;
+  m->NH = NH;
+  if ((rc = copy_rows(m, 0, XL, yL, NL))) return rc;
+  if ((rc = copy_rows(m, NL, XH, yH, NH))) return rc;
+  m->factored = false;
+  return factor_one(m);
+}
+
+int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (k < 0) return set_err(MFGP_ERR_ARG, "negative k");
+  const int64_t n = m->NL + m->NH;
+  if ((rc = ensure_cap(m, n + k))) return rc;
+  if ((rc = copy_rows(m, n, X, y, k))) return rc;
+  m->NH += k;
+  m->factored = false;
+  return factor_one(m);
+}
+
+int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (n_keep_hifi < 0 || n_keep_hifi > m->NH) return set_err(MFGP_ERR_ARG, "bad truncate size");
+  if (n_keep_hifi != m->NH) {
+    m->NH = n_keep_hifi;
+    m->factored = false;
+  }
+  return MFGP_OK;
+}
+
+int mfgp_predict(mfgp_model* m, double* mu, double* var) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  mfgp_ctx* c = m->ctx;
+  if (m->M > 0 && (!mu || !var)) return set_err(MFGP_ERR_ARG, "null output");
+  if (!factor_current(m)) {
+    if ((rc = factor_one(m))) return rc;
+  }
+  if (m->M == 0) return MFGP_OK;
+  const int64_t N = m->NL + m->NH;
+  const size_t vb = v_bytes(m->M, N);
+  const size_t ob = sizeof(double) * 2 * (size_t)m->M;
+  if ((rc = ensure_ws(c, vb + ob))) return rc;
+  int slot;
+  GPDesc* hd = acquire_slot(c, slot, rc);
+  if (!hd) return rc;
+  fill_desc(hd[0], m);
+  hd[0].V = c->ws;
+  hd[0].mu = reinterpret_cast<double*>(reinterpret_cast<char*>(c->ws) + vb);
+  hd[0].var = hd[0].mu + m->M;
+  const GPDesc* dd = nullptr;
+  if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
+  if ((rc = enqueue_predict(c, dd, hd, 1))) return rc;
+  HIP_TRY(hipMemcpyAsync(mu, hd[0].mu, sizeof(double) * m->M, hipMemcpyDefault, c->stream));
+  HIP_TRY(hipMemcpyAsync(var, hd[0].var, sizeof(double) * m->M, hipMemcpyDefault, c->stream));
+  if ((rc = release_slot(c, slot))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MFGP_OK;
+}
+
+int64_t mfgp_model_n(const mfgp_model* m) { return m ? m->NL + m->NH : -1; }
+int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
+int64_t mfgp_model_m(const mfgp_model* m) { return m ? m->M : -1; }
+
+int mfgp_get_factor(mfgp_model* m, double* L_out) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (!factor_current(m)) {
+    if ((rc = factor_one(m))) return rc;
+  }
+  const int64_t N = m->NL + m->NH;
+  if (N == 0) return MFGP_OK;
+  std::vector<double> cm((size_t)m->ld * N);
+  HIP_TRY(hipMemcpyAsync(cm.data(), m->A, sizeof(double) * m->ld * N, hipMemcpyDeviceToHost, m->ctx->stream));
+  HIP_TRY(hipStreamSynchronize(m->ctx->stream));
+  for (int64_t i = 0; i < N; ++i)
+    for (int64_t j = 0; j < N; ++j) L_out[i * N + j] = (j <= i) ? cm[(size_t)j * m->ld + i] : 0.0;
+  return MFGP_OK;
+}
+
+int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
+                              double* mu, double* var, int flags) {
+  if (!models || count <= 0) return set_err(MFGP_ERR_ARG, "empty batch");
+  mfgp_ctx* c = models[0]->ctx;
+  int rc = MFGP_OK;
+  for (int i = 0; i < count; ++i) {
+    if ((rc = check_model(models[i]))) return rc;
+    if (models[i]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
+    if (k && k[i] < 0) return set_err(MFGP_ERR_ARG, "negative k");
+  }
+  // append new rows
+  int64_t off = 0, out_off = 0;
+  for (int i = 0; i < count; ++i) {
+    mfgp_model* m = models[i];
+    const int64_t ki = k ? k[i] : 0;
+    const int64_t n = m->NL + m->NH;
+    if ((rc = ensure_cap(m, n + ki))) return rc;
+    if (ki > 0) {
+      if ((rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
+      m->NH += ki;
+    }
+    off += ki;
+  }
+  // workspace: V scratch for every model of a sub-batch
+  for (int b0 = 0; b0 < count; b0 += MAXB) {
+    const int nb = std::min(MAXB, count - b0);
+    size_t need = 0;
+    for (int i = 0; i < nb; ++i) {
+      mfgp_model* m = models[b0 + i];
+      need += v_bytes(m->M, m->NL + m->NH);
+    }
+    if ((rc = ensure_ws(c, need))) return rc;
+    int slot;
+    GPDesc* hd = acquire_slot(c, slot, rc);
+    if (!hd) return rc;
+    size_t vo = 0;
+    for (int i = 0; i < nb; ++i) {
+      mfgp_model* m = models[b0 + i];
+      fill_desc(hd[i], m);
+      hd[i].V = reinterpret_cast<double*>(reinterpret_cast<char*>(c->ws) + vo);
+      vo += v_bytes(m->M, m->NL + m->NH);
+      hd[i].mu = mu + out_off;
+      hd[i].var = var + out_off;
+      out_off += m->M;
+    }
+    const GPDesc* dd = nullptr;
+    if ((rc = upload_slot(c, slot, nb, &dd))) return rc;
+    if ((rc = enqueue_factor(c, dd, hd, nb))) return rc;
+    if ((rc = enqueue_predict(c, dd, hd, nb))) return rc;
+    if ((rc = release_slot(c, slot))) return rc;
+    for (int i = 0; i < nb; ++i) {
+      mfgp_model* m = models[b0 + i];
+      m->factored = true;
+      m->factor_N = m->NL + m->NH;
+      std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
+      m->factor_jitter = m->jitter;
+      c->async_status.push_back(m->status);
+    }
+  }
+  if (flags & MFGP_ASYNC) return MFGP_OK;
+  return mfgp_ctx_synchronize(c);
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// Internal types shared by the HIP kernels (mfgp_kernels.hip) and the C ABI
+// (mfgp_capi.hip). Not part of the public interface (include/mfgp_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mfgp {
+
+constexpr int NB = 64;    // row block of the factor and of V = L^-1 psi^T
+constexpr int BM = 64;    // grid cells per predict workgroup
+constexpr int NT = 256;   // threads per workgroup (4 waves of 64)
+constexpr int TILE = NB * NB;
+
+// Hyperparameters in linear scale, derived on the host from the log-scaled
+// vectors of simulator.py:53-56 / 83-84. SF uses the *L fields only.
+struct Hyp {
+  int kind;            // 0 = SF, 1 = MF
+  int pad_;
+  double sL, lL;       // output scale and length scale of k_L (SF: k)
+  double sH, lH;       // k_H (MF only)
+  double rho, rho2;    // AR(1) scale and rho*rho (gp:414, "rho ** 2")
+  double noiseL, noiseH;
+  double meanL, meanH; // prior means (gp:132 SF; gp:415-416 MF)
+  double jitter;       // gp:42 / gp:298
+  double kss;          // prior variance k**(x,x) (gp:146, gp:435-436)
+};
+
+// One GP of a batch. Device pointers; sizes in elements.
+struct GPDesc {
+  const double* X;     // [N,2] training coords: lofi rows [0,NL), hifi rows [NL,N)
+  const double* y;     // [N]
+  double* A;           // [ld,ld] column-major; lower triangle = L after the factor
+  double* Linv;        // [nb][NB*NB] column-major inverses of the diagonal blocks of L
+  const double* grid;  // [M,2]
+  double* V;           // predict scratch [ceil(M/BM)][ceil(N/NB)][NB*BM]
+  double* mu;          // [M]
+  double* var;         // [M]
+  int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
+  int64_t ld, N, NL, M;
+  Hyp hf;              // hyperparameters of the factorisation (updt_info time)
+  Hyp hp;              // hyperparameters of predict (predict time)
+};
+
+inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
+inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
+inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + BM - 1) / BM; }
+
+// Launchers (mfgp_kernels.hip). `d` points to `count` descriptors in device memory.
+hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);
+hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, hipStream_t s);
+hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
+hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, hipStream_t s);
+hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
+
+}  // namespace mfgp

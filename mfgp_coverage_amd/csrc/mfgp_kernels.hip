@@ -1,0 +1,474 @@
+// HIP kernels of the GP posterior update for gfx950 (MI355X), fp64.
+//
+// Reference path (MSU-dcypherlab/mfgp-coverage, gaussian_process.py):
+//   k_assemble    <- kernel(X,X) + sigma_n I + jitter I, SF gp:253-254, MF gp:523-529
+//                    (+ one augmented row r = y - m so the factor also yields z = L^-1 r)
+//   k_potrf_diag  \
+//   k_panel        > np.linalg.cholesky (gp:254, gp:529), blocked right-looking, NB = 64,
+//   k_syrk        /  with the explicit inverse of every diagonal block kept for the solves
+//   k_predict     <- predict (gp:121-148 / gp:401-438): psi = k(X*,X) generated in registers,
+//                    V = L^-1 psi^T by blocked forward substitution on f64 MFMA, and the
+//                    epilogue mu = m + V^T z (= m + psi alpha), var = k** - colsum(V o V)
+//                    (= diag(k** - psi K^-1 psi^T)); the M x M matrices of the reference
+//                    are never formed.
+//
+// Matrices are column-major; 64x64 operand tiles are staged "k-major" in LDS,
+// As[k][i], with an XOR swizzle of bit 4 of the column on odd k so that the
+// ds_read_b64 fragment loads of v_mfma_f64_16x16x4f64 are bank-conflict free.
+// f64 MFMA fragment maps (pinned on the hardware by tools/probe_mfma_f64.hip):
+//   A[i][k]: lane l holds A[l&15][l>>4];  B[k][j]: lane l holds B[l>>4][l&15];
+//   C/D:     lane l, reg v holds C[(l>>4) + 4v][l&15].
+#include <climits>
+#include "mfgp_internal.h"
+
+namespace mfgp {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz(int k, int i) { return k * NB + (i ^ ((k & 1) << 4)); }
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Per-wave 32x32 accumulator = 2x2 MFMA tiles of 16x16.
+struct Acc {
+  d4 c[2][2];
+};
+
+__device__ __forceinline__ void acc_zero(Acc& a) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) a.c[m][n] = d4{0.0, 0.0, 0.0, 0.0};
+}
+
+// acc (+/-)= A[64x64] * B[64x64] restricted to this wave's 32x32 output block.
+// As[swz(k,i)] = A[i][k], Bs[swz(k,j)] = B[k][j].
+template <bool NEG>
+__device__ __forceinline__ void tile_mma(const double* __restrict__ As, const double* __restrict__ Bs,
+                                         Acc& acc, int wm, int wn, int lane) {
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < NB; k0 += 4) {
+    const int k = k0 + q;
+    double a0 = As[swz(k, wm * 32 + r)];
+    double a1 = As[swz(k, wm * 32 + 16 + r)];
+    const double b0 = Bs[swz(k, wn * 32 + r)];
+    const double b1 = Bs[swz(k, wn * 32 + 16 + r)];
+    if (NEG) {
+      a0 = -a0;
+      a1 = -a1;
+    }
+    acc.c[0][0] = mfma(a0, b0, acc.c[0][0]);
+    acc.c[0][1] = mfma(a0, b1, acc.c[0][1]);
+    acc.c[1][0] = mfma(a1, b0, acc.c[1][0]);
+    acc.c[1][1] = mfma(a1, b1, acc.c[1][1]);
+  }
+}
+
+// Ts[swz(k,i)] = G[(c0+k)*ld + r0 + i], k,i in [0,64): a column-major 64x64 tile,
+// each source column becoming one k-row. 16-byte loads, coalesced along i.
+__device__ __forceinline__ void load_tile_cm(double* __restrict__ Ts, const double* __restrict__ G,
+                                             int64_t ld, int64_t r0, int64_t c0, int tid) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int k = p * 8 + (tid >> 5);
+    const int i = (tid & 31) * 2;
+    const double2 v = *reinterpret_cast<const double2*>(G + (c0 + k) * ld + r0 + i);
+    *reinterpret_cast<double2*>(Ts + swz(k, i)) = v;
+  }
+}
+
+// C/D element (mt, nt, v) of this lane <-> tile (row, col).
+__device__ __forceinline__ int acc_row(int wm, int mt, int q, int v) { return wm * 32 + mt * 16 + q + 4 * v; }
+__device__ __forceinline__ int acc_col(int wn, int nt, int r) { return wn * 32 + nt * 16 + r; }
+
+// ---------------------------------------------------------------------------
+// Squared-exponential kernel, gaussian_process.py:66-79, in the reference's
+// operation order: scale each coordinate by the length scale (a division),
+// subtract, square, sum over D = 2, exp(-0.5 * .), times the output scale.
+// No FMA contraction, so the rounding matches NumPy's elementwise ops.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double se_scaled(double ax, double ay, double bx, double by, double s) {
+#pragma clang fp contract(off)
+  const double dx = ax - bx;
+  const double dy = ay - by;
+  const double d2 = dx * dx + dy * dy;
+  return s * exp(-0.5 * d2);
+}
+
+__device__ __forceinline__ double div_(double a, double b) {
+#pragma clang fp contract(off)
+  return a / b;
+}
+
+// K entry (i, j), both < N, jitter and noise included (gp:253-254 / gp:523-529).
+__device__ __forceinline__ double k_entry(const Hyp& h, const double* __restrict__ X, int64_t NL,
+                                          int64_t gi, int64_t gj) {
+#pragma clang fp contract(off)
+  const double xi = X[2 * gi], yi = X[2 * gi + 1];
+  const double xj = X[2 * gj], yj = X[2 * gj + 1];
+  const double kl = se_scaled(div_(xi, h.lL), div_(yi, h.lL), div_(xj, h.lL), div_(yj, h.lL), h.sL);
+  double v;
+  if (h.kind == 0) {
+    v = kl;
+    if (gi == gj) v = (v + h.noiseL) + h.jitter;
+  } else {
+    const bool li = gi < NL, lj = gj < NL;
+    if (li && lj) {
+      v = kl;                                            // K_LL (gp:523)
+      if (gi == gj) v = (v + h.noiseL) + h.jitter;
+    } else if (li != lj) {
+      v = h.rho * kl;                                    // K_LH (gp:524)
+    } else {
+      const double kh = se_scaled(div_(xi, h.lH), div_(yi, h.lH), div_(xj, h.lH), div_(yj, h.lH), h.sH);
+      v = h.rho2 * kl + kh;                              // K_HH (gp:525-526)
+      if (gi == gj) v = (v + h.noiseH) + h.jitter;
+    }
+  }
+  return v;
+}
+
+__device__ __forceinline__ void tri_index(int64_t t, int& I, int& J) {
+  int i = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((int64_t)(i + 1) * (i + 2) / 2 <= t) ++i;
+  while ((int64_t)i * (i + 1) / 2 > t) --i;
+  I = i;
+  J = (int)(t - (int64_t)i * (i + 1) / 2);
+}
+
+// ---------------------------------------------------------------------------
+// Assembly: lower-triangular tiles of the augmented matrix
+//   [ K + (sigma_n + jitter) I   .  ]   rows 0..N-1
+//   [ (y - m)^T                  1  ]   row N  (its pivot is forced to 1)
+//   [ 0                          I  ]   padding up to a multiple of NB
+// Grid (tiles, batch); 256 threads; thread -> (row i = tid & 63, column group).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_assemble(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t N = d.N, NL = d.NL, ld = d.ld;
+  const int64_t T = nblocks_factor(N);
+  const int64_t t = blockIdx.x;
+  if (t == 0 && threadIdx.x == 0) *d.status = INT_MAX;
+  if (t >= T * (T + 1) / 2) return;
+  int I, J;
+  tri_index(t, I, J);
+  const Hyp& h = d.hf;
+  const int i = threadIdx.x & 63;
+  const int64_t gi = (int64_t)I * NB + i;
+  double* __restrict__ A = d.A;
+  for (int jj = threadIdx.x >> 6; jj < NB; jj += 4) {
+    const int64_t gj = (int64_t)J * NB + jj;
+    double v;
+    if (gj > gi) {
+      v = 0.0;
+    } else if (gi < N) {
+      v = k_entry(h, d.X, NL, gi, gj);
+    } else if (gi == N && gj < N) {
+      // residual y - m (gp:133 SF; gp:419-421 MF): lofi rows use mean_L, hifi mean_H
+      const double m = (h.kind == 1 && gj < NL) ? h.meanL : h.meanH;
+      v = d.y[gj] - m;
+    } else {
+      v = (gi == gj) ? 1.0 : 0.0;
+    }
+    A[gj * ld + gi] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal block kb: unblocked Cholesky of the 64x64 tile in LDS, then the
+// explicit inverse of the triangular factor (column c solved by thread c).
+// Rows >= N (the augmented row and padding) get pivot 1; a non-positive pivot
+// on a real row is recorded in *status (LAPACK potrf's INFO, which NumPy turns
+// into LinAlgError, gp:254 / gp:529) and replaced by 1 to keep the batch finite.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb) {
+  const GPDesc& d = descs[blockIdx.x];
+  const int64_t N = d.N, ld = d.ld;
+  if (kb >= nblocks_factor(N)) return;
+  __shared__ double S[NB * (NB + 1)];
+  const int tid = threadIdx.x;
+  const int64_t o = (int64_t)kb * NB;
+  double* __restrict__ A = d.A;
+  for (int e = tid; e < NB * NB; e += NT) {
+    const int i = e & 63, j = e >> 6;
+    S[i * (NB + 1) + j] = (j <= i) ? A[(o + j) * ld + o + i] : 0.0;
+  }
+  __syncthreads();
+  for (int j = 0; j < NB; ++j) {
+    if (tid == 0) {
+      double p = S[j * (NB + 1) + j];
+      const int64_t g = o + j;
+      if (g >= N) {
+        p = 1.0;
+      } else if (!(p > 0.0)) {
+        atomicMin(d.status, (int)(g + 1));
+        p = 1.0;
+      }
+      S[j * (NB + 1) + j] = sqrt(p);
+    }
+    __syncthreads();
+    if (tid > j && tid < NB) S[tid * (NB + 1) + j] = S[tid * (NB + 1) + j] / S[j * (NB + 1) + j];
+    __syncthreads();
+    {
+      const int a = tid & 63;
+      if (a > j) {
+        const double la = S[a * (NB + 1) + j];
+        for (int b = j + 1 + (tid >> 6); b <= a; b += 4) S[a * (NB + 1) + b] -= la * S[b * (NB + 1) + j];
+      }
+    }
+  }
+  __syncthreads();
+  // write L (lower, zeros above)
+  for (int e = tid; e < NB * NB; e += NT) {
+    const int i = e & 63, j = e >> 6;
+    A[(o + j) * ld + o + i] = (j <= i) ? S[i * (NB + 1) + j] : 0.0;
+  }
+  // explicit inverse: thread c < 64 computes column c by forward substitution
+  if (tid < NB) {
+    const int c = tid;
+    double x[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < i; ++m) s -= S[i * (NB + 1) + m] * x[m];
+      x[i] = s / S[i * (NB + 1) + i];
+    }
+    double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) Li[c * NB + i] = x[i];
+  }
+}
+
+// Panel: L_ik = A_ik * Linv_kk^T for every row block i > kb.
+__global__ __launch_bounds__(NT) void k_panel(const GPDesc* __restrict__ descs, int kb) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t nb = nblocks_factor(d.N);
+  const int64_t ib = kb + 1 + (int64_t)blockIdx.x;
+  if (ib >= nb) return;
+  __shared__ double As[TILE], Bs[TILE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  load_tile_cm(As, d.A, d.ld, ib * NB, (int64_t)kb * NB, tid);
+  load_tile_cm(Bs, d.Linv + (int64_t)kb * TILE, NB, 0, 0, tid);  // Bs[m][j] = Linv[j][m]
+  __syncthreads();
+  Acc acc;
+  acc_zero(acc);
+  tile_mma<false>(As, Bs, acc, wm, wn, lane);
+  const int r = lane & 15, q = lane >> 4;
+  double* __restrict__ A = d.A;
+  const int64_t ld = d.ld;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
+        A[((int64_t)kb * NB + col) * ld + ib * NB + row] = acc.c[mt][nt][v];
+      }
+}
+
+// Trailing update: A_ij -= L_ik L_jk^T for kb < j <= i (lower tiles only).
+__global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, int kb) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t nb = nblocks_factor(d.N);
+  const int64_t T = nb - kb - 1;
+  const int64_t t = blockIdx.x;
+  if (T <= 0 || t >= T * (T + 1) / 2) return;
+  int ii, jj;
+  tri_index(t, ii, jj);
+  const int64_t ib = kb + 1 + ii, jb = kb + 1 + jj;
+  __shared__ double As[TILE], Bs[TILE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t ld = d.ld;
+  double* __restrict__ A = d.A;
+  load_tile_cm(As, A, ld, ib * NB, (int64_t)kb * NB, tid);
+  load_tile_cm(Bs, A, ld, jb * NB, (int64_t)kb * NB, tid);
+  Acc acc;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
+        acc.c[mt][nt][v] = A[(jb * NB + col) * ld + ib * NB + row];
+      }
+  __syncthreads();
+  tile_mma<true>(As, Bs, acc, wm, wn, lane);
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
+        A[(jb * NB + col) * ld + ib * NB + row] = acc.c[mt][nt][v];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// Fused predict. One workgroup = one GP x 64 grid cells. For each 64-row block
+// I of the training set (sequential, left-looking):
+//   acc  = psi_I^T                          (exp in registers, gp:139 / gp:426-429)
+//   acc -= sum_{J<I} L_IJ V_J               (f64 MFMA, V_J re-read from scratch)
+//   V_I  = Linv_II acc                      (f64 MFMA)
+//   var_part += colsum(V_I o V_I);  mu_part += V_I^T z_I
+// then mu = m + mu_part (gp:142-143 / gp:432), var = k** - var_part (diag of
+// gp:146 / gp:435-436). z = L^-1 (y - m) is row N of the augmented factor.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT, 2) void k_predict(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t M = d.M;
+  const int64_t c0 = (int64_t)blockIdx.x * BM;
+  if (c0 >= M) return;
+  __shared__ double As[TILE], Bs[TILE];
+  __shared__ double zs[NB];
+  __shared__ double red[2][2][BM];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int r = lane & 15, q = lane >> 4;
+  const Hyp& h = d.hp;
+  const int64_t N = d.N, NL = d.NL, ld = d.ld;
+  const int64_t nblk = nblocks_rows(N);
+  const double* __restrict__ X = d.X;
+
+  // this lane's two grid cells (columns), scaled by the length scales
+  double cLx[2], cLy[2], cHx[2], cHy[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    int64_t c = c0 + acc_col(wn, nt, r);
+    if (c >= M) c = M - 1;
+    const double gx = d.grid[2 * c], gy = d.grid[2 * c + 1];
+    cLx[nt] = div_(gx, h.lL);
+    cLy[nt] = div_(gy, h.lL);
+    cHx[nt] = div_(gx, h.lH);
+    cHy[nt] = div_(gy, h.lH);
+  }
+  double vsum[2] = {0.0, 0.0}, msum[2] = {0.0, 0.0};
+  double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * nblk * TILE;
+
+  for (int64_t I = 0; I < nblk; ++I) {
+    Acc acc;
+    // psi_I^T in the accumulator layout
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t g = I * NB + acc_row(wm, mt, q, v);
+        double pv[2] = {0.0, 0.0};
+        if (g < N) {
+          const double tx = X[2 * g], ty = X[2 * g + 1];
+          const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
+          if (h.kind == 0) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) pv[nt] = se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
+          } else if (g < NL) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) pv[nt] = h.rho * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
+          } else {
+            const double tHx = div_(tx, h.lH), tHy = div_(ty, h.lH);
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+#pragma clang fp contract(off)
+              pv[nt] = h.rho2 * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL) +
+                       se_scaled(cHx[nt], cHy[nt], tHx, tHy, h.sH);
+            }
+          }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc.c[mt][nt][v] = pv[nt];
+      }
+    // acc -= L_IJ V_J
+    for (int64_t J = 0; J < I; ++J) {
+      __syncthreads();
+      load_tile_cm(As, d.A, ld, I * NB, J * NB, tid);
+      load_tile_cm(Bs, Vt + J * TILE, NB, 0, 0, tid);
+      __syncthreads();
+      tile_mma<true>(As, Bs, acc, wm, wn, lane);
+    }
+    __syncthreads();
+    load_tile_cm(As, d.Linv + I * TILE, NB, 0, 0, tid);  // As[m][i] = Linv[i][m]
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) Bs[swz(acc_row(wm, mt, q, v), acc_col(wn, nt, r))] = acc.c[mt][nt][v];
+    if (tid < NB) {
+      const int64_t g = I * NB + tid;
+      zs[tid] = (g < N) ? d.A[g * ld + N] : 0.0;  // z_g = L[N][g]
+    }
+    __syncthreads();
+    Acc vb;
+    acc_zero(vb);
+    tile_mma<false>(As, Bs, vb, wm, wn, lane);
+    const bool keep = (I + 1 < nblk);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
+          const double val = vb.c[mt][nt][v];
+          if (keep) Vt[I * TILE + row * BM + col] = val;
+          if (I * NB + row < N) {
+            vsum[nt] += val * val;
+            msum[nt] += val * zs[row];
+          }
+        }
+  }
+  // reduce over the 4 row groups of the wave (lanes r, r+16, r+32, r+48)
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    vsum[nt] += __shfl_xor(vsum[nt], 16);
+    vsum[nt] += __shfl_xor(vsum[nt], 32);
+    msum[nt] += __shfl_xor(msum[nt], 16);
+    msum[nt] += __shfl_xor(msum[nt], 32);
+  }
+  __syncthreads();
+  if (q == 0) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      red[0][wm][acc_col(wn, nt, r)] = vsum[nt];
+      red[1][wm][acc_col(wn, nt, r)] = msum[nt];
+    }
+  }
+  __syncthreads();
+  if (tid < BM) {
+    const int64_t c = c0 + tid;
+    if (c < M) {
+      const double vs = red[0][0][tid] + red[0][1][tid];
+      const double ms = red[1][0][tid] + red[1][1][tid];
+      d.mu[c] = ms + h.meanH;
+      d.var[c] = h.kss - vs;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_assemble, dim3((unsigned)max_tiles, count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, hipStream_t s) {
+  hipLaunchKernelGGL(k_potrf_diag, dim3(count), dim3(NT), 0, s, d, kb);
+  return hipGetLastError();
+}
+hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s) {
+  hipLaunchKernelGGL(k_panel, dim3((unsigned)max_below, count), dim3(NT), 0, s, d, kb);
+  return hipGetLastError();
+}
+hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, hipStream_t s) {
+  hipLaunchKernelGGL(k_syrk, dim3((unsigned)max_tri, count), dim3(NT), 0, s, d, kb);
+  return hipGetLastError();
+}
+hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_predict, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+
+}  // namespace mfgp

@@ -1,0 +1,299 @@
+"""Drop-in SFGP / MFGP with the reference's Python surface, computed on MI355X.
+
+Mirrors ``gaussian_process.py`` of MSU-dcypherlab/mfgp-coverage (imported by the
+simulator at simulator.py:25): same class names, constructor signatures,
+writable ``.hyp`` / ``.jitter``, the ``X, y`` / ``X_L, y_L, X_H, y_H`` attributes,
+``updt_info`` / ``updt`` / ``updt_hifi`` / ``predict``, ``copy.deepcopy`` and
+``isinstance`` (simulator.py:339, 361-366). The training set, the Cholesky
+factor and the grid live on the GPU (libmfgp_hip.so); numpy arrays are kept on
+the host only as the readable mirror the callers use.
+
+Differences from the reference, all on the output side of the contract:
+
+* ``predict`` returns ``(mu [M,1] ndarray, DiagCov)``. ``DiagCov`` carries the
+  diagonal of the posterior covariance -- the only part any caller reads
+  (``np.diag`` at simulator.py:301, 341, 685, 855; ``np.amax`` at 672, 842,
+  1014; plotter.py:160). ``np.diag``/``np.amax``/``np.argmax`` of it give what
+  they give on the dense matrix (for a PSD covariance the maximum entry lies on
+  the diagonal); any other use materialises it only when M == 1.
+* The factorisation is the GPU's; results agree with the reference to the
+  tolerance in oracle/gp_oracle.py (mu rel 1e-6, var rel 1e-6 floored at
+  1e-6 * k**).
+* Training (``likelihood``/``train``, gp:81-119, 344-399) and the unused extras
+  (``ExpectedImprovement``, ``draw_*``, ``pred_var``, ``get_*_var``) are out of
+  scope of this engine.
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+
+from . import _lib
+
+
+class DiagCov:
+    """Diagonal-only stand-in for the dense [M,M] posterior covariance of gp:146 / gp:435-436."""
+
+    __slots__ = ("var",)
+
+    def __init__(self, var):
+        self.var = np.asarray(var, dtype=np.float64).reshape(-1)
+
+    @property
+    def shape(self):
+        return (self.var.shape[0], self.var.shape[0])
+
+    ndim = 2
+    dtype = np.dtype(np.float64)
+
+    def diagonal(self):
+        return self.var.copy()
+
+    def __len__(self):
+        return self.var.shape[0]
+
+    def __getitem__(self, idx):
+        if isinstance(idx, tuple) and len(idx) == 2 and all(isinstance(i, (int, np.integer)) for i in idx):
+            i, j = (int(v) % self.var.shape[0] for v in idx)
+            if i == j:
+                return self.var[i]
+        return self._dense()[idx]
+
+    def _dense(self):
+        if self.var.shape[0] == 1:
+            return self.var.reshape(1, 1).copy()
+        raise TypeError("DiagCov holds only the diagonal of the posterior covariance (the off-diagonal "
+                        "entries are never computed); use np.diag(cov) / np.amax(cov)")
+
+    def __array__(self, dtype=None, copy=None):
+        d = self._dense()
+        return d if dtype is None else d.astype(dtype)
+
+    def __array_function__(self, func, types, args, kwargs):
+        if func in (np.diag, np.diagonal):
+            k = kwargs.get("k", kwargs.get("offset", args[1] if len(args) > 1 else 0))
+            if k == 0:
+                return self.var.copy()
+        if func in (np.amax, np.max) and kwargs.get("axis", args[1] if len(args) > 1 else None) is None:
+            return self.var.max()
+        if func is np.argmax and kwargs.get("axis", args[1] if len(args) > 1 else None) is None:
+            # flat index of the maximum of the dense matrix (first diagonal maximum)
+            i = int(np.argmax(self.var))
+            return i * self.var.shape[0] + i
+        if func is np.trace:
+            return self.var.sum()
+        args = tuple(self._dense() if a is self else a for a in args)
+        return func(*args, **kwargs)
+
+    def __array_ufunc__(self, ufunc, method, *inputs, **kwargs):
+        inputs = tuple(self._dense() if x is self else x for x in inputs)
+        return getattr(ufunc, method)(*inputs, **kwargs)
+
+    def __repr__(self):
+        return f"DiagCov(M={self.var.shape[0]}, diag={self.var!r})"
+
+
+def _dense_op(name):
+    def op(self, *other):
+        return getattr(self._dense(), name)(*other)
+    op.__name__ = name
+    return op
+
+
+for _name in ("__add__", "__radd__", "__sub__", "__rsub__", "__mul__", "__rmul__", "__truediv__",
+              "__rtruediv__", "__neg__", "__abs__", "__lt__", "__le__", "__gt__", "__ge__"):
+    setattr(DiagCov, _name, _dense_op(_name))
+
+
+def _as2(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1, 2))
+
+
+def _as1(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1))
+
+
+class _DeviceGP:
+    """Shared device plumbing of SFGP / MFGP."""
+
+    _kind = None
+
+    def _dev(self):
+        m = self.__dict__.get("_model")
+        if m is None:
+            m = _lib.Model(_lib.context(), self._kind, self._hyp_vec(), self.jitter)
+            self.__dict__["_model"] = m
+            self.__dict__["_synced"] = None
+            self.__dict__["_grid"] = None
+        return m
+
+    def _hyp_vec(self):
+        return np.ascontiguousarray(np.asarray(self.hyp, dtype=np.float64).reshape(-1))
+
+    def _push_hyp(self):
+        self._dev().set_hyp(self._hyp_vec(), self.jitter)
+
+    def _grid_to_device(self, X_star):
+        xs = _as2(X_star)
+        g = self.__dict__.get("_grid")
+        if g is None or g.shape != xs.shape or not np.array_equal(g, xs):
+            self._dev().set_grid(xs)
+            self.__dict__["_grid"] = xs.copy()
+
+    def _predict_dev(self, X_star):
+        self._sync_data()
+        self._push_hyp()
+        self._grid_to_device(X_star)
+        mu, var = self._dev().predict()
+        return mu.reshape(-1, 1), DiagCov(var)
+
+    @property
+    def L(self):
+        """Lower Cholesky factor of K + jitter*I (gp:254 / gp:529), downloaded on demand."""
+        self._sync_data()
+        self._push_hyp()
+        return self._dev().factor()
+
+    def __deepcopy__(self, memo):
+        new = self.__class__.__new__(self.__class__)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            if k == "_model":
+                continue
+            new.__dict__[k] = copy.deepcopy(v, memo)
+        m = self.__dict__.get("_model")
+        if m is not None:
+            new.__dict__["_model"] = m.clone()
+            # the clone holds exactly the device state of `self`; re-key its sync marker
+            syn = self.__dict__.get("_synced")
+            if syn is not None:
+                new.__dict__["_synced"] = tuple(copy.deepcopy(a, memo) if a is not None else None for a in syn)
+        return new
+
+
+class SFGP(_DeviceGP):
+    """Single-fidelity GP (gaussian_process.py:23-268) on the GPU."""
+
+    _kind = _lib.SF
+
+    def __init__(self, X, y, len):
+        self.D = X.shape[1]                   # gp:36
+        self.X = X
+        self.y = y
+        self.hyp = self.init_params(len)      # gp:40
+        self.jitter = 1e-8                    # gp:42
+        # gp:44 computes the NLML here only to set self.L; the factor is built
+        # lazily on the device at the first updt*/predict instead.
+
+    def init_params(self, len):
+        """gaussian_process.py:46-64."""
+        hyp = np.log(np.ones(self.D + 1))
+        self.idx_theta = np.arange(hyp.shape[0])
+        logsigma_n = np.array([-4.0])
+        hyp = np.concatenate([hyp, logsigma_n])
+        hyp[0] = -4.0
+        hyp[2] = np.log(len)
+        return hyp
+
+    def _sync_data(self):
+        syn = self.__dict__.get("_synced")
+        if syn is not None and syn[0] is self.X and syn[1] is self.y:
+            return
+        X, y = _as2(self.X), _as1(self.y)
+        self._push_hyp()
+        self._dev().set_data(np.empty((0, 2)), np.empty(0), X, y)
+        self.__dict__["_synced"] = (self.X, self.y)
+
+    def updt_info(self, X_new, y_new):
+        """gaussian_process.py:229-255: replace the data and refactor (raises LinAlgError if not PD)."""
+        self.X = X_new
+        self.y = y_new
+        self.__dict__["_synced"] = None
+        self._sync_data()
+
+    def updt(self, X_addition, y_addition):
+        """gaussian_process.py:257-268: append (k >= 0 rows) and refactor."""
+        prev = (self.X, self.y)
+        self.X = np.vstack((self.X, X_addition))
+        self.y = np.vstack((self.y, y_addition))
+        syn = self.__dict__.get("_synced")
+        if syn is not None and syn[0] is prev[0] and syn[1] is prev[1]:
+            self._push_hyp()
+            self.__dict__["_synced"] = None
+            self._dev().append(_as2(X_addition), _as1(y_addition))
+            self.__dict__["_synced"] = (self.X, self.y)
+        else:
+            self.__dict__["_synced"] = None
+            self._sync_data()
+
+    def predict(self, X_star):
+        """gaussian_process.py:121-148 -> (mu [M,1], DiagCov of the posterior covariance)."""
+        return self._predict_dev(X_star)
+
+
+class MFGP(_DeviceGP):
+    """Two-level AR(1) multi-fidelity GP (gaussian_process.py:271-578) on the GPU."""
+
+    _kind = _lib.MF
+
+    def __init__(self, X_L, y_L, X_H, y_H, len_L, len_H):
+        self.D = X_H.shape[1]                 # gp:287
+        self.X_L = X_L
+        self.y_L = y_L
+        self.X_H = X_H
+        self.y_H = y_H
+        self.idx_theta_L = np.empty([0, 0])
+        self.idx_theta_H = np.empty([0, 0])
+        self.hyp = self.init_params(len_L, len_H)
+        self.jitter = 1e-8                    # gp:298
+
+    def init_params(self, len_L, len_H):
+        """gaussian_process.py:300-327."""
+        hyp = np.ones(self.D + 1)
+        hyp[0] = 0
+        self.idx_theta_L = np.arange(hyp.shape[0])
+        hyp = np.concatenate((hyp, hyp))
+        self.idx_theta_H = np.arange(self.idx_theta_L[-1] + 1, hyp.shape[0])
+        rho = np.array([-1.0])
+        sigma_n = np.array([0, 0])
+        hyp = np.concatenate((hyp, rho, sigma_n))
+        hyp[0] = 0
+        hyp[3] = 0
+        hyp[2] = np.log(len_L)
+        hyp[5] = np.log(len_H)
+        return hyp
+
+    def _sync_data(self):
+        syn = self.__dict__.get("_synced")
+        if syn is not None and all(a is b for a, b in zip(syn, (self.X_L, self.y_L, self.X_H, self.y_H))):
+            return
+        self._push_hyp()
+        self._dev().set_data(_as2(self.X_L), _as1(self.y_L), _as2(self.X_H), _as1(self.y_H))
+        self.__dict__["_synced"] = (self.X_L, self.y_L, self.X_H, self.y_H)
+
+    def updt_info(self, X_L_new, y_L_new, X_H_new, y_H_new):
+        """gaussian_process.py:493-529."""
+        self.X_L, self.y_L, self.X_H, self.y_H = X_L_new, y_L_new, X_H_new, y_H_new
+        self.__dict__["_synced"] = None
+        self._sync_data()
+
+    def updt_hifi(self, X_H_addition, y_H_addition):
+        """gaussian_process.py:531-542: append hifi rows (k >= 0) and refactor."""
+        prev = (self.X_L, self.y_L, self.X_H, self.y_H)
+        self.X_H = np.vstack((self.X_H, X_H_addition))
+        self.y_H = np.vstack((self.y_H, y_H_addition))
+        syn = self.__dict__.get("_synced")
+        if syn is not None and all(a is b for a, b in zip(syn, prev)):
+            self._push_hyp()
+            self.__dict__["_synced"] = None
+            self._dev().append(_as2(X_H_addition), _as1(y_H_addition))
+            self.__dict__["_synced"] = (self.X_L, self.y_L, self.X_H, self.y_H)
+        else:
+            self.__dict__["_synced"] = None
+            self._sync_data()
+
+    def predict(self, X_star):
+        """gaussian_process.py:401-438 -> (mu [M,1], DiagCov of the posterior covariance)."""
+        return self._predict_dev(X_star)
+

@@ -1,0 +1,88 @@
+"""The drop-in boundary without a GPU: the C-ABI library loads and exports every
+symbol include/mfgp_hip.h declares, the Python mirror has the reference's
+surface, DiagCov behaves like the dense covariance for the callers' uses, and
+the product path refuses to run without a device (no CPU fallback)."""
+import copy
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "mfgp_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mfgp_[a-z_0-9]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__ as ge
+    ge.build()
+    from mfgp_coverage_amd import _lib
+    return _lib
+
+
+def test_library_exports_every_declared_symbol(lib):
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    h = lib.lib()
+    for s in syms:
+        assert hasattr(h, s), s
+        assert s in lib.SIGNATURES, s
+    assert set(lib.SIGNATURES) == set(syms)
+    assert b"gfx950" in h.mfgp_version()
+
+
+def test_library_is_gfx950_code_object(lib):
+    data = open(lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    for k in (b"k_predict", b"k_potrf_diag", b"k_panel", b"k_syrk", b"k_assemble"):
+        assert k in data
+
+
+def test_mirror_surface_without_device(lib):
+    from mfgp_coverage_amd.gaussian_process import MFGP, SFGP
+    e2, e1 = np.empty((0, 2)), np.empty((0, 1))
+    sf = SFGP(e2, e1, 1)
+    # gp:46-64 defaults
+    np.testing.assert_array_equal(sf.hyp, [-4.0, 0.0, 0.0, -4.0])
+    assert sf.D == 2 and sf.jitter == 1e-8 and list(sf.idx_theta) == [0, 1, 2]
+    mf = MFGP(e2, e1, e2, e1, 1, 1)
+    np.testing.assert_array_equal(mf.hyp, [0, 1, 0, 0, 1, 0, -1, 0, 0])   # gp:300-327
+    assert list(mf.idx_theta_L) == [0, 1, 2] and list(mf.idx_theta_H) == [3, 4, 5]
+    for name in ("updt_info", "updt", "predict"):
+        assert callable(getattr(sf, name))
+    for name in ("updt_info", "updt_hifi", "predict"):
+        assert callable(getattr(mf, name))
+    c = copy.deepcopy(sf)   # no device state yet: plain copy
+    assert isinstance(c, SFGP) and c is not sf
+
+
+def test_no_cpu_fallback(lib):
+    from mfgp_coverage_amd.gaussian_process import SFGP
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    m = SFGP(np.zeros((1, 2)), np.zeros((1, 1)), 1)
+    with pytest.raises(RuntimeError, match="libmfgp_hip"):
+        m.predict(np.zeros((4, 2)))
+
+
+def test_diagcov_semantics():
+    from mfgp_coverage_amd.gaussian_process import DiagCov
+    v = np.array([0.1, 0.5, 0.2])
+    c = DiagCov(v)
+    np.testing.assert_array_equal(np.diag(c), v)                # simulator.py:301, 341, 685, 855
+    assert np.amax(c) == 0.5                                    # simulator.py:672, 842, 1014
+    assert np.argmax(c) == 1 * 3 + 1
+    assert c.shape == (3, 3) and c[1, 1] == 0.5
+    with pytest.raises(TypeError):
+        np.asarray(c)
+    one = DiagCov(np.array([0.25]))                             # get_neg_var's 1x1 (gp:556-557)
+    assert float(2.0 * one[0, 0]) == 0.5
+    np.testing.assert_array_equal(np.asarray(one), [[0.25]])
+    assert (np.array([[1.0]]) + 2.0 * one)[0, 0] == 1.5
