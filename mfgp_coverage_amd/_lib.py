@@ -67,6 +67,14 @@ def lib():
         if _lib is None:
             if not os.path.exists(LIB_PATH):
                 raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+            # One HIP runtime per process: PyTorch-ROCm bundles its own
+            # libamdhip64.so.7 (same SONAME as /opt/rocm's). Loading torch first
+            # makes the dynamic linker bind this library to that same runtime, so
+            # torch tensors, streams and RCCL share one HIP runtime with the kernels.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             h = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 f = getattr(h, name)
