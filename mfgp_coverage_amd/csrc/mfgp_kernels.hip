@@ -23,7 +23,33 @@
 
 namespace mfgp {
 
+// Diagnostic phase stamps (tools/bench_diag.hip builds with -DMFGP_STAMPS); no-op otherwise.
+#ifdef MFGP_STAMPS
+__device__ long long* g_stamps;
+#define STAMP(id)                                                                        \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_stamps[id] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(id) \
+  do {            \
+  } while (0)
+#endif
+
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+// Generic -> global address space, so loads/stores through descriptor pointers
+// are emitted as global_* (vmcnt only) instead of flat_* (vmcnt + lgkmcnt).
+#define GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GLOBAL T* gp(T* p) {
+  return (GLOBAL T*)p;
+}
+template <class T>
+__device__ __forceinline__ const GLOBAL T* gp(const T* p) {
+  return (const GLOBAL T*)p;
+}
 
 __device__ __forceinline__ int swz(int k, int i) { return k * NB + (i ^ ((k & 1) << 4)); }
 
@@ -75,8 +101,34 @@ __device__ __forceinline__ void load_tile_cm(double* __restrict__ Ts, const doub
   for (int p = 0; p < 8; ++p) {
     const int k = p * 8 + (tid >> 5);
     const int i = (tid & 31) * 2;
-    const double2 v = *reinterpret_cast<const double2*>(G + (c0 + k) * ld + r0 + i);
-    *reinterpret_cast<double2*>(Ts + swz(k, i)) = v;
+    const dv2 v = *reinterpret_cast<const GLOBAL dv2*>(gp(G) + (c0 + k) * ld + r0 + i);
+    *reinterpret_cast<dv2*>(Ts + swz(k, i)) = v;
+  }
+}
+
+// Register staging of a column-major 64x64 tile (issue-early / write-late):
+// fetch_tile_cm issues the 8 16-byte global loads per thread; store_tile writes
+// them to the swizzled k-major LDS image once the buffer is free.
+struct Stage {
+  dv2 v[8];
+};
+
+__device__ __forceinline__ void fetch_tile_cm(Stage& st, const double* __restrict__ G, int64_t ld, int64_t r0,
+                                              int64_t c0, int tid) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int k = p * 8 + (tid >> 5);
+    const int i = (tid & 31) * 2;
+    st.v[p] = *reinterpret_cast<const GLOBAL dv2*>(gp(G) + (c0 + k) * ld + r0 + i);
+  }
+}
+
+__device__ __forceinline__ void store_tile(double* __restrict__ Ts, const Stage& st, int tid) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int k = p * 8 + (tid >> 5);
+    const int i = (tid & 31) * 2;
+    *reinterpret_cast<dv2*>(Ts + swz(k, i)) = st.v[p];
   }
 }
 
@@ -177,69 +229,222 @@ __global__ __launch_bounds__(NT) void k_assemble(const GPDesc* __restrict__ desc
 }
 
 // ---------------------------------------------------------------------------
-// Diagonal block kb: unblocked Cholesky of the 64x64 tile in LDS, then the
-// explicit inverse of the triangular factor (column c solved by thread c).
+// Diagonal block kb: Cholesky of the 64x64 tile and the explicit inverse of its
+// factor, blocked in 16x16 sub-blocks so the serial part is four 16-step chains:
+//   for each 16-column sub-block: (a) wave 0 factors the 16x16 diagonal block
+//   (lane r owns row r in registers, column broadcasts by v_readlane) and inverts
+//   it (lane c solves column c); (b) the sub-panel below is multiplied by that
+//   inverse; (c) the trailing sub-matrix is updated -- (b) and (c) by all 256
+//   threads. Then Linv's off-diagonal 16x16 blocks follow by block substitution.
 // Rows >= N (the augmented row and padding) get pivot 1; a non-positive pivot
 // on a real row is recorded in *status (LAPACK potrf's INFO, which NumPy turns
 // into LinAlgError, gp:254 / gp:529) and replaced by 1 to keep the batch finite.
 // ---------------------------------------------------------------------------
+constexpr int SP = NB + 1;   // padded row stride of the row-major LDS tiles
+constexpr int DB = 16;       // sub-block
+constexpr int DP = DB + 1;
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// Broadcast lane k of each 16-lane DPP row to the whole row (row_newbcast:k, gfx90a+).
+// The DPP control must be an immediate: the switch folds away once the callers'
+// fully unrolled loops make k a constant.
+template <int K>
+__device__ __forceinline__ double bcast16_(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + K, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + K, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double bcast16(double v, int k) {
+  switch (k) {
+    case 0: return bcast16_<0>(v);
+    case 1: return bcast16_<1>(v);
+    case 2: return bcast16_<2>(v);
+    case 3: return bcast16_<3>(v);
+    case 4: return bcast16_<4>(v);
+    case 5: return bcast16_<5>(v);
+    case 6: return bcast16_<6>(v);
+    case 7: return bcast16_<7>(v);
+    case 8: return bcast16_<8>(v);
+    case 9: return bcast16_<9>(v);
+    case 10: return bcast16_<10>(v);
+    case 11: return bcast16_<11>(v);
+    case 12: return bcast16_<12>(v);
+    case 13: return bcast16_<13>(v);
+    case 14: return bcast16_<14>(v);
+    default: return bcast16_<15>(v);
+  }
+}
+
+// 16x16 f64 MFMA block product on LDS operands: acc (+/-)= A[16xK] * B[Kx16] with
+// A[i][k] = A[i*ars + k*acs], B[k][j] = B[k*brs + j*bcs].
+template <bool NEG>
+__device__ __forceinline__ d4 mfma16(const double* __restrict__ A, int ars, int acs, const double* __restrict__ B,
+                                     int brs, int bcs, int K, d4 acc, int lane) {
+  const int r = lane & 15, q = lane >> 4;
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    double a = A[r * ars + (k0 + q) * acs];
+    if (NEG) a = -a;
+    acc = mfma(a, B[(k0 + q) * brs + r * bcs], acc);
+  }
+  return acc;
+}
+
+// S: 64x64 row-major (stride SP), lower triangle = the matrix. On exit S = L
+// (zeros above the diagonal) and R = L^-1 (row-major, zeros above).
+__device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R, double* __restrict__ T,
+                                 double* __restrict__ U, int64_t g0, int64_t N, int* status) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r16 = lane & 15, q16 = lane >> 4;
+  for (int kk = 0; kk < NB / DB; ++kk) {
+    const int o = kk * DB;
+    if (w == 0) {
+      // (a) factor the 16x16 diagonal block in registers: lane r holds row o+(r&15)
+      //     (the four 16-lane DPP rows of the wave hold identical copies); column
+      //     values are broadcast inside each DPP row with row_newbcast, so no
+      //     SGPR/LDS round trip sits on the pivot chain. LAPACK dpotf2 order:
+      //     pivot = sqrt(a_jj), column scaled by 1/pivot.
+      double d[DB];
+#pragma unroll
+      for (int c = 0; c < DB; ++c) d[c] = S[(o + r16) * SP + o + c];
+      double rdiag = 1.0;
+      int fail = INT_MAX;
+#pragma unroll
+      for (int j = 0; j < DB; ++j) {
+        double p = bcast16(d[j], j);
+        const int64_t g = g0 + o + j;
+        const bool pad = g >= N;
+        const bool bad = !pad && !(p > 0.0);
+        fail = bad ? min(fail, (int)(g + 1)) : fail;
+        p = (pad || bad) ? 1.0 : p;
+        const double rs = rsqrt(p);
+        const double l = (r16 > j) ? d[j] * rs : (r16 == j ? p * rs : 0.0);
+        rdiag = (r16 == j) ? rs : rdiag;
+        d[j] = l;
+        const double lu = (r16 > j) ? l : 0.0;
+#pragma unroll
+        for (int k = j + 1; k < DB; ++k) d[k] -= lu * bcast16(l, k);
+      }
+      if (fail != INT_MAX && lane == 0) atomicMin(status, fail);
+      if (lane < DB) {
+#pragma unroll
+        for (int c = 0; c < DB; ++c) S[(o + lane) * SP + o + c] = (c <= lane) ? d[c] : 0.0;
+      }
+      // inverse of the 16x16 factor: lane c solves column c = r16 by forward
+      // substitution; L[i][m] is register m of DPP-row lane i.
+      double x[DB];
+#pragma unroll
+      for (int i = 0; i < DB; ++i) {
+        double s0 = (i == r16) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+        for (int m = 0; m < i; ++m) {
+          const double lim = bcast16(d[m], i);
+          if (m & 1) s1 -= lim * x[m]; else s0 -= lim * x[m];
+        }
+        x[i] = (s0 + s1) * bcast16(rdiag, i);
+      }
+      if (lane < DB) {
+#pragma unroll
+        for (int i = 0; i < DB; ++i) T[kk * DB * DP + i * DP + lane] = x[i];
+      }
+    }
+    __syncthreads();
+    STAMP(2 + 3 * kk);
+    const int nrest = NB / DB - 1 - kk;   // 16-row blocks below the diagonal block
+    // (b) sub-panel P = A_sub * Dinv^T, one 16x16 block per wave (MFMA)
+    if (w < nrest) {
+      const int R0 = o + DB + DB * w;
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = mfma16<false>(S + R0 * SP + o, SP, 1, T + kk * DB * DP, 1, DP, DB, acc, lane);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) S[(R0 + q16 + 4 * v) * SP + o + r16] = acc[v];
+    }
+    __syncthreads();
+    STAMP(3 + 3 * kk);
+    // (c) trailing update of the lower 16x16 blocks of rows/cols [o+16, 64) (MFMA)
+    for (int t = w; t < nrest * (nrest + 1) / 2; t += NT / 64) {
+      int bi = 0;
+      while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+      const int bj = t - bi * (bi + 1) / 2;
+      const int R0 = o + DB + DB * bi, C0 = o + DB + DB * bj;
+      d4 acc;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[v] = S[(R0 + q16 + 4 * v) * SP + C0 + r16];
+      acc = mfma16<true>(S + R0 * SP + o, SP, 1, S + C0 * SP + o, 1, SP, DB, acc, lane);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) S[(R0 + q16 + 4 * v) * SP + C0 + r16] = acc[v];
+    }
+    __syncthreads();
+    STAMP(4 + 3 * kk);
+  }
+  // Linv: diagonal blocks from T, then block rows I = 1..3 by substitution:
+  //   Linv_IJ = -Dinv_I * sum_{m=J}^{I-1} L_Im Linv_mJ      (MFMA, wave w -> J = w)
+  for (int e = tid; e < NB * NB; e += NT) {
+    const int i = e >> 6, j = e & 63;
+    R[i * SP + j] = ((i >> 4) == (j >> 4) && j <= i) ? T[(i >> 4) * DB * DP + (i & 15) * DP + (j & 15)] : 0.0;
+  }
+  __syncthreads();
+  STAMP(14);
+  for (int I = 1; I < NB / DB; ++I) {
+    if (w < I) {
+      const int J = w;
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = mfma16<false>(S + (I * DB) * SP + J * DB, SP, 1, R + (J * DB) * SP + J * DB, SP, 1, (I - J) * DB, acc,
+                          lane);
+      double* Uj = U + J * DB * DP;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) Uj[(q16 + 4 * v) * DP + r16] = acc[v];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+      acc2 = mfma16<true>(T + I * DB * DP, DP, 1, Uj, DP, 1, DB, acc2, lane);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) R[(I * DB + q16 + 4 * v) * SP + J * DB + r16] = acc2[v];
+    }
+    __syncthreads();
+    STAMP(14 + I);
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb) {
   const GPDesc& d = descs[blockIdx.x];
   const int64_t N = d.N, ld = d.ld;
   if (kb >= nblocks_factor(N)) return;
-  __shared__ double S[NB * (NB + 1)];
+  __shared__ double S[NB * SP], R[NB * SP], T[(NB / DB) * DB * DP], U[(NB / DB - 1) * DB * DP];
   const int tid = threadIdx.x;
   const int64_t o = (int64_t)kb * NB;
   double* __restrict__ A = d.A;
-  for (int e = tid; e < NB * NB; e += NT) {
-    const int i = e & 63, j = e >> 6;
-    S[i * (NB + 1) + j] = (j <= i) ? A[(o + j) * ld + o + i] : 0.0;
-  }
-  __syncthreads();
-  for (int j = 0; j < NB; ++j) {
-    if (tid == 0) {
-      double p = S[j * (NB + 1) + j];
-      const int64_t g = o + j;
-      if (g >= N) {
-        p = 1.0;
-      } else if (!(p > 0.0)) {
-        atomicMin(d.status, (int)(g + 1));
-        p = 1.0;
-      }
-      S[j * (NB + 1) + j] = sqrt(p);
+  STAMP(0);
+  {
+    // unconditional loads (the upper part of the tile is masked afterwards) keep
+    // all 16 loads per thread in flight
+    double v[NB * NB / NT];
+#pragma unroll
+    for (int t = 0; t < NB * NB / NT; ++t) {
+      const int e = tid + t * NT, i = e & 63, j = e >> 6;
+      v[t] = A[(o + j) * ld + o + i];
     }
-    __syncthreads();
-    if (tid > j && tid < NB) S[tid * (NB + 1) + j] = S[tid * (NB + 1) + j] / S[j * (NB + 1) + j];
-    __syncthreads();
-    {
-      const int a = tid & 63;
-      if (a > j) {
-        const double la = S[a * (NB + 1) + j];
-        for (int b = j + 1 + (tid >> 6); b <= a; b += 4) S[a * (NB + 1) + b] -= la * S[b * (NB + 1) + j];
-      }
+#pragma unroll
+    for (int t = 0; t < NB * NB / NT; ++t) {
+      const int e = tid + t * NT, i = e & 63, j = e >> 6;
+      S[i * SP + j] = (j <= i) ? v[t] : 0.0;
     }
   }
   __syncthreads();
-  // write L (lower, zeros above)
+  STAMP(1);
+  factor_invert_64(S, R, T, U, o, N, d.status);
+  double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
+#pragma unroll 4
   for (int e = tid; e < NB * NB; e += NT) {
-    const int i = e & 63, j = e >> 6;
-    A[(o + j) * ld + o + i] = (j <= i) ? S[i * (NB + 1) + j] : 0.0;
+    const int i = e & 63, j = e >> 6;   // column-major: consecutive threads -> consecutive rows
+    A[(o + j) * ld + o + i] = S[i * SP + j];
+    Li[j * NB + i] = R[i * SP + j];
   }
-  // explicit inverse: thread c < 64 computes column c by forward substitution
-  if (tid < NB) {
-    const int c = tid;
-    double x[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      double s = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int m = 0; m < i; ++m) s -= S[i * (NB + 1) + m] * x[m];
-      x[i] = s / S[i * (NB + 1) + i];
-    }
-    double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) Li[c * NB + i] = x[i];
-  }
+  STAMP(18);
 }
 
 // Panel: L_ik = A_ik * Linv_kk^T for every row block i > kb.
@@ -381,16 +586,30 @@ __global__ __launch_bounds__(NT, 2) void k_predict(const GPDesc* __restrict__ de
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc.c[mt][nt][v] = pv[nt];
       }
-    // acc -= L_IJ V_J
+    // acc -= L_IJ V_J; the tiles of step J+1 (and finally Linv_II) are in flight
+    // in registers while step J runs on the MFMA.
+    // (one call site per staging buffer, operands chosen by scalar selects, so the
+    // stages stay in registers)
+    Stage sa, sb;
+    {
+      const bool more = I > 0;
+      fetch_tile_cm(sa, more ? d.A : d.Linv + I * TILE, more ? ld : NB, more ? I * NB : 0, 0, tid);
+      fetch_tile_cm(sb, Vt, NB, 0, 0, tid);
+    }
     for (int64_t J = 0; J < I; ++J) {
       __syncthreads();
-      load_tile_cm(As, d.A, ld, I * NB, J * NB, tid);
-      load_tile_cm(Bs, Vt + J * TILE, NB, 0, 0, tid);
+      store_tile(As, sa, tid);
+      store_tile(Bs, sb, tid);
       __syncthreads();
+      const bool more = J + 1 < I;
+      // As[m][i] = Linv[i][m] after the last step
+      fetch_tile_cm(sa, more ? d.A : d.Linv + I * TILE, more ? ld : NB, more ? I * NB : 0, more ? (J + 1) * NB : 0,
+                    tid);
+      fetch_tile_cm(sb, Vt + (more ? J + 1 : J) * TILE, NB, 0, 0, tid);
       tile_mma<true>(As, Bs, acc, wm, wn, lane);
     }
     __syncthreads();
-    load_tile_cm(As, d.Linv + I * TILE, NB, 0, 0, tid);  // As[m][i] = Linv[i][m]
+    store_tile(As, sa, tid);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
