@@ -95,6 +95,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     from mfgp_coverage_amd import _lib, synthetic
+    from mfgp_coverage_amd.ensemble import gather_trajectories, shard_seeds
 
     _lib.set_device(local)
     ctx = _lib.context()
@@ -109,8 +110,8 @@ def main():
     M = G * G
     N = NL + NH
     wls, models = [], []
-    for b in range(B):
-        wl = synthetic.Workload(G, NL, NH0, k, total, seed=rank * B + b)
+    for seed in shard_seeds(world * B, world, rank):
+        wl = synthetic.Workload(G, NL, NH0, k, total, seed=seed)
         mdl = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
         mdl.set_grid(wl.xs)
         mdl.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
@@ -142,13 +143,8 @@ def main():
     for s in range(W, total):
         step(s)
     traj = varmax[W:].transpose(0, 1).contiguous()           # [B, K] per-seed VarMax trajectory
-    if world > 1:
-        parts = [torch.empty_like(traj) for _ in range(world)]
-        dist.all_gather(parts, traj)                          # the single RCCL exchange
-        allt = torch.cat(parts, 0)
-    else:
-        allt = traj
-    agg = torch.stack([allt.mean(0), allt.std(0) if allt.shape[0] > 1 else torch.zeros_like(allt[0])])
+    _, agg_mean, agg_std = gather_trajectories(traj, world)   # the single RCCL exchange
+    agg = torch.stack([agg_mean, torch.nan_to_num(agg_std)])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
