@@ -12,7 +12,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmfgp_hip.so")
+LIB_PATH = os.environ.get("MFGP_LIB") or os.path.join(HERE, "libmfgp_hip.so")
 
 OK, ERR_NOT_PD, ERR_ARG, ERR_DEVICE = 0, 1, 2, 3
 SF, MF = 0, 1

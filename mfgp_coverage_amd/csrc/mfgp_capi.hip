@@ -310,7 +310,7 @@ int enqueue_predict(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
 }
 
 size_t v_bytes(int64_t M, int64_t N) {
-  return sizeof(double) * (size_t)ntiles_grid(M) * (size_t)nblocks_rows(N) * TILE;
+  return sizeof(double) * (size_t)ntiles_grid(M) * (size_t)prow_blocks(N) * PRB * PBM;
 }
 
 int read_status(mfgp_model* m) {

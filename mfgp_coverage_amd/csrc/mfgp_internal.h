@@ -10,6 +10,9 @@ constexpr int NB = 64;    // row block of the factor and of V = L^-1 psi^T
 constexpr int BM = 64;    // grid cells per predict workgroup
 constexpr int NT = 256;   // threads per workgroup (4 waves of 64)
 constexpr int TILE = NB * NB;
+constexpr int PRB = 128;  // predict: training rows per left-looking block
+constexpr int PBM = 128;  // predict: grid cells per workgroup
+constexpr int PNT = 512;  // predict: threads per workgroup (8 waves)
 
 // Hyperparameters in linear scale, derived on the host from the log-scaled
 // vectors of simulator.py:53-56 / 83-84. SF uses the *L fields only.
@@ -43,7 +46,8 @@ struct GPDesc {
 
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
 inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
-inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + BM - 1) / BM; }
+inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1) / PBM; }
+inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1) / PRB; }
 
 // Launchers (mfgp_kernels.hip). `d` points to `count` descriptors in device memory.
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);

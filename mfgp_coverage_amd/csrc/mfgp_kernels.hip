@@ -516,67 +516,159 @@ __global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, i
 }
 
 // ---------------------------------------------------------------------------
-// Fused predict. One workgroup = one GP x 64 grid cells. For each 64-row block
-// I of the training set (sequential, left-looking):
+// Fused predict. One workgroup (512 threads, 8 waves) = one GP x 128 grid
+// cells. For each 128-row block I of the training set (sequential,
+// left-looking):
 //   acc  = psi_I^T                          (exp in registers, gp:139 / gp:426-429)
-//   acc -= sum_{J<I} L_IJ V_J               (f64 MFMA, V_J re-read from scratch)
-//   V_I  = Linv_II acc                      (f64 MFMA)
+//   acc -= sum_{J<I} L_IJ V_J               (f64 MFMA over 32-deep K steps)
+//   V_I  = L_II^-1 acc                      (two 64-row halves, 64-wide inverses:
+//          V_top = Linv_a acc_top;  V_bot = Linv_b (acc_bot - L_ba V_top))
 //   var_part += colsum(V_I o V_I);  mu_part += V_I^T z_I
 // then mu = m + mu_part (gp:142-143 / gp:432), var = k** - var_part (diag of
 // gp:146 / gp:435-436). z = L^-1 (y - m) is row N of the augmented factor.
+//
+// 128x128 output tiles give 16 flop per byte of staged operand (L and V); the V
+// panels of earlier row blocks are re-read from HBM/MALL N/256 times. Operand
+// staging: global_load_lds_dwordx4 (LDS-DMA) into a 2-stage ring of 32-deep K
+// steps (32 KB of L + 32 KB of V per stage), one barrier per step: step s+1
+// streams into the other stage while step s runs on the MFMA. The XOR swizzle
+// of the LDS image is applied on the global source addresses (the DMA writes
+// lane-linear). All LDS lives in one array (hipcc vmcnt trap).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT, 2) void k_predict(const GPDesc* __restrict__ descs) {
+constexpr int KS = 32;                   // K depth of one pipeline step
+constexpr int PW = 128;                  // row width of the predict LDS images
+constexpr int STAGE = 2 * KS * PW;       // doubles per stage: As [KS][128] + Bs [KS][128]
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+__device__ __forceinline__ int swzp(int k, int i) { return k * PW + (i ^ ((k & 1) << 4)); }
+
+// DMA kn rows of 128 doubles into a swizzled [kn][128] LDS image:
+// dst[swzp(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves one
+// 1 KB row; the 8 waves take rows round-robin.
+__device__ __forceinline__ void dma_rows(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
+                                         int64_t c0, int kn, int w, int lane) {
+  for (int k = w; k < kn; k += PNT / 64) {
+    const int i = (2 * lane) ^ ((k & 1) << 4);
+    const double* src = G + (c0 + k) * ld + r0 + i;
+    __builtin_amdgcn_global_load_lds((const GLOBAL void*)src, (lds_vptr)(dst + k * PW), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Main-loop accumulator: wave (wm 0..3, wn 0..1) owns rows wm*32.. x cols wn*64..
+struct AccP {
+  d4 c[2][4];
+};
+// Diagonal-step accumulator: wave owns 16 rows x 64 cols of a 64-row half.
+struct AccH {
+  d4 c[4];
+};
+
+__device__ __forceinline__ void main_mma(const double* __restrict__ As, const double* __restrict__ Bs, AccP& acc,
+                                         int wm, int wn, int lane) {
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll 1
+  for (int k0 = 0; k0 < KS; k0 += 4) {
+    const int k = k0 + q;
+    double a[2], b[4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) a[mt] = -As[swzp(k, wm * 32 + mt * 16 + r)];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b[nt] = Bs[swzp(k, wn * 64 + nt * 16 + r)];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc.c[mt][nt] = mfma(a[mt], b[nt], acc.c[mt][nt]);
+  }
+}
+
+// A fragments of a column-major 64x64 block (A[i][k] = G[k*lda + i]) for the 16
+// rows p16.. of this wave, all 16 K steps: frag[t] = A[p16 + r][4t + q].
+__device__ __forceinline__ void load_afrag(double* frag, const double* __restrict__ G, int64_t lda, int p16,
+                                           int lane) {
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) frag[t] = gp(G)[(int64_t)(4 * t + q) * lda + p16 + r];
+}
+
+// acc (+/-)= A[16x64] (fragments) * img[rows rb..rb+63][cols wn*64..]
+template <bool NEG>
+__device__ __forceinline__ void half_mma(const double* frag, const double* __restrict__ img, int rb, AccH& acc,
+                                         int wn, int lane) {
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const double a = NEG ? -frag[t] : frag[t];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc.c[nt] = mfma(a, img[swzp(rb + 4 * t + q, wn * 64 + nt * 16 + r)], acc.c[nt]);
+  }
+}
+
+__global__ __launch_bounds__(PNT, 1) void k_predict(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
   const int64_t M = d.M;
-  const int64_t c0 = (int64_t)blockIdx.x * BM;
+  const int64_t c0 = (int64_t)blockIdx.x * PBM;
   if (c0 >= M) return;
-  __shared__ double As[TILE], Bs[TILE];
-  __shared__ double zs[NB];
-  __shared__ double red[2][2][BM];
+  // ring: stage s at lds[s*STAGE] = As [KS][128] then Bs [KS][128]; the diagonal
+  // step reuses the whole ring as the [128][128] image of acc / V.
+  __shared__ double lds[2 * STAGE + PRB];
+  double* const zs = lds + 2 * STAGE;
+  double* const img = lds;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int r = lane & 15, q = lane >> 4;
+  const int p16 = (w >> 1) * 16;   // diagonal-step rows of this wave inside a 64-row half
   const Hyp& h = d.hp;
   const int64_t N = d.N, NL = d.NL, ld = d.ld;
-  const int64_t nblk = nblocks_rows(N);
+  const int64_t nrb = prow_blocks(N);
+  const int64_t nbf = nblocks_factor(N);
   const double* __restrict__ X = d.X;
+  const double* __restrict__ Amat = d.A;
+  double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * nrb * (PRB * PBM);
 
-  // this lane's two grid cells (columns), scaled by the length scales
-  double cLx[2], cLy[2], cHx[2], cHy[2];
+  double vsum[4] = {0.0, 0.0, 0.0, 0.0}, msum[4] = {0.0, 0.0, 0.0, 0.0};
+
+  for (int64_t I = 0; I < nrb; ++I) {
+    const int64_t base = I * PRB;
+    const int nk = (int)(base / KS);   // K steps: all columns left of the block
+    if (nk > 0) {   // prologue: step 0 into stage 0 (overlaps the psi generation)
+      dma_rows(lds, Amat, ld, base, 0, KS, w, lane);
+      dma_rows(lds + KS * PW, Vt, PBM, 0, 0, KS, w, lane);
+    }
+    AccP acc;
+    // this lane's four grid cells (columns wn*64 + nt*16 + r in both layouts),
+    // scaled by the length scales (recomputed per block row: saves registers)
+    double cLx[4], cLy[4], cHx[4], cHy[4];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    int64_t c = c0 + acc_col(wn, nt, r);
-    if (c >= M) c = M - 1;
-    const double gx = d.grid[2 * c], gy = d.grid[2 * c + 1];
-    cLx[nt] = div_(gx, h.lL);
-    cLy[nt] = div_(gy, h.lL);
-    cHx[nt] = div_(gx, h.lH);
-    cHy[nt] = div_(gy, h.lH);
-  }
-  double vsum[2] = {0.0, 0.0}, msum[2] = {0.0, 0.0};
-  double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * nblk * TILE;
-
-  for (int64_t I = 0; I < nblk; ++I) {
-    Acc acc;
-    // psi_I^T in the accumulator layout
+    for (int nt = 0; nt < 4; ++nt) {
+      int64_t c = c0 + wn * 64 + nt * 16 + r;
+      if (c >= M) c = M - 1;
+      const double gx = d.grid[2 * c], gy = d.grid[2 * c + 1];
+      cLx[nt] = div_(gx, h.lL);
+      cLy[nt] = div_(gy, h.lL);
+      cHx[nt] = div_(gx, h.lH);
+      cHy[nt] = div_(gy, h.lH);
+    }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int64_t g = I * NB + acc_row(wm, mt, q, v);
-        double pv[2] = {0.0, 0.0};
+        const int64_t g = base + wm * 32 + mt * 16 + q + 4 * v;
+        double pv[4] = {0.0, 0.0, 0.0, 0.0};
         if (g < N) {
           const double tx = X[2 * g], ty = X[2 * g + 1];
           const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
           if (h.kind == 0) {
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) pv[nt] = se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
+            for (int nt = 0; nt < 4; ++nt) pv[nt] = se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
           } else if (g < NL) {
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) pv[nt] = h.rho * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
+            for (int nt = 0; nt < 4; ++nt) pv[nt] = h.rho * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
           } else {
             const double tHx = div_(tx, h.lH), tHy = div_(ty, h.lH);
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
+            for (int nt = 0; nt < 4; ++nt) {
 #pragma clang fp contract(off)
               pv[nt] = h.rho2 * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL) +
                        se_scaled(cHx[nt], cHy[nt], tHx, tHy, h.sH);
@@ -584,84 +676,129 @@ __global__ __launch_bounds__(NT, 2) void k_predict(const GPDesc* __restrict__ de
           }
         }
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc.c[mt][nt][v] = pv[nt];
+        for (int nt = 0; nt < 4; ++nt) acc.c[mt][nt][v] = pv[nt];
       }
-    // acc -= L_IJ V_J; the tiles of step J+1 (and finally Linv_II) are in flight
-    // in registers while step J runs on the MFMA.
-    // (one call site per staging buffer, operands chosen by scalar selects, so the
-    // stages stay in registers)
-    Stage sa, sb;
-    {
-      const bool more = I > 0;
-      fetch_tile_cm(sa, more ? d.A : d.Linv + I * TILE, more ? ld : NB, more ? I * NB : 0, 0, tid);
-      fetch_tile_cm(sb, Vt, NB, 0, 0, tid);
-    }
-    for (int64_t J = 0; J < I; ++J) {
-      __syncthreads();
-      store_tile(As, sa, tid);
-      store_tile(Bs, sb, tid);
-      __syncthreads();
-      const bool more = J + 1 < I;
-      // As[m][i] = Linv[i][m] after the last step
-      fetch_tile_cm(sa, more ? d.A : d.Linv + I * TILE, more ? ld : NB, more ? I * NB : 0, more ? (J + 1) * NB : 0,
-                    tid);
-      fetch_tile_cm(sb, Vt + (more ? J + 1 : J) * TILE, NB, 0, 0, tid);
-      tile_mma<true>(As, Bs, acc, wm, wn, lane);
-    }
+    vm_wait_all();
     __syncthreads();
-    store_tile(As, sa, tid);
+    // acc -= L_I,<I V_<I over 32-deep steps; step s+1 is in flight during step s
+    for (int s = 0; s < nk; ++s) {
+      double* cur = lds + (s & 1) * STAGE;
+#ifndef MFGP_DIAG_NODMA
+      if (s + 1 < nk) {
+        double* nxt = lds + ((s + 1) & 1) * STAGE;
+        const int64_t kc = (int64_t)(s + 1) * KS;
+#ifndef MFGP_DIAG_NODMA_L
+        dma_rows(nxt, Amat, ld, base, kc, KS, w, lane);
+#endif
+#ifndef MFGP_DIAG_NODMA_V
+        dma_rows(nxt + KS * PW, Vt, PBM, 0, kc, KS, w, lane);
+#endif
+      }
+#endif
+      main_mma(cur, cur + KS * PW, acc, wm, wn, lane);
+#ifndef MFGP_DIAG_NOBAR
+      vm_wait_all();
+      __syncthreads();
+#endif
+    }
+    // ---- diagonal block: V_I = L_II^-1 acc, in two 64-row halves ----
+    const int64_t fa = 2 * I, fb = 2 * I + 1;       // 64-blocks of the factor
+    const bool has_b = fb < nbf;                    // bottom half holds real rows
+    double frag[16];
+    load_afrag(frag, d.Linv + fa * TILE, NB, p16, lane);   // Linv_a
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+      for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) Bs[swz(acc_row(wm, mt, q, v), acc_col(wn, nt, r))] = acc.c[mt][nt][v];
-    if (tid < NB) {
-      const int64_t g = I * NB + tid;
-      zs[tid] = (g < N) ? d.A[g * ld + N] : 0.0;  // z_g = L[N][g]
+        for (int v = 0; v < 4; ++v) img[swzp(wm * 32 + mt * 16 + q + 4 * v, wn * 64 + nt * 16 + r)] = acc.c[mt][nt][v];
+    if (tid < PRB) {
+      const int64_t g = base + tid;
+      zs[tid] = (g < N) ? Amat[g * ld + N] : 0.0;  // z_g = L[N][g]
     }
     __syncthreads();
-    Acc vb;
-    acc_zero(vb);
-    tile_mma<false>(As, Bs, vb, wm, wn, lane);
-    const bool keep = (I + 1 < nblk);
+    const bool keep = (I + 1 < nrb);
+    // V_top = Linv_a * acc_top
+    AccH vh;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
+    half_mma<false>(frag, img, 0, vh, wn, lane);
+    if (has_b) load_afrag(frag, Amat + fa * NB * ld + fb * NB, ld, p16, lane);   // L_ba
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = p16 + q + 4 * v, col = wn * 64 + nt * 16 + r;
+        const double val = vh.c[nt][v];
+        if (keep) gp(Vt)[(base + row) * PBM + col] = val;
+        if (base + row < N) {
+          vsum[nt] += val * val;
+          msum[nt] += val * zs[row];
+        }
+      }
+    __syncthreads();   // every wave is done reading acc_top
+    if (has_b) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) img[swzp(p16 + q + 4 * v, wn * 64 + nt * 16 + r)] = vh.c[nt][v];
+      __syncthreads();
+      // T = acc_bot - L_ba V_top   (each wave: its own 16 rows of the bottom half)
+      AccH th;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) th.c[nt][v] = img[swzp(64 + p16 + q + 4 * v, wn * 64 + nt * 16 + r)];
+      half_mma<true>(frag, img, 0, th, wn, lane);
+      load_afrag(frag, d.Linv + fb * TILE, NB, p16, lane);   // Linv_b
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) img[swzp(64 + p16 + q + 4 * v, wn * 64 + nt * 16 + r)] = th.c[nt][v];
+      __syncthreads();
+      // V_bot = Linv_b T
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
+      half_mma<false>(frag, img, 64, vh, wn, lane);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
-          const double val = vb.c[mt][nt][v];
-          if (keep) Vt[I * TILE + row * BM + col] = val;
-          if (I * NB + row < N) {
+          const int row = 64 + p16 + q + 4 * v, col = wn * 64 + nt * 16 + r;
+          const double val = vh.c[nt][v];
+          if (keep) gp(Vt)[(base + row) * PBM + col] = val;
+          if (base + row < N) {
             vsum[nt] += val * val;
             msum[nt] += val * zs[row];
           }
         }
+    }
+    vm_wait_all();      // V_I stores complete before any later DMA reads them
+    __syncthreads();    // and before the next prologue overwrites the LDS images
   }
-  // reduce over the 4 row groups of the wave (lanes r, r+16, r+32, r+48)
+  // reduce over the 4 row groups of the wave (lanes r, r+16, r+32, r+48), then
+  // over the 4 waves sharing a column half (LDS, reusing the ring)
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
+  for (int nt = 0; nt < 4; ++nt) {
     vsum[nt] += __shfl_xor(vsum[nt], 16);
     vsum[nt] += __shfl_xor(vsum[nt], 32);
     msum[nt] += __shfl_xor(msum[nt], 16);
     msum[nt] += __shfl_xor(msum[nt], 32);
   }
-  __syncthreads();
+  double* red = lds;   // [2][4][PBM]
   if (q == 0) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      red[0][wm][acc_col(wn, nt, r)] = vsum[nt];
-      red[1][wm][acc_col(wn, nt, r)] = msum[nt];
+    for (int nt = 0; nt < 4; ++nt) {
+      red[(0 * 4 + (w >> 1)) * PBM + wn * 64 + nt * 16 + r] = vsum[nt];
+      red[(1 * 4 + (w >> 1)) * PBM + wn * 64 + nt * 16 + r] = msum[nt];
     }
   }
   __syncthreads();
-  if (tid < BM) {
+  if (tid < PBM) {
     const int64_t c = c0 + tid;
     if (c < M) {
-      const double vs = red[0][0][tid] + red[0][1][tid];
-      const double ms = red[1][0][tid] + red[1][1][tid];
+      const double vs = (red[0 * PBM + tid] + red[1 * PBM + tid]) + (red[2 * PBM + tid] + red[3 * PBM + tid]);
+      const double ms = (red[4 * PBM + tid] + red[5 * PBM + tid]) + (red[6 * PBM + tid] + red[7 * PBM + tid]);
       d.mu[c] = ms + h.meanH;
       d.var[c] = h.kss - vs;
     }
@@ -686,7 +823,7 @@ hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, hipS
   return hipGetLastError();
 }
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_predict, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
+  hipLaunchKernelGGL(k_predict, dim3((unsigned)max_ctiles, count), dim3(PNT), 0, s, d);
   return hipGetLastError();
 }
 

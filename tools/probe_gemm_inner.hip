@@ -4,6 +4,19 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef double d4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double rnd(unsigned e, unsigned salt) {
+  unsigned x = e * 2654435761u ^ salt; x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+  unsigned y = x * 2246822519u + 0x9e3779b9u; y ^= y >> 16;
+  return ((double)x / 4294967296.0 - 0.5) + ((double)y / 4294967296.0) * 1e-7;
+}
+#ifdef RANDOM_DATA
+#define FILL_A(e) rnd(e, 17u)
+#define FILL_B(e) rnd(e, 91u)
+#else
+#define FILL_A(e) (1e-3 * ((e) % 97))
+#define FILL_B(e) (1e-3 * ((e) % 89))
+#endif
+
 #define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s at %d\n",hipGetErrorString(e),__LINE__); return 1;}}while(0)
 
 // VALU: 256 threads, 128x128 output tile, thread = 8x8 block; K-step 16 in LDS, swept `reps` times.
@@ -12,7 +25,7 @@ __global__ __launch_bounds__(256) void valu_k(double* out, int reps) {
   constexpr int BMt = 16 * TM;  // 128 for TM=8
   __shared__ double As[16][BMt], Bs[16][BMt];
   const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
-  for (int e = t; e < 16 * BMt; e += 256) { As[e / BMt][e % BMt] = 1e-3 * (e % 97); Bs[e / BMt][e % BMt] = 1e-3 * (e % 89); }
+  for (int e = t; e < 16 * BMt; e += 256) { As[e / BMt][e % BMt] = FILL_A(e); Bs[e / BMt][e % BMt] = FILL_B(e); }
   __syncthreads();
   double c[TM][TM] = {};
   for (int rp = 0; rp < reps; ++rp) {
@@ -37,7 +50,7 @@ __global__ __launch_bounds__(256) void valu_k(double* out, int reps) {
 __global__ __launch_bounds__(256) void mfma_k(double* out, int reps) {
   __shared__ double As[64 * 64], Bs[64 * 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1, r = lane & 15, q = lane >> 4;
-  for (int e = t; e < 4096; e += 256) { As[e] = 1e-3 * (e % 97); Bs[e] = 1e-3 * (e % 89); }
+  for (int e = t; e < 4096; e += 256) { As[e] = FILL_A(e); Bs[e] = FILL_B(e); }
   __syncthreads();
   d4 c[2][2] = {};
   for (int rp = 0; rp < reps; ++rp) {
@@ -60,8 +73,8 @@ __global__ __launch_bounds__(256) void mfma_k(double* out, int reps) {
 __global__ __launch_bounds__(256) void mfma42_k(double* out, int reps) {
   __shared__ double As[64 * 128], Bs[64 * 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1, r = lane & 15, q = lane >> 4;
-  for (int e = t; e < 8192; e += 256) As[e] = 1e-3 * (e % 97);
-  for (int e = t; e < 4096; e += 256) Bs[e] = 1e-3 * (e % 89);
+  for (int e = t; e < 8192; e += 256) As[e] = FILL_A(e);
+  for (int e = t; e < 4096; e += 256) Bs[e] = FILL_B(e);
   __syncthreads();
   d4 c[4][2] = {};
   for (int rp = 0; rp < reps; ++rp) {
@@ -105,6 +118,14 @@ int main() {
     CK(hipEventElapsedTime(&ms, e0, e1));
     fl = (double)nb * 128 * 64 * 64 * 2.0 * (reps / 4);
     printf("MFMA 4x2/wave 128x64/WG   %d WG/CU: %6.2f TF (%.3f ms)\n", bpc, fl / ms / 1e9, ms);
+  }
+  // sustained: ~15 ms launches back to back (DVFS settles)
+  for (int rep = 0; rep < 3; ++rep) {
+    int nb = 512, reps = 256 * 12;
+    CK(hipEventRecord(e0)); mfma_k<<<nb, 256>>>(dO, reps); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    double fl = (double)nb * 64 * 64 * 64 * 2.0 * reps;
+    printf("sustained MFMA 2x2/wave 2 WG/CU: %6.2f TF (%.3f ms)\n", fl / ms / 1e9, ms);
   }
   return 0;
 }
