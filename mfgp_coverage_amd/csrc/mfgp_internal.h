@@ -11,8 +11,8 @@ constexpr int BM = 64;    // grid cells per predict workgroup
 constexpr int NT = 256;   // threads per workgroup (4 waves of 64)
 constexpr int TILE = NB * NB;
 constexpr int PRB = 128;  // predict: training rows per left-looking block
-constexpr int PBM = 128;  // predict: grid cells per workgroup
-constexpr int PNT = 512;  // predict: threads per workgroup (8 waves)
+constexpr int PBM = 64;   // predict: grid cells per workgroup
+constexpr int PNT = 256;  // predict: threads per workgroup (4 waves; two workgroups per CU)
 
 // Hyperparameters in linear scale, derived on the host from the log-scaled
 // vectors of simulator.py:53-56 / 83-84. SF uses the *L fields only.

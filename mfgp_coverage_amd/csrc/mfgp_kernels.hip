@@ -516,38 +516,40 @@ __global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, i
 }
 
 // ---------------------------------------------------------------------------
-// Fused predict. One workgroup (512 threads, 8 waves) = one GP x 128 grid
-// cells. For each 128-row block I of the training set (sequential,
-// left-looking):
+// Fused predict. One workgroup (256 threads, 4 waves; two workgroups per CU) =
+// one GP x 64 grid cells. For each 128-row block I of the training set
+// (sequential, left-looking):
 //   acc  = psi_I^T                          (exp in registers, gp:139 / gp:426-429)
-//   acc -= sum_{J<I} L_IJ V_J               (f64 MFMA over 32-deep K steps)
+//   acc -= sum_{J<I} L_IJ V_J               (f64 MFMA over 16-deep K steps)
 //   V_I  = L_II^-1 acc                      (two 64-row halves, 64-wide inverses:
 //          V_top = Linv_a acc_top;  V_bot = Linv_b (acc_bot - L_ba V_top))
 //   var_part += colsum(V_I o V_I);  mu_part += V_I^T z_I
 // then mu = m + mu_part (gp:142-143 / gp:432), var = k** - var_part (diag of
 // gp:146 / gp:435-436). z = L^-1 (y - m) is row N of the augmented factor.
 //
-// 128x128 output tiles give 16 flop per byte of staged operand (L and V); the V
-// panels of earlier row blocks are re-read from HBM/MALL N/256 times. Operand
-// staging: global_load_lds_dwordx4 (LDS-DMA) into a 2-stage ring of 32-deep K
-// steps (32 KB of L + 32 KB of V per stage), one barrier per step: step s+1
-// streams into the other stage while step s runs on the MFMA. The XOR swizzle
-// of the LDS image is applied on the global source addresses (the DMA writes
-// lane-linear). All LDS lives in one array (hipcc vmcnt trap).
+// Staging: global_load_lds_dwordx4 (LDS-DMA) into a 3-stage ring of 16-deep K
+// steps (16 KB of L + 8 KB of V per stage) with two steps in flight, a counted
+// vmcnt and one raw s_barrier per step (no __syncthreads in the loop: its fence
+// would drain the DMA). The XOR swizzles of the LDS images are applied on the
+// global source addresses (the DMA writes lane-linear). All LDS lives in one
+// array (hipcc vmcnt trap). The V panels of earlier row blocks are re-read from
+// HBM N/256 times -- the 128-row blocks halve that traffic against 64-row ones;
+// the second workgroup on the CU hides each one's psi / diagonal phases.
 // ---------------------------------------------------------------------------
-constexpr int KS = 32;                   // K depth of one pipeline step
-constexpr int PW = 128;                  // row width of the predict LDS images
-constexpr int STAGE = 2 * KS * PW;       // doubles per stage: As [KS][128] + Bs [KS][128]
+constexpr int KS = 16;                   // K depth of one pipeline step
+constexpr int PW = 128;                  // row width of the L image (= PRB)
+constexpr int NSTAGE = 3;
+constexpr int STAGE = KS * PW + KS * PBM;   // doubles per stage: As [KS][128] + Bs [KS][64]
+constexpr int GLDS_PER_STEP = (KS + KS * PBM / 128) / (PNT / 64);   // per wave: 4 (L) + 2 (V)
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
 __device__ __forceinline__ int swzp(int k, int i) { return k * PW + (i ^ ((k & 1) << 4)); }
 
 // DMA kn rows of 128 doubles into a swizzled [kn][128] LDS image:
-// dst[swzp(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves one
-// 1 KB row; the 8 waves take rows round-robin.
-__device__ __forceinline__ void dma_rows(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
-                                         int64_t c0, int kn, int w, int lane) {
+// dst[swzp(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves one 1 KB row.
+__device__ __forceinline__ void dma_rows128(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
+                                            int64_t c0, int kn, int w, int lane) {
   for (int k = w; k < kn; k += PNT / 64) {
     const int i = (2 * lane) ^ ((k & 1) << 4);
     const double* src = G + (c0 + k) * ld + r0 + i;
@@ -555,28 +557,41 @@ __device__ __forceinline__ void dma_rows(double* dst, const double* __restrict__
   }
 }
 
+// DMA kn rows of 64 doubles into a swizzled [kn][64] LDS image:
+// dst[swz(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves two rows.
+__device__ __forceinline__ void dma_rows64(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
+                                           int64_t c0, int kn, int w, int lane) {
+  for (int p = w; p < kn / 2; p += PNT / 64) {
+    const int k = 2 * p + (lane >> 5);
+    const int i = ((lane & 31) * 2) ^ ((k & 1) << 4);
+    const double* src = G + (c0 + k) * ld + r0 + i;
+    __builtin_amdgcn_global_load_lds((const GLOBAL void*)src, (lds_vptr)(dst + 2 * p * NB), 16, 0, 0);
+  }
+}
+
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Main-loop accumulator: wave (wm 0..3, wn 0..1) owns rows wm*32.. x cols wn*64..
+// Main-loop accumulator: wave wm owns rows wm*32.. x all 64 cells.
 struct AccP {
   d4 c[2][4];
 };
-// Diagonal-step accumulator: wave owns 16 rows x 64 cols of a 64-row half.
+// Diagonal-step accumulator: wave owns 16 rows of a 64-row half x 64 cells.
 struct AccH {
   d4 c[4];
 };
 
+// acc += A[32 rows of this wave][KS] * B[KS][64]  (acc holds -psi + sum L V)
 __device__ __forceinline__ void main_mma(const double* __restrict__ As, const double* __restrict__ Bs, AccP& acc,
-                                         int wm, int wn, int lane) {
+                                         int wm, int lane) {
   const int r = lane & 15, q = lane >> 4;
-#pragma unroll 1
+#pragma unroll
   for (int k0 = 0; k0 < KS; k0 += 4) {
     const int k = k0 + q;
     double a[2], b[4];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) a[mt] = -As[swzp(k, wm * 32 + mt * 16 + r)];
+    for (int mt = 0; mt < 2; ++mt) a[mt] = As[swzp(k, wm * 32 + mt * 16 + r)];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) b[nt] = Bs[swzp(k, wn * 64 + nt * 16 + r)];
+    for (int nt = 0; nt < 4; ++nt) b[nt] = Bs[swz(k, nt * 16 + r)];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -593,32 +608,34 @@ __device__ __forceinline__ void load_afrag(double* frag, const double* __restric
   for (int t = 0; t < 16; ++t) frag[t] = gp(G)[(int64_t)(4 * t + q) * lda + p16 + r];
 }
 
-// acc (+/-)= A[16x64] (fragments) * img[rows rb..rb+63][cols wn*64..]
+// acc (+/-)= A[16 x 4*nt4] (fragments) * img[rows rb..][64 cells]; nt4 K steps
 template <bool NEG>
 __device__ __forceinline__ void half_mma(const double* frag, const double* __restrict__ img, int rb, AccH& acc,
-                                         int wn, int lane) {
+                                         int nt4, int lane) {
   const int r = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
-    const double a = NEG ? -frag[t] : frag[t];
+    if (t < nt4) {
+      const double a = NEG ? -frag[t] : frag[t];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc.c[nt] = mfma(a, img[swzp(rb + 4 * t + q, wn * 64 + nt * 16 + r)], acc.c[nt]);
+      for (int nt = 0; nt < 4; ++nt) acc.c[nt] = mfma(a, img[swz(rb + 4 * t + q, nt * 16 + r)], acc.c[nt]);
+    }
   }
 }
 
-__global__ __launch_bounds__(PNT, 1) void k_predict(const GPDesc* __restrict__ descs) {
+__global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
   const int64_t M = d.M;
   const int64_t c0 = (int64_t)blockIdx.x * PBM;
   if (c0 >= M) return;
-  // ring: stage s at lds[s*STAGE] = As [KS][128] then Bs [KS][128]; the diagonal
-  // step reuses the whole ring as the [128][128] image of acc / V.
-  __shared__ double lds[2 * STAGE + PRB];
-  double* const zs = lds + 2 * STAGE;
+  // ring: stage s at lds[s*STAGE] = As [KS][128] then Bs [KS][64]; the diagonal
+  // step reuses the ring as the [128][64] image of acc / V (64 KB <= 72 KB).
+  __shared__ double lds[NSTAGE * STAGE + PRB];
+  double* const zs = lds + NSTAGE * STAGE;
   double* const img = lds;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
-  const int p16 = (w >> 1) * 16;   // diagonal-step rows of this wave inside a 64-row half
+  const int p16 = w * 16;   // diagonal-step rows of this wave inside a 64-row half
   const Hyp& h = d.hp;
   const int64_t N = d.N, NL = d.NL, ld = d.ld;
   const int64_t nrb = prow_blocks(N);
@@ -626,109 +643,110 @@ __global__ __launch_bounds__(PNT, 1) void k_predict(const GPDesc* __restrict__ d
   const double* __restrict__ X = d.X;
   const double* __restrict__ Amat = d.A;
   double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * nrb * (PRB * PBM);
-
   double vsum[4] = {0.0, 0.0, 0.0, 0.0}, msum[4] = {0.0, 0.0, 0.0, 0.0};
 
   for (int64_t I = 0; I < nrb; ++I) {
     const int64_t base = I * PRB;
     const int nk = (int)(base / KS);   // K steps: all columns left of the block
-    if (nk > 0) {   // prologue: step 0 into stage 0 (overlaps the psi generation)
-      dma_rows(lds, Amat, ld, base, 0, KS, w, lane);
-      dma_rows(lds + KS * PW, Vt, PBM, 0, 0, KS, w, lane);
+    // prologue: steps 0 and 1 in flight while psi is generated
+#pragma unroll
+    for (int s0 = 0; s0 < 2; ++s0) {
+      if (s0 < nk) {
+        double* st = lds + s0 * STAGE;
+        dma_rows128(st, Amat, ld, base, (int64_t)s0 * KS, KS, w, lane);
+        dma_rows64(st + KS * PW, Vt, PBM, 0, (int64_t)s0 * KS, KS, w, lane);
+      }
     }
     AccP acc;
-    // this lane's four grid cells (columns wn*64 + nt*16 + r in both layouts),
-    // scaled by the length scales (recomputed per block row: saves registers)
-    double cLx[4], cLy[4], cHx[4], cHy[4];
+    {
+      // this lane's four grid cells (columns nt*16 + r), scaled by the length scales
+      double cLx[4], cLy[4], cHx[4], cHy[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      int64_t c = c0 + wn * 64 + nt * 16 + r;
-      if (c >= M) c = M - 1;
-      const double gx = d.grid[2 * c], gy = d.grid[2 * c + 1];
-      cLx[nt] = div_(gx, h.lL);
-      cLy[nt] = div_(gy, h.lL);
-      cHx[nt] = div_(gx, h.lH);
-      cHy[nt] = div_(gy, h.lH);
-    }
+      for (int nt = 0; nt < 4; ++nt) {
+        int64_t c = c0 + nt * 16 + r;
+        if (c >= M) c = M - 1;
+        const double gx = d.grid[2 * c], gy = d.grid[2 * c + 1];
+        cLx[nt] = div_(gx, h.lL);
+        cLy[nt] = div_(gy, h.lL);
+        cHx[nt] = div_(gx, h.lH);
+        cHy[nt] = div_(gy, h.lH);
+      }
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int64_t g = base + wm * 32 + mt * 16 + q + 4 * v;
-        double pv[4] = {0.0, 0.0, 0.0, 0.0};
-        if (g < N) {
-          const double tx = X[2 * g], ty = X[2 * g + 1];
-          const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
-          if (h.kind == 0) {
+        for (int v = 0; v < 4; ++v) {
+          const int64_t g = base + w * 32 + mt * 16 + q + 4 * v;
+          double pv[4] = {0.0, 0.0, 0.0, 0.0};
+          if (g < N) {
+            const double tx = X[2 * g], ty = X[2 * g + 1];
+            const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
+            if (h.kind == 0) {
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) pv[nt] = se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
-          } else if (g < NL) {
+              for (int nt = 0; nt < 4; ++nt) pv[nt] = se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
+            } else if (g < NL) {
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) pv[nt] = h.rho * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
-          } else {
-            const double tHx = div_(tx, h.lH), tHy = div_(ty, h.lH);
+              for (int nt = 0; nt < 4; ++nt) pv[nt] = h.rho * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL);
+            } else {
+              const double tHx = div_(tx, h.lH), tHy = div_(ty, h.lH);
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
+              for (int nt = 0; nt < 4; ++nt) {
 #pragma clang fp contract(off)
-              pv[nt] = h.rho2 * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL) +
-                       se_scaled(cHx[nt], cHy[nt], tHx, tHy, h.sH);
+                pv[nt] = h.rho2 * se_scaled(cLx[nt], cLy[nt], tLx, tLy, h.sL) +
+                         se_scaled(cHx[nt], cHy[nt], tHx, tHy, h.sH);
+              }
             }
           }
-        }
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc.c[mt][nt][v] = pv[nt];
-      }
-    vm_wait_all();
-    __syncthreads();
-    // acc -= L_I,<I V_<I over 32-deep steps; step s+1 is in flight during step s
-    for (int s = 0; s < nk; ++s) {
-      double* cur = lds + (s & 1) * STAGE;
-#ifndef MFGP_DIAG_NODMA
-      if (s + 1 < nk) {
-        double* nxt = lds + ((s + 1) & 1) * STAGE;
-        const int64_t kc = (int64_t)(s + 1) * KS;
-#ifndef MFGP_DIAG_NODMA_L
-        dma_rows(nxt, Amat, ld, base, kc, KS, w, lane);
-#endif
-#ifndef MFGP_DIAG_NODMA_V
-        dma_rows(nxt + KS * PW, Vt, PBM, 0, kc, KS, w, lane);
-#endif
-      }
-#endif
-      main_mma(cur, cur + KS * PW, acc, wm, wn, lane);
-#ifndef MFGP_DIAG_NOBAR
-      vm_wait_all();
-      __syncthreads();
-#endif
+          for (int nt = 0; nt < 4; ++nt) acc.c[mt][nt][v] = -pv[nt];   // acc = -psi + sum L V
+        }
     }
-    // ---- diagonal block: V_I = L_II^-1 acc, in two 64-row halves ----
+    double frag[16];
+    if (nk > 0) {
+      // step 0 landed (step 1 may still be in flight)
+      if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_STEP) : "memory");
+      else vm_wait_all();
+      __builtin_amdgcn_s_barrier();
+    }
+    // acc += L_I,<I V_<I over 16-deep steps; steps s+1, s+2 in flight during step s
+    for (int s = 0; s < nk; ++s) {
+      const double* cur = lds + (s % NSTAGE) * STAGE;
+      if (s + 2 < nk) {
+        double* nxt = lds + ((s + 2) % NSTAGE) * STAGE;
+        const int64_t kc = (int64_t)(s + 2) * KS;
+        dma_rows128(nxt, Amat, ld, base, kc, KS, w, lane);
+        dma_rows64(nxt + KS * PW, Vt, PBM, 0, kc, KS, w, lane);
+      }
+      main_mma(cur, cur + KS * PW, acc, w, lane);
+      if (s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(GLDS_PER_STEP) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // ---- diagonal block: V_I = L_II^-1 (psi - L V), two 64-row halves ----
     const int64_t fa = 2 * I, fb = 2 * I + 1;       // 64-blocks of the factor
     const bool has_b = fb < nbf;                    // bottom half holds real rows
-    double frag[16];
     load_afrag(frag, d.Linv + fa * TILE, NB, p16, lane);   // Linv_a
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) img[swzp(wm * 32 + mt * 16 + q + 4 * v, wn * 64 + nt * 16 + r)] = acc.c[mt][nt][v];
+        for (int v = 0; v < 4; ++v) img[swz(w * 32 + mt * 16 + q + 4 * v, nt * 16 + r)] = -acc.c[mt][nt][v];
     if (tid < PRB) {
       const int64_t g = base + tid;
       zs[tid] = (g < N) ? Amat[g * ld + N] : 0.0;  // z_g = L[N][g]
     }
     __syncthreads();
     const bool keep = (I + 1 < nrb);
-    // V_top = Linv_a * acc_top
+    // V_top = Linv_a * T_top (Linv_a lower triangular: rows p16.. need K < p16 + 16)
     AccH vh;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
-    half_mma<false>(frag, img, 0, vh, wn, lane);
+    half_mma<false>(frag, img, 0, vh, (p16 + 16) / 4, lane);
     if (has_b) load_afrag(frag, Amat + fa * NB * ld + fb * NB, ld, p16, lane);   // L_ba
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int row = p16 + q + 4 * v, col = wn * 64 + nt * 16 + r;
+        const int row = p16 + q + 4 * v, col = nt * 16 + r;
         const double val = vh.c[nt][v];
         if (keep) gp(Vt)[(base + row) * PBM + col] = val;
         if (base + row < N) {
@@ -736,35 +754,35 @@ __global__ __launch_bounds__(PNT, 1) void k_predict(const GPDesc* __restrict__ d
           msum[nt] += val * zs[row];
         }
       }
-    __syncthreads();   // every wave is done reading acc_top
+    __syncthreads();   // every wave is done reading T_top
     if (has_b) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) img[swzp(p16 + q + 4 * v, wn * 64 + nt * 16 + r)] = vh.c[nt][v];
+        for (int v = 0; v < 4; ++v) img[swz(p16 + q + 4 * v, nt * 16 + r)] = vh.c[nt][v];
       __syncthreads();
-      // T = acc_bot - L_ba V_top   (each wave: its own 16 rows of the bottom half)
+      // T_bot -= L_ba V_top   (each wave: its own 16 rows of the bottom half)
       AccH th;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) th.c[nt][v] = img[swzp(64 + p16 + q + 4 * v, wn * 64 + nt * 16 + r)];
-      half_mma<true>(frag, img, 0, th, wn, lane);
+        for (int v = 0; v < 4; ++v) th.c[nt][v] = img[swz(64 + p16 + q + 4 * v, nt * 16 + r)];
+      half_mma<true>(frag, img, 0, th, 16, lane);
       load_afrag(frag, d.Linv + fb * TILE, NB, p16, lane);   // Linv_b
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) img[swzp(64 + p16 + q + 4 * v, wn * 64 + nt * 16 + r)] = th.c[nt][v];
+        for (int v = 0; v < 4; ++v) img[swz(64 + p16 + q + 4 * v, nt * 16 + r)] = th.c[nt][v];
       __syncthreads();
-      // V_bot = Linv_b T
+      // V_bot = Linv_b T_bot
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
-      half_mma<false>(frag, img, 64, vh, wn, lane);
+      half_mma<false>(frag, img, 64, vh, (p16 + 16) / 4, lane);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int row = 64 + p16 + q + 4 * v, col = wn * 64 + nt * 16 + r;
+          const int row = 64 + p16 + q + 4 * v, col = nt * 16 + r;
           const double val = vh.c[nt][v];
           if (keep) gp(Vt)[(base + row) * PBM + col] = val;
           if (base + row < N) {
@@ -777,7 +795,7 @@ __global__ __launch_bounds__(PNT, 1) void k_predict(const GPDesc* __restrict__ d
     __syncthreads();    // and before the next prologue overwrites the LDS images
   }
   // reduce over the 4 row groups of the wave (lanes r, r+16, r+32, r+48), then
-  // over the 4 waves sharing a column half (LDS, reusing the ring)
+  // over the 4 waves (LDS, reusing the ring)
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     vsum[nt] += __shfl_xor(vsum[nt], 16);
@@ -789,8 +807,8 @@ __global__ __launch_bounds__(PNT, 1) void k_predict(const GPDesc* __restrict__ d
   if (q == 0) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      red[(0 * 4 + (w >> 1)) * PBM + wn * 64 + nt * 16 + r] = vsum[nt];
-      red[(1 * 4 + (w >> 1)) * PBM + wn * 64 + nt * 16 + r] = msum[nt];
+      red[(0 * 4 + w) * PBM + nt * 16 + r] = vsum[nt];
+      red[(1 * 4 + w) * PBM + nt * 16 + r] = msum[nt];
     }
   }
   __syncthreads();
