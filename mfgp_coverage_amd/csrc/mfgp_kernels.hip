@@ -569,6 +569,17 @@ __device__ __forceinline__ void dma_rows64(double* dst, const double* __restrict
   }
 }
 
+// Buffer-descriptor LDS-DMA (buffer_load_dwordx4 ... lds): the lane part of the
+// source offset is a VGPR fixed for the whole kernel, the row/step part an SGPR,
+// so one DMA costs an s_mov to M0 and the load -- no per-row address VALU.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const double* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes), 0x00020000);
+}
+
+__device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, double* dst, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr)dst, 16, voff, soff, 0, 0);
+}
+
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Main-loop accumulator: wave wm owns rows wm*32.. x all 64 cells.
@@ -633,7 +644,8 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
   __shared__ double lds[NSTAGE * STAGE + PRB];
   double* const zs = lds + NSTAGE * STAGE;
   double* const img = lds;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave id (uniform)
   const int r = lane & 15, q = lane >> 4;
   const int p16 = w * 16;   // diagonal-step rows of this wave inside a 64-row half
   const Hyp& h = d.hp;
@@ -644,6 +656,28 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
   const double* __restrict__ Amat = d.A;
   double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * nrb * (PRB * PBM);
   double vsum[4] = {0.0, 0.0, 0.0, 0.0}, msum[4] = {0.0, 0.0, 0.0, 0.0};
+  // DMA plan of one K step (kc = first factor column / V row of the step):
+  //  L image [KS][128]: wave w moves rows k = w + 4j (j < 4), all of parity w&1;
+  //    src = A[(kc + k)*ld + base + ((2*lane) ^ sw)]
+  //  V image [KS][64]:  wave w moves row pairs p = w + 4j (j < 2), rows 2p + (lane>>5);
+  //    src = Vt[(kc + 2p + (lane>>5))*64 + (((lane&31)*2) ^ ((lane>>5)<<4))]
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(Amat, (int64_t)8 * ld * ld);
+  const __amdgpu_buffer_rsrc_t rsV = make_rsrc(Vt, (int64_t)8 * nrb * PRB * PBM);
+  const unsigned voffA = (unsigned)(8 * ((2 * lane) ^ ((w & 1) << 4)));
+  const unsigned voffV =
+      (unsigned)(8 * ((lane >> 5) * PBM + (((lane & 31) * 2) ^ ((lane >> 5) << 4))));
+  auto dma_step = [&](double* st, int64_t base_, int64_t kc) {
+#pragma unroll
+    for (int j = 0; j < KS / 4; ++j) {
+      const int k = w + 4 * j;
+      dma_buf(rsA, st + k * PW, voffA, (unsigned)(8 * ((kc + k) * ld + base_)));
+    }
+#pragma unroll
+    for (int j = 0; j < KS / 8; ++j) {
+      const int pp = w + 4 * j;
+      dma_buf(rsV, st + KS * PW + 2 * pp * PBM, voffV, (unsigned)(8 * (kc + 2 * pp) * PBM));
+    }
+  };
 
   for (int64_t I = 0; I < nrb; ++I) {
     const int64_t base = I * PRB;
@@ -651,11 +685,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
     // prologue: steps 0 and 1 in flight while psi is generated
 #pragma unroll
     for (int s0 = 0; s0 < 2; ++s0) {
-      if (s0 < nk) {
-        double* st = lds + s0 * STAGE;
-        dma_rows128(st, Amat, ld, base, (int64_t)s0 * KS, KS, w, lane);
-        dma_rows64(st + KS * PW, Vt, PBM, 0, (int64_t)s0 * KS, KS, w, lane);
-      }
+      if (s0 < nk) dma_step(lds + s0 * STAGE, base, (int64_t)s0 * KS);
     }
     AccP acc;
     {
@@ -710,12 +740,9 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
     // acc += L_I,<I V_<I over 16-deep steps; steps s+1, s+2 in flight during step s
     for (int s = 0; s < nk; ++s) {
       const double* cur = lds + (s % NSTAGE) * STAGE;
-      if (s + 2 < nk) {
-        double* nxt = lds + ((s + 2) % NSTAGE) * STAGE;
-        const int64_t kc = (int64_t)(s + 2) * KS;
-        dma_rows128(nxt, Amat, ld, base, kc, KS, w, lane);
-        dma_rows64(nxt + KS * PW, Vt, PBM, 0, kc, KS, w, lane);
-      }
+#ifndef MFGP_DIAG_NODMA   // diagnostic build: compute on stale LDS (timing only)
+      if (s + 2 < nk) dma_step(lds + ((s + 2) % NSTAGE) * STAGE, base, (int64_t)(s + 2) * KS);
+#endif
       main_mma(cur, cur + KS * PW, acc, w, lane);
       if (s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(GLDS_PER_STEP) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -740,7 +767,9 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
     AccH vh;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
+#ifndef MFGP_DIAG_NODIAG
     half_mma<false>(frag, img, 0, vh, (p16 + 16) / 4, lane);
+#endif
     if (has_b) load_afrag(frag, Amat + fa * NB * ld + fb * NB, ld, p16, lane);   // L_ba
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
@@ -767,7 +796,9 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int v = 0; v < 4; ++v) th.c[nt][v] = img[swz(64 + p16 + q + 4 * v, nt * 16 + r)];
+#ifndef MFGP_DIAG_NODIAG
       half_mma<true>(frag, img, 0, th, 16, lane);
+#endif
       load_afrag(frag, d.Linv + fb * TILE, NB, p16, lane);   // Linv_b
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
@@ -777,7 +808,9 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
       // V_bot = Linv_b T_bot
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
+#ifndef MFGP_DIAG_NODIAG
       half_mma<false>(frag, img, 64, vh, (p16 + 16) / 4, lane);
+#endif
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
