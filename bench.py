@@ -39,8 +39,8 @@ PEAK_F64_TFLOPS = 78.6   # MI355X f64 matrix (= vector) spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--seeds-per-gpu", type=int, default=8)
     p.add_argument("--grid", type=int, default=128)
     p.add_argument("--nl", type=int, default=1024)
@@ -140,8 +140,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    host_t = []
     for s in range(W, total):
+        th = time.perf_counter()
         step(s)
+        host_t.append(time.perf_counter() - th)
     traj = varmax[W:].transpose(0, 1).contiguous()           # [B, K] per-seed VarMax trajectory
     _, agg_mean, agg_std = gather_trajectories(traj, world)   # the single RCCL exchange
     agg = torch.stack([agg_mean, torch.nan_to_num(agg_std)])
@@ -187,6 +190,7 @@ def main():
                 "frac": achieved / PEAK_F64_TFLOPS, "traffic": None,
                 "kernel": "k_predict", "flops_per_launch": flops, "avg_launch_ms": avg_ms,
             },
+            "host_enqueue_ms_per_step": 1e3 * float(np.mean(host_t)),
             "breakdown_ms_per_step": {
                 "predict": tm["predict_ms"] / K, "factor": tm["factor_ms"] / K,
             },

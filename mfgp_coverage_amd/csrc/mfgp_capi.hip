@@ -267,6 +267,9 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.mu = nullptr;
   d.var = nullptr;
   d.status = m->status;
+  d.srcX = nullptr;
+  d.srcY = nullptr;
+  d.k_new = 0;
   d.ld = m->ld;
   d.N = m->NL + m->NH;
   d.NL = m->NL;
@@ -346,6 +349,16 @@ int factor_one(mfgp_model* m) {
 bool factor_current(const mfgp_model* m) {
   return m->factored && m->factor_N == m->NL + m->NH && m->factor_jitter == m->jitter &&
          std::memcmp(m->factor_hyp, m->hyp, sizeof(m->hyp)) == 0;
+}
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
 }
 
 int copy_rows(mfgp_model* m, int64_t at, const double* X, const double* y, int64_t k) {
@@ -648,15 +661,19 @@ int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, c
     if (models[i]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
     if (k && k[i] < 0) return set_err(MFGP_ERR_ARG, "negative k");
   }
-  // append new rows
+  // append new rows: device-resident sources are copied by one k_append launch
+  // per sub-batch (below); host sources by plain copies here
+  const bool dev_src = is_device_ptr(X) && is_device_ptr(y);
+  std::vector<int64_t> src_off(count, 0);
   int64_t off = 0, out_off = 0;
   for (int i = 0; i < count; ++i) {
     mfgp_model* m = models[i];
     const int64_t ki = k ? k[i] : 0;
     const int64_t n = m->NL + m->NH;
     if ((rc = ensure_cap(m, n + ki))) return rc;
+    src_off[i] = off;
     if (ki > 0) {
-      if ((rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
+      if (!dev_src && (rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
       m->NH += ki;
     }
     off += ki;
@@ -682,9 +699,15 @@ int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, c
       hd[i].mu = mu + out_off;
       hd[i].var = var + out_off;
       out_off += m->M;
+      if (dev_src && k && k[b0 + i] > 0) {
+        hd[i].srcX = X + 2 * src_off[b0 + i];
+        hd[i].srcY = y + src_off[b0 + i];
+        hd[i].k_new = k[b0 + i];
+      }
     }
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb, &dd))) return rc;
+    if (dev_src) HIP_TRY(launch_append(dd, nb, c->stream));
     if ((rc = enqueue_factor(c, dd, hd, nb))) return rc;
     if ((rc = enqueue_predict(c, dd, hd, nb))) return rc;
     if ((rc = release_slot(c, slot))) return rc;

@@ -39,6 +39,9 @@ struct GPDesc {
   double* mu;          // [M]
   double* var;         // [M]
   int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
+  const double* srcX;  // device rows to append at row N - k_new (k_append), or null
+  const double* srcY;
+  int64_t k_new;
   int64_t ld, N, NL, M;
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
@@ -50,6 +53,7 @@ inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1)
 inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1) / PRB; }
 
 // Launchers (mfgp_kernels.hip). `d` points to `count` descriptors in device memory.
+hipError_t launch_append(const GPDesc* d, int count, hipStream_t s);
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);
 hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, hipStream_t s);
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);

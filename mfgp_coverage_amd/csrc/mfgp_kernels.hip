@@ -856,7 +856,26 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
   }
 }
 
+// Append the batch's new (device-resident) rows to every model's training set:
+// one launch for the whole batch instead of two copies per model.
+__global__ __launch_bounds__(64) void k_append(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.x];
+  const int64_t k = d.k_new;
+  if (k <= 0) return;
+  double* X = const_cast<double*>(d.X);
+  double* y = const_cast<double*>(d.y);
+  const int64_t at = d.N - k;
+  for (int64_t e = threadIdx.x; e < 3 * k; e += 64) {
+    if (e < 2 * k) X[2 * at + e] = d.srcX[e];
+    else y[at + e - 2 * k] = d.srcY[e - 2 * k];
+  }
+}
+
 // ---------------------------------------------------------------------------
+hipError_t launch_append(const GPDesc* d, int count, hipStream_t s) {
+  hipLaunchKernelGGL(k_append, dim3(count), dim3(64), 0, s, d);
+  return hipGetLastError();
+}
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s) {
   hipLaunchKernelGGL(k_assemble, dim3((unsigned)max_tiles, count), dim3(NT), 0, s, d);
   return hipGetLastError();

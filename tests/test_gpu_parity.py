@@ -222,8 +222,10 @@ def test_larger_vs_oracle(gp, kind, G, N, NL):
     _check(mu, cov, mu_r, var_r, hyp)
 
 
-def test_batched_ragged_vs_single(gp):
-    """mfgp_batch_append_predict over GPs of different N and M equals per-model results."""
+@pytest.mark.parametrize("src", ["host", "device"])
+def test_batched_ragged_vs_single(gp, src):
+    """mfgp_batch_append_predict over GPs of different N and M equals per-model results
+    (new rows from host memory -> copies; from device memory -> the k_append kernel)."""
     import ctypes
 
     from mfgp_coverage_amd import _lib
@@ -247,8 +249,12 @@ def test_batched_ragged_vs_single(gp):
     import torch
     mu_d = torch.empty(tot, dtype=torch.float64, device="cuda")
     var_d = torch.empty(tot, dtype=torch.float64, device="cuda")
-    _lib.batch_append_predict(models, Xn.ctypes.data, yn.ctypes.data, [c[3] for c in cases],
-                              mu_d.data_ptr(), var_d.data_ptr())
+    if src == "host":
+        xp, yp = Xn.ctypes.data, yn.ctypes.data
+    else:
+        Xd, yd = torch.from_numpy(Xn).cuda(), torch.from_numpy(yn).cuda()
+        xp, yp = Xd.data_ptr(), yd.data_ptr()
+    _lib.batch_append_predict(models, xp, yp, [c[3] for c in cases], mu_d.data_ptr(), var_d.data_ptr())
     mu, var = mu_d.cpu().numpy(), var_d.cpu().numpy()
     off = 0
     for (mu_r, var_r), M in zip(refs, Ms):
