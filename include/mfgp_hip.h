@@ -101,7 +101,12 @@ int mfgp_get_factor(mfgp_model* m, double* L_out);
  * order). One set of launches serves the whole batch. flags: MFGP_ASYNC. */
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y,
                               const int64_t* k, double* mu, double* var, int flags);
-/* Drop the last `k` hifi rows of each model without refactoring (benchmark reset). */
+/* The two halves of mfgp_batch_append_predict (append + refactor only; predict
+ * from the current factors only). mfgp_batch_predict needs a current factor. */
+int mfgp_batch_append_factor(mfgp_model** models, int count, const double* X, const double* y,
+                             const int64_t* k, int flags);
+int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, int flags);
+/* Keep only the first n_keep_hifi hifi rows (no refactor; benchmark reset). */
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi);
 
 const char* mfgp_last_error(void);

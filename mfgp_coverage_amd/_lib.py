@@ -49,6 +49,10 @@ SIGNATURES = {
     "mfgp_batch_append_predict": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p,
                                                  ctypes.c_void_p, _c_int64_p, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_int]),
+    "mfgp_batch_append_factor": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_void_p, _c_int64_p, ctypes.c_int]),
+    "mfgp_batch_predict": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int]),
     "mfgp_truncate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "mfgp_last_error": (ctypes.c_char_p, []),
     "mfgp_version": (ctypes.c_char_p, []),
@@ -238,3 +242,20 @@ def batch_append_predict(models, X, y, k, mu_ptr, var_ptr, asynchronous=False):
                                          ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
                                          ASYNC if asynchronous else 0)
     check(rc)
+
+
+def batch_append_factor(models, X, y, k, asynchronous=False):
+    """Append + refactor a batch (device or host row pointers); no predict."""
+    n = len(models)
+    arr = (ctypes.c_void_p * n)(*[m.handle.value for m in models])
+    ks = (ctypes.c_int64 * n)(*[int(v) for v in k])
+    check(lib().mfgp_batch_append_factor(arr, n, ctypes.c_void_p(X), ctypes.c_void_p(y), ks,
+                                         ASYNC if asynchronous else 0))
+
+
+def batch_predict(models, mu_ptr, var_ptr, asynchronous=False):
+    """Posterior mean / variance of a batch from its current factors."""
+    n = len(models)
+    arr = (ctypes.c_void_p * n)(*[m.handle.value for m in models])
+    check(lib().mfgp_batch_predict(arr, n, ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
+                                   ASYNC if asynchronous else 0))

@@ -290,12 +290,14 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int rc = ev_begin(c, ev, 1);
   if (rc) return rc;
   HIP_TRY(launch_assemble(dd, count, max_tiles, c->stream));
+  // Blocked right-looking Cholesky, per 64-column step: diagonal factor +
+  // inverse (k_potrf_diag), panel (k_panel), trailing update (k_syrk).
   for (int kb = 0; kb < max_nb; ++kb) {
-    HIP_TRY(launch_potrf_diag(dd, count, kb, c->stream));
+    HIP_TRY(launch_potrf_diag(dd, count, kb, 0, c->stream));
     const int64_t below = max_nb - kb - 1;
     if (below > 0) {
       HIP_TRY(launch_panel(dd, count, kb, below, c->stream));
-      HIP_TRY(launch_syrk(dd, count, kb, below * (below + 1) / 2, c->stream));
+      HIP_TRY(launch_syrk(dd, count, kb, below * (below + 1) / 2, 0, c->stream));
     }
   }
   return ev_end(c, ev);
@@ -651,8 +653,10 @@ int mfgp_get_factor(mfgp_model* m, double* L_out) {
   return MFGP_OK;
 }
 
-int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
-                              double* mu, double* var, int flags) {
+// Shared driver of the batched entry points: append (optional), factor
+// (do_factor) and predict (do_predict) `count` models with one set of launches.
+static int batch_run(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
+                     double* mu, double* var, int flags, bool do_factor, bool do_predict) {
   if (!models || count <= 0) return set_err(MFGP_ERR_ARG, "empty batch");
   mfgp_ctx* c = models[0]->ctx;
   int rc = MFGP_OK;
@@ -660,33 +664,40 @@ int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, c
     if ((rc = check_model(models[i]))) return rc;
     if (models[i]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
     if (k && k[i] < 0) return set_err(MFGP_ERR_ARG, "negative k");
+    if (!do_factor && !factor_current(models[i]))
+      return set_err(MFGP_ERR_ARG, "model %d has no current factor (call mfgp_batch_append_factor first)", i);
   }
+  if (do_predict && (!mu || !var)) return set_err(MFGP_ERR_ARG, "null output");
   // append new rows: device-resident sources are copied by one k_append launch
   // per sub-batch (below); host sources by plain copies here
-  const bool dev_src = is_device_ptr(X) && is_device_ptr(y);
+  const bool has_new = do_factor && k && X && y;
+  const bool dev_src = has_new && is_device_ptr(X) && is_device_ptr(y);
   std::vector<int64_t> src_off(count, 0);
   int64_t off = 0, out_off = 0;
-  for (int i = 0; i < count; ++i) {
-    mfgp_model* m = models[i];
-    const int64_t ki = k ? k[i] : 0;
-    const int64_t n = m->NL + m->NH;
-    if ((rc = ensure_cap(m, n + ki))) return rc;
-    src_off[i] = off;
-    if (ki > 0) {
-      if (!dev_src && (rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
-      m->NH += ki;
+  if (do_factor) {
+    for (int i = 0; i < count; ++i) {
+      mfgp_model* m = models[i];
+      const int64_t ki = has_new ? k[i] : 0;
+      const int64_t n = m->NL + m->NH;
+      if ((rc = ensure_cap(m, n + ki))) return rc;
+      src_off[i] = off;
+      if (ki > 0) {
+        if (!dev_src && (rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
+        m->NH += ki;
+      }
+      off += ki;
     }
-    off += ki;
   }
-  // workspace: V scratch for every model of a sub-batch
   for (int b0 = 0; b0 < count; b0 += MAXB) {
     const int nb = std::min(MAXB, count - b0);
     size_t need = 0;
-    for (int i = 0; i < nb; ++i) {
-      mfgp_model* m = models[b0 + i];
-      need += v_bytes(m->M, m->NL + m->NH);
+    if (do_predict) {
+      for (int i = 0; i < nb; ++i) {
+        mfgp_model* m = models[b0 + i];
+        need += v_bytes(m->M, m->NL + m->NH);
+      }
+      if ((rc = ensure_ws(c, need))) return rc;   // V scratch for every model of the sub-batch
     }
-    if ((rc = ensure_ws(c, need))) return rc;
     int slot;
     GPDesc* hd = acquire_slot(c, slot, rc);
     if (!hd) return rc;
@@ -694,12 +705,14 @@ int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, c
     for (int i = 0; i < nb; ++i) {
       mfgp_model* m = models[b0 + i];
       fill_desc(hd[i], m);
-      hd[i].V = reinterpret_cast<double*>(reinterpret_cast<char*>(c->ws) + vo);
-      vo += v_bytes(m->M, m->NL + m->NH);
-      hd[i].mu = mu + out_off;
-      hd[i].var = var + out_off;
-      out_off += m->M;
-      if (dev_src && k && k[b0 + i] > 0) {
+      if (do_predict) {
+        hd[i].V = reinterpret_cast<double*>(reinterpret_cast<char*>(c->ws) + vo);
+        vo += v_bytes(m->M, m->NL + m->NH);
+        hd[i].mu = mu + out_off;
+        hd[i].var = var + out_off;
+        out_off += m->M;
+      }
+      if (dev_src && k[b0 + i] > 0) {
         hd[i].srcX = X + 2 * src_off[b0 + i];
         hd[i].srcY = y + src_off[b0 + i];
         hd[i].k_new = k[b0 + i];
@@ -708,20 +721,36 @@ int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, c
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb, &dd))) return rc;
     if (dev_src) HIP_TRY(launch_append(dd, nb, c->stream));
-    if ((rc = enqueue_factor(c, dd, hd, nb))) return rc;
-    if ((rc = enqueue_predict(c, dd, hd, nb))) return rc;
+    if (do_factor && (rc = enqueue_factor(c, dd, hd, nb))) return rc;
+    if (do_predict && (rc = enqueue_predict(c, dd, hd, nb))) return rc;
     if ((rc = release_slot(c, slot))) return rc;
-    for (int i = 0; i < nb; ++i) {
-      mfgp_model* m = models[b0 + i];
-      m->factored = true;
-      m->factor_N = m->NL + m->NH;
-      std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
-      m->factor_jitter = m->jitter;
-      c->async_status.push_back(m->status);
+    if (do_factor) {
+      for (int i = 0; i < nb; ++i) {
+        mfgp_model* m = models[b0 + i];
+        m->factored = true;
+        m->factor_N = m->NL + m->NH;
+        std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
+        m->factor_jitter = m->jitter;
+        c->async_status.push_back(m->status);
+      }
     }
   }
   if (flags & MFGP_ASYNC) return MFGP_OK;
   return mfgp_ctx_synchronize(c);
+}
+
+int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
+                              double* mu, double* var, int flags) {
+  return batch_run(models, count, X, y, k, mu, var, flags, true, true);
+}
+
+int mfgp_batch_append_factor(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
+                             int flags) {
+  return batch_run(models, count, X, y, k, nullptr, nullptr, flags, true, false);
+}
+
+int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, int flags) {
+  return batch_run(models, count, nullptr, nullptr, nullptr, mu, var, flags, false, true);
 }
 
 }  // extern "C"

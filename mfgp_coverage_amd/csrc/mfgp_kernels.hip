@@ -132,6 +132,36 @@ __device__ __forceinline__ void store_tile(double* __restrict__ Ts, const Stage&
   }
 }
 
+constexpr int PW = 128;                  // row width of the predict L image (= PRB)
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+__device__ __forceinline__ int swzp(int k, int i) { return k * PW + (i ^ ((k & 1) << 4)); }
+
+// DMA kn rows of 128 doubles into a swizzled [kn][128] LDS image:
+// dst[swzp(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves one 1 KB row.
+__device__ __forceinline__ void dma_rows128(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
+                                            int64_t c0, int kn, int w, int lane) {
+  for (int k = w; k < kn; k += PNT / 64) {
+    const int i = (2 * lane) ^ ((k & 1) << 4);
+    const double* src = G + (c0 + k) * ld + r0 + i;
+    __builtin_amdgcn_global_load_lds((const GLOBAL void*)src, (lds_vptr)(dst + k * PW), 16, 0, 0);
+  }
+}
+
+// DMA kn rows of 64 doubles into a swizzled [kn][64] LDS image:
+// dst[swz(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves two rows.
+__device__ __forceinline__ void dma_rows64(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
+                                           int64_t c0, int kn, int w, int lane) {
+  for (int p = w; p < kn / 2; p += PNT / 64) {
+    const int k = 2 * p + (lane >> 5);
+    const int i = ((lane & 31) * 2) ^ ((k & 1) << 4);
+    const double* src = G + (c0 + k) * ld + r0 + i;
+    __builtin_amdgcn_global_load_lds((const GLOBAL void*)src, (lds_vptr)(dst + 2 * p * NB), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // C/D element (mt, nt, v) of this lane <-> tile (row, col).
 __device__ __forceinline__ int acc_row(int wm, int mt, int q, int v) { return wm * 32 + mt * 16 + q + 4 * v; }
 __device__ __forceinline__ int acc_col(int wn, int nt, int r) { return wn * 32 + nt * 16 + r; }
@@ -410,16 +440,48 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
   }
 }
 
-__global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb) {
+// With `upd`, the tile first receives the last trailing update of the previous
+// step, A_kk -= L_k,k-1 L_k,k-1^T (f64 MFMA), so that the rest of that trailing
+// update can run concurrently on the side stream (look-ahead, see capi).
+__global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb, int upd) {
   const GPDesc& d = descs[blockIdx.x];
   const int64_t N = d.N, ld = d.ld;
   if (kb >= nblocks_factor(N)) return;
-  __shared__ double S[NB * SP], R[NB * SP], T[(NB / DB) * DB * DP], U[(NB / DB - 1) * DB * DP];
-  const int tid = threadIdx.x;
+  // one LDS array: As/Bs of the update (2 x 32 KB) alias S/R/T/U of the factor
+  __shared__ double sh[2 * NB * SP + (NB / DB) * DB * DP + (NB / DB - 1) * DB * DP];
+  double* const S = sh;
+  double* const R = sh + NB * SP;
+  double* const T = R + NB * SP;
+  double* const U = T + (NB / DB) * DB * DP;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int64_t o = (int64_t)kb * NB;
   double* __restrict__ A = d.A;
   STAMP(0);
-  {
+  if (upd && kb > 0) {
+    double* As = sh;
+    load_tile_cm(As, A, ld, o, o - NB, tid);   // L_k,k-1 (A operand and, transposed, B operand)
+    const int r = lane & 15, q = lane >> 4;
+    Acc acc;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          acc.c[mt][nt][v] = A[(o + acc_col(wn, nt, r)) * ld + o + acc_row(wm, mt, q, v)];
+    __syncthreads();
+    tile_mma<true>(As, As, acc, wm, wn, lane);
+    __syncthreads();   // As is overwritten by S below
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int i = acc_row(wm, mt, q, v), j = acc_col(wn, nt, r);
+          S[i * SP + j] = (j <= i) ? acc.c[mt][nt][v] : 0.0;
+        }
+  } else {
     // unconditional loads (the upper part of the tile is masked afterwards) keep
     // all 16 loads per thread in flight
     double v[NB * NB / NT];
@@ -475,12 +537,86 @@ __global__ __launch_bounds__(NT) void k_panel(const GPDesc* __restrict__ descs, 
       }
 }
 
+// Step kb of the blocked Cholesky in one launch: every workgroup factors and
+// inverts the diagonal tile (redundantly -- it is latency, not work, that matters
+// here) and then forms one panel tile L_ik = A_ik Linv_kk^T; workgroup 0 also
+// writes L_kk and Linv_kk. Grid (max(1, tiles below), batch). The A_ik tile
+// streams into LDS by DMA while the diagonal factor runs.
+__global__ __launch_bounds__(NT) void k_panel_diag(const GPDesc* __restrict__ descs, int kb) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t N = d.N, ld = d.ld;
+  const int64_t nb = nblocks_factor(N);
+  if (kb >= nb) return;
+  const int64_t ib = kb + 1 + (int64_t)blockIdx.x;
+  const bool do_panel = ib < nb;
+  if (!do_panel && blockIdx.x > 0) return;
+  __shared__ double sh[2 * NB * SP + (NB / DB) * DB * DP + (NB / DB - 1) * DB * DP + TILE];
+  double* const S = sh;
+  double* const R = sh + NB * SP;
+  double* const T = R + NB * SP;
+  double* const U = T + (NB / DB) * DB * DP;
+  double* const As = U + (NB / DB - 1) * DB * DP;   // A_ik image [k][i] (DMA)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t o = (int64_t)kb * NB;
+  double* __restrict__ A = d.A;
+  if (do_panel) dma_rows64(As, A, ld, ib * NB, o, NB, w, lane);
+  {
+    double v[NB * NB / NT];
+#pragma unroll
+    for (int t = 0; t < NB * NB / NT; ++t) {
+      const int e = tid + t * NT, i = e & 63, j = e >> 6;
+      v[t] = A[(o + j) * ld + o + i];
+    }
+#pragma unroll
+    for (int t = 0; t < NB * NB / NT; ++t) {
+      const int e = tid + t * NT, i = e & 63, j = e >> 6;
+      S[i * SP + j] = (j <= i) ? v[t] : 0.0;
+    }
+  }
+  __syncthreads();
+  factor_invert_64(S, R, T, U, o, N, d.status);
+  if (blockIdx.x == 0) {
+    double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
+#pragma unroll 4
+    for (int e = tid; e < NB * NB; e += NT) {
+      const int i = e & 63, j = e >> 6;
+      A[(o + j) * ld + o + i] = S[i * SP + j];
+      Li[j * NB + i] = R[i * SP + j];
+    }
+  }
+  if (!do_panel) return;
+  __syncthreads();   // S is free
+  // Bs[m][j] = Linv[j][m] (swizzled k-major image in the S region)
+  for (int e = tid; e < NB * NB; e += NT) {
+    const int m = e >> 6, j = e & 63;
+    S[swz(m, j)] = R[j * SP + m];
+  }
+  vm_wait_all();     // the A_ik DMA has landed
+  __syncthreads();
+  Acc acc;
+  acc_zero(acc);
+  tile_mma<false>(As, S, acc, wm, wn, lane);
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
+        A[(o + col) * ld + ib * NB + row] = acc.c[mt][nt][v];
+      }
+}
+
 // Trailing update: A_ij -= L_ik L_jk^T for kb < j <= i (lower tiles only).
-__global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, int kb) {
+// Trailing tiles t0, t0+1, ... of step kb (t0 = 1 skips tile (kb+1, kb+1), which
+// the look-ahead diagonal kernel updates itself).
+__global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, int kb, int t0) {
   const GPDesc& d = descs[blockIdx.y];
   const int64_t nb = nblocks_factor(d.N);
   const int64_t T = nb - kb - 1;
-  const int64_t t = blockIdx.x;
+  const int64_t t = blockIdx.x + (int64_t)t0;
   if (T <= 0 || t >= T * (T + 1) / 2) return;
   int ii, jj;
   tri_index(t, ii, jj);
@@ -537,37 +673,9 @@ __global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, i
 // the second workgroup on the CU hides each one's psi / diagonal phases.
 // ---------------------------------------------------------------------------
 constexpr int KS = 16;                   // K depth of one pipeline step
-constexpr int PW = 128;                  // row width of the L image (= PRB)
 constexpr int NSTAGE = 3;
 constexpr int STAGE = KS * PW + KS * PBM;   // doubles per stage: As [KS][128] + Bs [KS][64]
 constexpr int GLDS_PER_STEP = (KS + KS * PBM / 128) / (PNT / 64);   // per wave: 4 (L) + 2 (V)
-
-typedef __attribute__((address_space(3))) void* lds_vptr;
-
-__device__ __forceinline__ int swzp(int k, int i) { return k * PW + (i ^ ((k & 1) << 4)); }
-
-// DMA kn rows of 128 doubles into a swizzled [kn][128] LDS image:
-// dst[swzp(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves one 1 KB row.
-__device__ __forceinline__ void dma_rows128(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
-                                            int64_t c0, int kn, int w, int lane) {
-  for (int k = w; k < kn; k += PNT / 64) {
-    const int i = (2 * lane) ^ ((k & 1) << 4);
-    const double* src = G + (c0 + k) * ld + r0 + i;
-    __builtin_amdgcn_global_load_lds((const GLOBAL void*)src, (lds_vptr)(dst + k * PW), 16, 0, 0);
-  }
-}
-
-// DMA kn rows of 64 doubles into a swizzled [kn][64] LDS image:
-// dst[swz(k, i)] = G[(c0 + k) * ld + r0 + i]. One wave-instruction moves two rows.
-__device__ __forceinline__ void dma_rows64(double* dst, const double* __restrict__ G, int64_t ld, int64_t r0,
-                                           int64_t c0, int kn, int w, int lane) {
-  for (int p = w; p < kn / 2; p += PNT / 64) {
-    const int k = 2 * p + (lane >> 5);
-    const int i = ((lane & 31) * 2) ^ ((k & 1) << 4);
-    const double* src = G + (c0 + k) * ld + r0 + i;
-    __builtin_amdgcn_global_load_lds((const GLOBAL void*)src, (lds_vptr)(dst + 2 * p * NB), 16, 0, 0);
-  }
-}
 
 // Buffer-descriptor LDS-DMA (buffer_load_dwordx4 ... lds): the lane part of the
 // source offset is a VGPR fixed for the whole kernel, the row/step part an SGPR,
@@ -580,7 +688,6 @@ __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, double* dst, 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr)dst, 16, voff, soff, 0, 0);
 }
 
-__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Main-loop accumulator: wave wm owns rows wm*32.. x all 64 cells.
 struct AccP {
@@ -880,16 +987,20 @@ hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStr
   hipLaunchKernelGGL(k_assemble, dim3((unsigned)max_tiles, count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
-hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, hipStream_t s) {
-  hipLaunchKernelGGL(k_potrf_diag, dim3(count), dim3(NT), 0, s, d, kb);
+hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStream_t s) {
+  hipLaunchKernelGGL(k_potrf_diag, dim3(count), dim3(NT), 0, s, d, kb, upd);
+  return hipGetLastError();
+}
+hipError_t launch_panel_diag(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s) {
+  hipLaunchKernelGGL(k_panel_diag, dim3((unsigned)(max_below > 0 ? max_below : 1), count), dim3(NT), 0, s, d, kb);
   return hipGetLastError();
 }
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s) {
   hipLaunchKernelGGL(k_panel, dim3((unsigned)max_below, count), dim3(NT), 0, s, d, kb);
   return hipGetLastError();
 }
-hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, hipStream_t s) {
-  hipLaunchKernelGGL(k_syrk, dim3((unsigned)max_tri, count), dim3(NT), 0, s, d, kb);
+hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s) {
+  hipLaunchKernelGGL(k_syrk, dim3((unsigned)max_tri, count), dim3(NT), 0, s, d, kb, t0);
   return hipGetLastError();
 }
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {

@@ -39,3 +39,4 @@ def gather_trajectories(traj, world: int, group=None):
     mean = allt.mean(0)
     std = allt.std(0, unbiased=True) if allt.shape[0] > 1 else torch.full_like(mean, float("nan"))
     return allt, mean, std
+
