@@ -52,6 +52,24 @@ def parse():
     return p.parse_args()
 
 
+def pmc_traffic(kernel="k_predict"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary (profiles/<round>_hbm_traffic.csv, written by tools/summarize_profile.py
+    from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x2 per the gfx950
+    correction of MI355X_MICROARCH.md section HBM)."""
+    import glob
+    import csv
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.csv")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Name"]:
+                tot = float(row["fetch_bytes_corrected"]) + float(row["write_bytes"])
+                return tot, os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def cpu_baseline(wl, hyp, s, NL, NH0, k, reps=3):
     """Time the oracle on one seed's update (same inputs as step s)."""
     from oracle import gp_oracle as O
@@ -165,6 +183,7 @@ def main():
         flops = B * (M * N * N + 4 * M * N)
         avg_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
         achieved = flops / (avg_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic()
         out = {
             "metric": METRIC,
             "value": world * B * K / elapsed,
@@ -187,7 +206,7 @@ def main():
             },
             "roofline": {
                 "bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / PEAK_F64_TFLOPS, "traffic": None,
+                "frac": achieved / PEAK_F64_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "k_predict", "flops_per_launch": flops, "avg_launch_ms": avg_ms,
             },
             "host_enqueue_ms_per_step": 1e3 * float(np.mean(host_t)),
