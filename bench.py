@@ -4,17 +4,28 @@ Workload (BASELINE.json configs[3], "australia8 MFGP, 8 agents x 64 Monte-Carlo
 seeds sharded over 8 MI355X"): each rank owns B = 8 independent seeds (one MF GP
 each, australia8_mf hyperparameters). One step = one GP posterior update of
 every seed (simulator.py:888-892): append the k = 8 agents' new hifi samples to
-N_L = 1024 lofi + 1016 hifi points (N = 2048), refactor from scratch, and
-compute the posterior mean and variance at all M = 16384 grid cells. Inputs are
+N_L = 1024 lofi + 1016 hifi points (N = 2048), update the factor, and compute
+the posterior mean and variance at all M = 16384 grid cells. Inputs are
 resident in HBM before the timed region. After the timed steps each rank's
 per-seed max-variance trajectory (the VarMax log, simulator.py:925) is
 all-gathered over RCCL for the loss/variance aggregation of runner.py:144-147.
 
+Two update paths are timed back to back on the same workload, with identical
+results (tests/test_gpu_incremental.py):
+  value          -- the library's default path: bordered-Cholesky append of the
+                    k rows (k_inc_factor) and one pass over the resident
+                    V = L^-1 psi^T for mean/variance at every cell (k_vstream);
+  full_recompute -- what the reference does per update: full refactor
+                    (k_assemble/potrf/panel/syrk) and V recomputed from scratch
+                    (k_predict).
+
 value = (ranks x seeds x steps) / max-over-ranks wall time.
-roofline: the fused predict kernel (dominant), algorithmic f64 flops per launch
-  = B x (M*N^2 + 4*M*N) [V = L^-1 psi^T triangular solve + mean/variance
-  reductions], over its average launch time measured with HIP events on the
-  launch stream; peak = MI355X f64 MFMA spec.
+roofline (value): k_vstream, HBM-bound; algorithmic bytes per launch =
+  B x 8 x [M (n0 + k + 4) + n0 (k + 1)] (V_old read once, V_new + mu + var
+  written, grid read; L21 and z once) over its average launch time (HIP events
+  on the launch stream); peak = MI355X HBM3E 8 TB/s.
+roofline (full_recompute): k_predict, MFMA-bound; B x (M N^2 + 4 M N) f64 flops
+  per launch; peak = MI355X f64 MFMA spec.
 cpu_baseline: the oracle's diag-only NumPy restatement (Cholesky, triangular
   solves, row-sum of squares) on one seed's update, on the host cores
   (rank 0, N = 1 only); the reference-faithful op sequence is timed beside it.
@@ -34,6 +45,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GP posterior updates/sec (128×128 grid, N_train=2048) at 1/2/4/8 MI355X"
 PEAK_F64_TFLOPS = 78.6   # MI355X f64 matrix (= vector) spec
+PEAK_HBM_GBS = 8000.0    # MI355X HBM3E
 
 
 def parse():
@@ -49,6 +61,7 @@ def parse():
     p.add_argument("--hyp", default="australia8_mf")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-faithful", type=int, default=1, help="also time the reference-faithful op sequence")
+    p.add_argument("--no-full", action="store_true", help="skip the full-recompute comparison run")
     return p.parse_args()
 
 
@@ -116,9 +129,10 @@ def main():
     from mfgp_coverage_amd.ensemble import gather_trajectories, shard_seeds
 
     _lib.set_device(local)
-    ctx = _lib.context()
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)
+    # one explicit stream for the library's launches and torch's reductions
+    # (the null stream would not order against the library's non-blocking stream)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     B, G, NL, NH, k = a.seeds_per_gpu, a.grid, a.nl, a.nh, a.agents
     NH0 = NH - k
@@ -127,63 +141,86 @@ def main():
     hyp = synthetic.HYP[a.hyp]
     M = G * G
     N = NL + NH
-    wls, models = [], []
-    for seed in shard_seeds(world * B, world, rank):
-        wl = synthetic.Workload(G, NL, NH0, k, total, seed=seed)
-        mdl = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
-        mdl.set_grid(wl.xs)
-        mdl.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
-        wls.append(wl)
-        models.append(mdl)
+    wls = [synthetic.Workload(G, NL, NH0, k, total, seed=seed) for seed in shard_seeds(world * B, world, rank)]
     Xnew = torch.from_numpy(np.ascontiguousarray(np.stack([w.Xnew for w in wls], 1).reshape(total, B * k, 2))).to(dev)
     ynew = torch.from_numpy(np.ascontiguousarray(np.stack([w.ynew for w in wls], 1).reshape(total, B * k))).to(dev)
     mu = torch.empty(B * M, dtype=torch.float64, device=dev)
     var = torch.empty(B * M, dtype=torch.float64, device=dev)
-    varmax = torch.zeros(total, B, dtype=torch.float64, device=dev)
     ks = [k] * B
 
-    def step(s):
-        for mdl in models:
-            mdl.truncate(NH0)
-        _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), ks, mu.data_ptr(),
-                                  var.data_ptr(), asynchronous=True)
-        varmax[s] = var.view(B, M).amax(dim=1)
+    def run(incremental):
+        ctx = _lib.context() if incremental else _lib.Context(local)
+        ctx.set_stream(stream.cuda_stream)
+        ctx.set_incremental(incremental)
+        models = []
+        for wl in wls:
+            mdl = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
+            mdl.set_grid(wl.xs)
+            mdl.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
+            models.append(mdl)
+        varmax = torch.zeros(total, B, dtype=torch.float64, device=dev)
 
-    for s in range(W):
-        step(s)
-    ctx.synchronize()
-    ctx.enable_timing(True)
-    ctx.reset_timing()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    host_t = []
-    for s in range(W, total):
-        th = time.perf_counter()
-        step(s)
-        host_t.append(time.perf_counter() - th)
-    traj = varmax[W:].transpose(0, 1).contiguous()           # [B, K] per-seed VarMax trajectory
-    _, agg_mean, agg_std = gather_trajectories(traj, world)   # the single RCCL exchange
-    agg = torch.stack([agg_mean, torch.nan_to_num(agg_std)])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    ctx.synchronize()   # raises LinAlgError if any factor was not positive definite
-    tm = ctx.timing()
-    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    if not os.environ.get("MFGP_LIB"):   # diagnostic library builds compute garbage on purpose
-        assert torch.isfinite(agg).all()
+        def step(s):
+            for mdl in models:
+                mdl.truncate(NH0)
+            _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), ks, mu.data_ptr(),
+                                      var.data_ptr(), asynchronous=True)
+            varmax[s] = var.view(B, M).amax(dim=1)
+
+        def aggregate(traj):
+            _, agg_mean, agg_std = gather_trajectories(traj, world)   # the single RCCL exchange
+            return torch.stack([agg_mean, torch.nan_to_num(agg_std)])
+
+        for s in range(W):
+            step(s)
+        aggregate(varmax[:W].transpose(0, 1).contiguous())   # first-use kernel loads / communicator setup
+        ctx.synchronize()
+        ctx.enable_timing(True)
+        ctx.reset_timing()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        host_t = []
+        for s in range(W, total):
+            th = time.perf_counter()
+            step(s)
+            host_t.append(time.perf_counter() - th)
+        traj = varmax[W:].transpose(0, 1).contiguous()           # [B, K] per-seed VarMax trajectory
+        agg = aggregate(traj)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        ctx.synchronize()   # raises LinAlgError if any factor was not positive definite
+        ctx.enable_timing(False)
+        tm = ctx.timing()
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        if not os.environ.get("MFGP_LIB"):   # diagnostic library builds compute garbage on purpose
+            assert torch.isfinite(agg).all()
+        st = models[0].stats()
+        del models
+        return {"elapsed": float(el.item()), "tm": tm, "host_ms": 1e3 * float(np.mean(host_t)), "stats": st,
+                "traj": traj.cpu().numpy()}
+
+    inc = run(True)
+    full = None if a.no_full else run(False)
+    if os.environ.get("MFGP_BENCH_DUMP") and rank == 0:
+        np.savez(os.environ["MFGP_BENCH_DUMP"], inc=inc["traj"], full=full["traj"] if full else inc["traj"])
+    if full is not None and rank == 0 and not os.environ.get("MFGP_LIB"):
+        # the two paths produce the same posterior (VarMax trajectories to rounding)
+        np.testing.assert_allclose(inc["traj"], full["traj"], rtol=1e-9)
 
     if rank == 0:
-        flops = B * (M * N * N + 4 * M * N)
-        avg_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
-        achieved = flops / (avg_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic()
+        elapsed, tm = inc["elapsed"], inc["tm"]
+        assert inc["stats"]["inc_factor"] >= K and inc["stats"]["vstream"] >= K, inc["stats"]
+        n0 = N - k
+        vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (k + 1))
+        v_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
+        v_gbs = vbytes / (v_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic("k_vstream")
         out = {
             "metric": METRIC,
             "value": world * B * K / elapsed,
@@ -200,20 +237,39 @@ def main():
             "config": {
                 "workload": f"{a.hyp} MFGP seed ensemble (BASELINE configs[3]): {B} seeds/GPU, "
                             f"{G}x{G} grid (M={M}), N_L={NL} lofi + N_H={NH} hifi ({NH0} + {k} new agent "
-                            f"samples appended per update), full refactor + mean/var at every cell, fp64",
+                            f"samples appended per update), factor update + mean/var at every cell, fp64",
+                "update": "incremental: bordered-Cholesky append (k_inc_factor) + one pass over the resident "
+                          "V = L^-1 psi^T (k_vstream); full_recompute below is the reference's per-update work",
                 "seeds_per_gpu": B, "grid": G, "N_train": N, "N_lofi": NL, "N_hifi": NH, "agents": k,
                 "global_seeds": world * B, "parallelism": f"seed-sharded x{world}, 1 RCCL all_gather",
             },
             "roofline": {
-                "bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / PEAK_F64_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "k_predict", "flops_per_launch": flops, "avg_launch_ms": avg_ms,
+                "bound": "hbm", "achieved": v_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": v_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": "k_vstream", "bytes_per_launch": vbytes, "avg_launch_ms": v_ms,
             },
-            "host_enqueue_ms_per_step": 1e3 * float(np.mean(host_t)),
+            "host_enqueue_ms_per_step": inc["host_ms"],
             "breakdown_ms_per_step": {
                 "predict": tm["predict_ms"] / K, "factor": tm["factor_ms"] / K,
             },
         }
+        if full is not None:
+            ft = full["tm"]
+            flops = B * (M * N * N + 4 * M * N)
+            avg_ms = ft["predict_ms"] / max(1, ft["predict_launches"])
+            achieved = flops / (avg_ms * 1e-3) / 1e12
+            ftraffic, _ = pmc_traffic("k_predict")
+            out["full_recompute"] = {
+                "value": world * B * K / full["elapsed"],
+                "ms_per_step": full["elapsed"] / K * 1e3,
+                "roofline": {
+                    "bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / PEAK_F64_TFLOPS, "traffic": ftraffic,
+                    "kernel": "k_predict", "flops_per_launch": flops, "avg_launch_ms": avg_ms,
+                },
+                "host_enqueue_ms_per_step": full["host_ms"],
+                "breakdown_ms_per_step": {"predict": ft["predict_ms"] / K, "factor": ft["factor_ms"] / K},
+            }
         if world == 1 and not a.no_cpu_baseline:
             cb, (XH, yH) = cpu_baseline(wls[0], hyp, W, NL, NH0, k)
             if a.cpu_faithful:

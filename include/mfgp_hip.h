@@ -51,7 +51,15 @@ int mfgp_ctx_set_stream(mfgp_ctx* ctx, void* hip_stream);
 void* mfgp_ctx_get_stream(mfgp_ctx* ctx);
 /* Wait for all work; returns MFGP_ERR_NOT_PD if an ASYNC batch hit a non-PD factor. */
 int mfgp_ctx_synchronize(mfgp_ctx* ctx);
-/* Kernel timing (HIP events around every launch of the fused predict kernel). */
+/* Incremental updates (default on): an append of k <= 16 rows to a current
+ * factor is a bordered Cholesky step (L21 = K21 L11^-T, L22 = chol(K22 - L21 L21^T))
+ * instead of the reference's full refactor (gp:254 / gp:529), and predict keeps
+ * V = L^-1 psi^T resident so that it streams V once instead of recomputing it.
+ * Results agree with the full path to rounding. 0 = refactor and recompute V
+ * on every update, as the reference does. */
+int mfgp_ctx_set_incremental(mfgp_ctx* ctx, int enable);
+/* Kernel timing (HIP events around every predict-kernel launch: fused predict
+ * or one-pass incremental predict). */
 int mfgp_ctx_enable_timing(mfgp_ctx* ctx, int enable);
 /* Sum of predict-kernel durations (ms) and launch count since the last reset;
  * also the same for the factor stage (assemble + blocked Cholesky). */
@@ -92,6 +100,10 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var);
 int64_t mfgp_model_n(const mfgp_model* m);      /* N = NL + NH */
 int64_t mfgp_model_nl(const mfgp_model* m);
 int64_t mfgp_model_m(const mfgp_model* m);
+/* Path introspection (tests / benchmarks): out[0..n) = {factor rows (-1 = none),
+ * resident V rows, full refactors, bordered appends, full predicts, one-pass
+ * predicts}. */
+int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n);
 /* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
 int mfgp_get_factor(mfgp_model* m, double* L_out);
 

@@ -29,6 +29,8 @@ SIGNATURES = {
     "mfgp_ctx_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "mfgp_ctx_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "mfgp_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "mfgp_ctx_set_incremental": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mfgp_model_stats": (ctypes.c_int, [ctypes.c_void_p, _c_int64_p, ctypes.c_int]),
     "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int64_p, _c_double_p, _c_int64_p]),
     "mfgp_ctx_reset_timing": (ctypes.c_int, [ctypes.c_void_p]),
@@ -129,6 +131,11 @@ class Context:
     def set_stream(self, stream_ptr):
         check(lib().mfgp_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
 
+    def set_incremental(self, on=True):
+        """Bordered-Cholesky appends + one-pass predicts over the resident V (default),
+        or full refactor + full V recompute on every update (the reference's work)."""
+        check(lib().mfgp_ctx_set_incremental(self.handle, 1 if on else 0))
+
     def enable_timing(self, on=True):
         check(lib().mfgp_ctx_enable_timing(self.handle, 1 if on else 0))
 
@@ -224,6 +231,13 @@ class Model:
     @property
     def n(self):
         return lib().mfgp_model_n(self.handle)
+
+    def stats(self):
+        """{factor_rows, v_rows, full_factor, inc_factor, full_predict, vstream} (path counters)."""
+        out = (ctypes.c_int64 * 6)()
+        check(lib().mfgp_model_stats(self.handle, out, 6))
+        keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream")
+        return dict(zip(keys, (int(v) for v in out)))
 
     def truncate(self, n_keep_hifi):
         check(lib().mfgp_truncate(self.handle, int(n_keep_hifi)))

@@ -72,6 +72,9 @@ struct mfgp_ctx {
   int64_t n_predict = 0, n_factor = 0;
   // deferred status words of ASYNC batches
   std::vector<int*> async_status;
+  // incremental append / predict (bordered Cholesky + resident V); off = always
+  // refactor and recompute V from scratch, as the reference does
+  bool incremental = true;
 };
 
 struct mfgp_model {
@@ -88,14 +91,21 @@ struct mfgp_model {
   int64_t ld = 0;
   double* A = nullptr;     // [ld,ld]
   double* Linv = nullptr;  // [ld/NB][TILE]
+  double* zv = nullptr;     // [cap] z = L^-1 (y - m)
   int* status = nullptr;
   bool factored = false;
-  int64_t factor_N = -1;
+  int64_t factor_N = -1;    // rows [0, factor_N) of A / Linv / zv hold the current factor
+  int64_t ablk = 0;         // 64-row blocks of A / Linv initialised (assembled or padded)
   double factor_hyp[9] = {0};
   double factor_jitter = 0.0;
   // grid (device)
   int64_t M = 0, Mcap = 0;
   double* grid = nullptr;
+  // resident V = L^-1 psi^T [vtiles][vld][PBM]; rows [0, v_n) valid for the current factor and grid
+  double* V = nullptr;
+  int64_t vld = 0, vtiles = 0, v_n = 0;
+  // path counters (mfgp_model_stats)
+  int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0;
 };
 
 namespace {
@@ -192,17 +202,20 @@ int ensure_ws(mfgp_ctx* c, size_t bytes) {
   return MFGP_OK;
 }
 
-// Grow the training capacity of m to hold `need` rows (keeps X/y contents).
+// Grow the training capacity of m to hold `need` rows. Keeps X / y and, when
+// the factor is current for some rows, A / Linv / zv too (copied into the new
+// leading dimension), so a growing GP stays on the incremental path.
 int ensure_cap(mfgp_model* m, int64_t need) {
   if (need <= m->cap && m->A) return MFGP_OK;
   mfgp_ctx* c = m->ctx;
   int64_t cap = std::max<int64_t>({need, m->cap + m->cap / 2, 63});
   int64_t ld = round_up(cap + 1, NB);
   cap = ld - 1;
-  double *X = nullptr, *y = nullptr, *A = nullptr, *Li = nullptr;
+  double *X = nullptr, *y = nullptr, *A = nullptr, *Li = nullptr, *zv = nullptr;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMalloc(&X, sizeof(double) * 2 * cap));
   HIP_TRY(hipMalloc(&y, sizeof(double) * cap));
+  HIP_TRY(hipMalloc(&zv, sizeof(double) * cap));
   HIP_TRY(hipMalloc(&A, sizeof(double) * ld * ld));
   HIP_TRY(hipMalloc(&Li, sizeof(double) * (ld / NB) * TILE));
   const int64_t n = m->NL + m->NH;
@@ -210,18 +223,54 @@ int ensure_cap(mfgp_model* m, int64_t need) {
     HIP_TRY(hipMemcpyAsync(X, m->X, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(y, m->y, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
   }
+  const bool keep = m->A && m->factored && m->ablk > 0;
+  if (keep) {
+    HIP_TRY(hipMemcpy2DAsync(A, sizeof(double) * ld, m->A, sizeof(double) * m->ld, sizeof(double) * m->ld, m->ld,
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(Li, m->Linv, sizeof(double) * (m->ld / NB) * TILE, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(zv, m->zv, sizeof(double) * m->cap, hipMemcpyDeviceToDevice, c->stream));
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (m->X) HIP_TRY(hipFree(m->X));
   if (m->y) HIP_TRY(hipFree(m->y));
   if (m->A) HIP_TRY(hipFree(m->A));
   if (m->Linv) HIP_TRY(hipFree(m->Linv));
+  if (m->zv) HIP_TRY(hipFree(m->zv));
   m->X = X;
   m->y = y;
   m->A = A;
   m->Linv = Li;
+  m->zv = zv;
   m->cap = cap;
   m->ld = ld;
-  m->factored = false;
+  if (!keep) {
+    m->factored = false;
+    m->ablk = 0;
+    m->v_n = 0;
+  }
+  return MFGP_OK;
+}
+
+// Resident V for the current capacity and grid (contents kept when it fits).
+int ensure_v(mfgp_model* m) {
+  const int64_t vld = round_up(m->cap, PRB);
+  const int64_t tiles = ntiles_grid(m->M);
+  if (m->V && m->vld == vld && m->vtiles >= tiles) return MFGP_OK;
+  hipStream_t s = m->ctx->stream;
+  double* V = nullptr;
+  HIP_TRY(hipMalloc(&V, sizeof(double) * (size_t)tiles * vld * PBM));
+  if (m->V && m->v_n > 0 && m->vtiles >= tiles && m->vld >= m->v_n) {
+    // capacity grew: move the valid rows of every tile to the new row stride
+    HIP_TRY(hipMemcpy2DAsync(V, sizeof(double) * vld * PBM, m->V, sizeof(double) * m->vld * PBM,
+                             sizeof(double) * m->v_n * PBM, tiles, hipMemcpyDeviceToDevice, s));
+  } else {
+    m->v_n = 0;
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  if (m->V) HIP_TRY(hipFree(m->V));
+  m->V = V;
+  m->vld = vld;
+  m->vtiles = tiles;
   return MFGP_OK;
 }
 
@@ -263,7 +312,8 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.A = m->A;
   d.Linv = m->Linv;
   d.grid = m->grid;
-  d.V = nullptr;
+  d.V = m->V;
+  d.zv = m->zv;
   d.mu = nullptr;
   d.var = nullptr;
   d.status = m->status;
@@ -274,6 +324,10 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.N = m->NL + m->NH;
   d.NL = m->NL;
   d.M = m->M;
+  d.vld = m->vld;
+  d.n0 = 0;
+  d.vres = 0;
+  d.ablk = m->ablk;
   d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
   d.hp = d.hf;
 }
@@ -300,6 +354,28 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
       HIP_TRY(launch_syrk(dd, count, kb, below * (below + 1) / 2, 0, c->stream));
     }
   }
+  int64_t max_n = 0;
+  for (int i = 0; i < count; ++i) max_n = std::max(max_n, hd[i].N);
+  HIP_TRY(launch_extract_z(dd, count, max_n, c->stream));
+  return ev_end(c, ev);
+}
+
+int enqueue_inc_factor(mfgp_ctx* c, const GPDesc* dd, int count) {
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 1);
+  if (rc) return rc;
+  HIP_TRY(launch_inc_factor(dd, count, c->stream));
+  return ev_end(c, ev);
+}
+
+int enqueue_vstream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
+  int64_t max_ct = 0;
+  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_grid(hd[i].M));
+  if (max_ct == 0) return MFGP_OK;
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 0);
+  if (rc) return rc;
+  HIP_TRY(launch_vstream(dd, count, max_ct, c->stream));
   return ev_end(c, ev);
 }
 
@@ -314,16 +390,56 @@ int enqueue_predict(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   return ev_end(c, ev);
 }
 
-size_t v_bytes(int64_t M, int64_t N) {
-  return sizeof(double) * (size_t)ntiles_grid(M) * (size_t)prow_blocks(N) * PRB * PBM;
-}
-
 int read_status(mfgp_model* m) {
   int st = INT_MAX;
   HIP_TRY(hipMemcpy(&st, m->status, sizeof(int), hipMemcpyDeviceToHost));
   if (st != INT_MAX)
     return set_err(MFGP_ERR_NOT_PD, "Matrix is not positive definite (leading minor of order %d)", st);
   return MFGP_OK;
+}
+
+bool hyp_same(const mfgp_model* m) {
+  return m->factor_jitter == m->jitter && std::memcmp(m->factor_hyp, m->hyp, sizeof(m->hyp)) == 0;
+}
+
+bool factor_current(const mfgp_model* m) {
+  return m->factored && m->factor_N == m->NL + m->NH && hyp_same(m);
+}
+
+// Rows [factor_N, N) can be appended to the current factor (k_inc_factor).
+bool can_inc_factor(const mfgp_model* m) {
+  const int64_t N = m->NL + m->NH;
+  return m->ctx->incremental && m->factored && hyp_same(m) && m->factor_N < N && N - m->factor_N <= KINC;
+}
+
+// Predict by one pass over the resident V (k_vstream): V valid for rows < v_n,
+// at most KINC factor rows beyond it (the factor must be current).
+bool can_vstream(const mfgp_model* m) {
+  const int64_t N = m->NL + m->NH;
+  return m->ctx->incremental && m->M > 0 && m->V && m->vtiles >= ntiles_grid(m->M) && m->v_n <= N &&
+         N - m->v_n <= KINC;
+}
+
+void mark_full_factor(mfgp_model* m) {
+  m->n_full_factor += 1;
+  m->factored = true;
+  m->factor_N = m->NL + m->NH;
+  std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
+  m->factor_jitter = m->jitter;
+  m->ablk = std::max(m->ablk, nblocks_factor(m->factor_N));
+  m->v_n = 0;   // V belonged to the previous factor
+}
+
+void mark_inc_factor(mfgp_model* m) {
+  m->n_inc_factor += 1;
+  m->factor_N = m->NL + m->NH;
+  m->ablk = std::max(m->ablk, nblocks_factor(m->factor_N));
+}
+
+void fill_inc_desc(GPDesc& d, mfgp_model* m) {
+  fill_desc(d, m);
+  d.n0 = m->factor_N;
+  d.vres = m->V ? m->v_n : 0;
 }
 
 // Factor one model now (synchronous, status checked).
@@ -340,17 +456,31 @@ int factor_one(mfgp_model* m) {
   if ((rc = enqueue_factor(c, dd, hd, 1))) return rc;
   if ((rc = release_slot(c, slot))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
-  m->factor_N = m->NL + m->NH;
-  std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
-  m->factor_jitter = m->jitter;
+  mark_full_factor(m);
   rc = read_status(m);
   m->factored = (rc == MFGP_OK);
   return rc;
 }
 
-bool factor_current(const mfgp_model* m) {
-  return m->factored && m->factor_N == m->NL + m->NH && m->factor_jitter == m->jitter &&
-         std::memcmp(m->factor_hyp, m->hyp, sizeof(m->hyp)) == 0;
+// Bring the factor up to date for all N rows: bordered append of the rows
+// beyond factor_N when possible, else a full refactor (synchronous).
+int update_factor(mfgp_model* m) {
+  if (factor_current(m)) return MFGP_OK;
+  if (!can_inc_factor(m)) return factor_one(m);
+  mfgp_ctx* c = m->ctx;
+  int rc, slot;
+  GPDesc* hd = acquire_slot(c, slot, rc);
+  if (!hd) return rc;
+  fill_inc_desc(hd[0], m);
+  const GPDesc* dd = nullptr;
+  if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
+  if ((rc = enqueue_inc_factor(c, dd, 1))) return rc;
+  if ((rc = release_slot(c, slot))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  mark_inc_factor(m);
+  rc = read_status(m);
+  m->factored = (rc == MFGP_OK);
+  return rc;
 }
 
 bool is_device_ptr(const void* p) {
@@ -376,7 +506,7 @@ int copy_rows(mfgp_model* m, int64_t at, const double* X, const double* y, int64
 extern "C" {
 
 const char* mfgp_last_error(void) { return g_err.c_str(); }
-const char* mfgp_version(void) { return "mfgp_hip 0.1 gfx950 f64"; }
+const char* mfgp_version(void) { return "mfgp_hip 0.2 gfx950 f64"; }
 
 int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (!out) return set_err(MFGP_ERR_ARG, "null out");
@@ -434,6 +564,13 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
   }
   c->async_status.clear();
   return rc;
+}
+
+int mfgp_ctx_set_incremental(mfgp_ctx* c, int enable) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->incremental = enable != 0;
+  return MFGP_OK;
 }
 
 int mfgp_ctx_enable_timing(mfgp_ctx* c, int enable) {
@@ -494,8 +631,10 @@ void mfgp_model_destroy(mfgp_model* m) {
   if (m->y) (void)hipFree(m->y);
   if (m->A) (void)hipFree(m->A);
   if (m->Linv) (void)hipFree(m->Linv);
+  if (m->zv) (void)hipFree(m->zv);
   if (m->status) (void)hipFree(m->status);
   if (m->grid) (void)hipFree(m->grid);
+  if (m->V) (void)hipFree(m->V);
   delete m;
 }
 
@@ -522,8 +661,10 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
     HIP_TRY(hipMemcpyAsync(m->A, src->A, sizeof(double) * src->ld * src->ld, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(m->Linv, src->Linv, sizeof(double) * (src->ld / NB) * TILE, hipMemcpyDeviceToDevice,
                            c->stream));
+    HIP_TRY(hipMemcpyAsync(m->zv, src->zv, sizeof(double) * src->cap, hipMemcpyDeviceToDevice, c->stream));
     m->factored = true;
     m->factor_N = src->factor_N;
+    m->ablk = src->ablk;
     std::memcpy(m->factor_hyp, src->factor_hyp, sizeof(m->factor_hyp));
     m->factor_jitter = src->factor_jitter;
   }
@@ -531,6 +672,13 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
     HIP_TRY(hipMalloc(&m->grid, sizeof(double) * 2 * src->M));
     HIP_TRY(hipMemcpyAsync(m->grid, src->grid, sizeof(double) * 2 * src->M, hipMemcpyDeviceToDevice, c->stream));
     m->M = m->Mcap = src->M;
+    // resident V (the Choi planner clones a model and keeps appending to the copy, sim:339)
+    if (m->factored && src->V && src->v_n > 0 && src->vld == round_up(m->cap, PRB)) {
+      if ((rc = ensure_v(m))) return rc;
+      HIP_TRY(hipMemcpyAsync(m->V, src->V, sizeof(double) * (size_t)src->vtiles * src->vld * PBM,
+                             hipMemcpyDeviceToDevice, c->stream));
+      m->v_n = src->v_n;
+    }
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   *out = m;
@@ -552,6 +700,7 @@ int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
   if (rc) return rc;
   if (M < 0 || (M > 0 && !xs)) return set_err(MFGP_ERR_ARG, "bad grid");
   mfgp_ctx* c = m->ctx;
+  m->v_n = 0;   // V columns belong to the previous grid
   if (M > m->Mcap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (m->grid) HIP_TRY(hipFree(m->grid));
@@ -588,8 +737,8 @@ int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
   if ((rc = ensure_cap(m, n + k))) return rc;
   if ((rc = copy_rows(m, n, X, y, k))) return rc;
   m->NH += k;
-  m->factored = false;
-  return factor_one(m);
+  if (!m->ctx->incremental) m->factored = false;   // reference behaviour: refactor from scratch
+  return update_factor(m);
 }
 
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
@@ -598,7 +747,10 @@ int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
   if (n_keep_hifi < 0 || n_keep_hifi > m->NH) return set_err(MFGP_ERR_ARG, "bad truncate size");
   if (n_keep_hifi != m->NH) {
     m->NH = n_keep_hifi;
-    m->factored = false;
+    // the factor, z and V of the leading rows do not depend on later rows
+    const int64_t N = m->NL + m->NH;
+    if (m->factored && m->factor_N > N) m->factor_N = N;
+    m->v_n = std::min(m->v_n, N);
   }
   return MFGP_OK;
 }
@@ -608,24 +760,24 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   if (rc) return rc;
   mfgp_ctx* c = m->ctx;
   if (m->M > 0 && (!mu || !var)) return set_err(MFGP_ERR_ARG, "null output");
-  if (!factor_current(m)) {
-    if ((rc = factor_one(m))) return rc;
-  }
+  if ((rc = update_factor(m))) return rc;
   if (m->M == 0) return MFGP_OK;
-  const int64_t N = m->NL + m->NH;
-  const size_t vb = v_bytes(m->M, N);
+  if ((rc = ensure_v(m))) return rc;
   const size_t ob = sizeof(double) * 2 * (size_t)m->M;
-  if ((rc = ensure_ws(c, vb + ob))) return rc;
+  if ((rc = ensure_ws(c, ob))) return rc;
   int slot;
   GPDesc* hd = acquire_slot(c, slot, rc);
   if (!hd) return rc;
   fill_desc(hd[0], m);
-  hd[0].V = c->ws;
-  hd[0].mu = reinterpret_cast<double*>(reinterpret_cast<char*>(c->ws) + vb);
+  hd[0].mu = c->ws;
   hd[0].var = hd[0].mu + m->M;
+  const bool vst = can_vstream(m);
+  hd[0].n0 = m->v_n;
   const GPDesc* dd = nullptr;
   if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
-  if ((rc = enqueue_predict(c, dd, hd, 1))) return rc;
+  if ((rc = vst ? enqueue_vstream(c, dd, hd, 1) : enqueue_predict(c, dd, hd, 1))) return rc;
+  (vst ? m->n_vstream : m->n_full_predict) += 1;
+  m->v_n = m->NL + m->NH;
   HIP_TRY(hipMemcpyAsync(mu, hd[0].mu, sizeof(double) * m->M, hipMemcpyDefault, c->stream));
   HIP_TRY(hipMemcpyAsync(var, hd[0].var, sizeof(double) * m->M, hipMemcpyDefault, c->stream));
   if ((rc = release_slot(c, slot))) return rc;
@@ -634,15 +786,21 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
 }
 
 int64_t mfgp_model_n(const mfgp_model* m) { return m ? m->NL + m->NH : -1; }
+
+int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
+  if (!m || !out) return set_err(MFGP_ERR_ARG, "null model/out");
+  const int64_t v[6] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+                        m->n_full_predict, m->n_vstream};
+  for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+  return MFGP_OK;
+}
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
 int64_t mfgp_model_m(const mfgp_model* m) { return m ? m->M : -1; }
 
 int mfgp_get_factor(mfgp_model* m, double* L_out) {
   int rc = check_model(m);
   if (rc) return rc;
-  if (!factor_current(m)) {
-    if ((rc = factor_one(m))) return rc;
-  }
+  if ((rc = update_factor(m))) return rc;
   const int64_t N = m->NL + m->NH;
   if (N == 0) return MFGP_OK;
   std::vector<double> cm((size_t)m->ld * N);
@@ -654,7 +812,9 @@ int mfgp_get_factor(mfgp_model* m, double* L_out) {
 }
 
 // Shared driver of the batched entry points: append (optional), factor
-// (do_factor) and predict (do_predict) `count` models with one set of launches.
+// (do_factor) and predict (do_predict) `count` models with one set of launches
+// per kind: bordered appends (k_inc_factor) and full refactors side by side,
+// then one-pass predicts over the resident V (k_vstream) and full predicts.
 static int batch_run(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                      double* mu, double* var, int flags, bool do_factor, bool do_predict) {
   if (!models || count <= 0) return set_err(MFGP_ERR_ARG, "empty batch");
@@ -672,66 +832,124 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
   // per sub-batch (below); host sources by plain copies here
   const bool has_new = do_factor && k && X && y;
   const bool dev_src = has_new && is_device_ptr(X) && is_device_ptr(y);
-  std::vector<int64_t> src_off(count, 0);
-  int64_t off = 0, out_off = 0;
-  if (do_factor) {
-    for (int i = 0; i < count; ++i) {
-      mfgp_model* m = models[i];
-      const int64_t ki = has_new ? k[i] : 0;
-      const int64_t n = m->NL + m->NH;
-      if ((rc = ensure_cap(m, n + ki))) return rc;
-      src_off[i] = off;
-      if (ki > 0) {
-        if (!dev_src && (rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
-        m->NH += ki;
-      }
-      off += ki;
+  std::vector<int64_t> src_off(count, 0), out_off(count, 0);
+  int64_t off = 0, oo = 0;
+  for (int i = 0; i < count; ++i) {
+    mfgp_model* m = models[i];
+    out_off[i] = oo;
+    oo += m->M;
+    if (!do_factor) continue;
+    const int64_t ki = has_new ? k[i] : 0;
+    const int64_t n = m->NL + m->NH;
+    if ((rc = ensure_cap(m, n + ki))) return rc;
+    src_off[i] = off;
+    if (ki > 0) {
+      if (!dev_src && (rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
+      m->NH += ki;
     }
+    off += ki;
+    if (!c->incremental) m->factored = false;   // reference behaviour: refactor every update
   }
+  std::vector<mfgp_model*> full, inc, fpred, vst;
   for (int b0 = 0; b0 < count; b0 += MAXB) {
     const int nb = std::min(MAXB, count - b0);
-    size_t need = 0;
     if (do_predict) {
-      for (int i = 0; i < nb; ++i) {
-        mfgp_model* m = models[b0 + i];
-        need += v_bytes(m->M, m->NL + m->NH);
-      }
-      if ((rc = ensure_ws(c, need))) return rc;   // V scratch for every model of the sub-batch
+      for (int i = 0; i < nb; ++i)
+        if (models[b0 + i]->M > 0 && (rc = ensure_v(models[b0 + i]))) return rc;
     }
     int slot;
-    GPDesc* hd = acquire_slot(c, slot, rc);
-    if (!hd) return rc;
-    size_t vo = 0;
-    for (int i = 0; i < nb; ++i) {
-      mfgp_model* m = models[b0 + i];
-      fill_desc(hd[i], m);
-      if (do_predict) {
-        hd[i].V = reinterpret_cast<double*>(reinterpret_cast<char*>(c->ws) + vo);
-        vo += v_bytes(m->M, m->NL + m->NH);
-        hd[i].mu = mu + out_off;
-        hd[i].var = var + out_off;
-        out_off += m->M;
-      }
-      if (dev_src && k[b0 + i] > 0) {
-        hd[i].srcX = X + 2 * src_off[b0 + i];
-        hd[i].srcY = y + src_off[b0 + i];
-        hd[i].k_new = k[b0 + i];
-      }
-    }
+    GPDesc* hd = nullptr;
     const GPDesc* dd = nullptr;
-    if ((rc = upload_slot(c, slot, nb, &dd))) return rc;
-    if (dev_src) HIP_TRY(launch_append(dd, nb, c->stream));
-    if (do_factor && (rc = enqueue_factor(c, dd, hd, nb))) return rc;
-    if (do_predict && (rc = enqueue_predict(c, dd, hd, nb))) return rc;
-    if ((rc = release_slot(c, slot))) return rc;
+    if (dev_src) {
+      if (!(hd = acquire_slot(c, slot, rc))) return rc;
+      for (int i = 0; i < nb; ++i) {
+        fill_desc(hd[i], models[b0 + i]);
+        if (k[b0 + i] > 0) {
+          hd[i].srcX = X + 2 * src_off[b0 + i];
+          hd[i].srcY = y + src_off[b0 + i];
+          hd[i].k_new = k[b0 + i];
+        }
+      }
+      if ((rc = upload_slot(c, slot, nb, &dd))) return rc;
+      HIP_TRY(launch_append(dd, nb, c->stream));
+      if ((rc = release_slot(c, slot))) return rc;
+    }
     if (do_factor) {
+      full.clear();
+      inc.clear();
       for (int i = 0; i < nb; ++i) {
         mfgp_model* m = models[b0 + i];
-        m->factored = true;
-        m->factor_N = m->NL + m->NH;
-        std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
-        m->factor_jitter = m->jitter;
-        c->async_status.push_back(m->status);
+        if (factor_current(m)) continue;
+        (can_inc_factor(m) ? inc : full).push_back(m);
+      }
+      if (!full.empty()) {
+        if (!(hd = acquire_slot(c, slot, rc))) return rc;
+        for (size_t i = 0; i < full.size(); ++i) fill_desc(hd[i], full[i]);
+        if ((rc = upload_slot(c, slot, (int)full.size(), &dd))) return rc;
+        if ((rc = enqueue_factor(c, dd, hd, (int)full.size()))) return rc;
+        if ((rc = release_slot(c, slot))) return rc;
+        for (mfgp_model* m : full) {
+          mark_full_factor(m);
+          c->async_status.push_back(m->status);
+        }
+      }
+      if (!inc.empty()) {
+        if (!(hd = acquire_slot(c, slot, rc))) return rc;
+        for (size_t i = 0; i < inc.size(); ++i) fill_inc_desc(hd[i], inc[i]);
+        if ((rc = upload_slot(c, slot, (int)inc.size(), &dd))) return rc;
+        if ((rc = enqueue_inc_factor(c, dd, (int)inc.size()))) return rc;
+        if ((rc = release_slot(c, slot))) return rc;
+        for (mfgp_model* m : inc) {
+          mark_inc_factor(m);
+          c->async_status.push_back(m->status);
+        }
+      }
+    }
+    if (do_predict) {
+      fpred.clear();
+      vst.clear();
+      std::vector<int64_t> fo, vo;
+      for (int i = 0; i < nb; ++i) {
+        mfgp_model* m = models[b0 + i];
+        if (m->M == 0) continue;
+        if (can_vstream(m)) {
+          vst.push_back(m);
+          vo.push_back(out_off[b0 + i]);
+        } else {
+          fpred.push_back(m);
+          fo.push_back(out_off[b0 + i]);
+        }
+      }
+      if (!fpred.empty()) {
+        if (!(hd = acquire_slot(c, slot, rc))) return rc;
+        for (size_t i = 0; i < fpred.size(); ++i) {
+          fill_desc(hd[i], fpred[i]);
+          hd[i].mu = mu + fo[i];
+          hd[i].var = var + fo[i];
+        }
+        if ((rc = upload_slot(c, slot, (int)fpred.size(), &dd))) return rc;
+        if ((rc = enqueue_predict(c, dd, hd, (int)fpred.size()))) return rc;
+        if ((rc = release_slot(c, slot))) return rc;
+      }
+      if (!vst.empty()) {
+        if (!(hd = acquire_slot(c, slot, rc))) return rc;
+        for (size_t i = 0; i < vst.size(); ++i) {
+          fill_desc(hd[i], vst[i]);
+          hd[i].n0 = vst[i]->v_n;
+          hd[i].mu = mu + vo[i];
+          hd[i].var = var + vo[i];
+        }
+        if ((rc = upload_slot(c, slot, (int)vst.size(), &dd))) return rc;
+        if ((rc = enqueue_vstream(c, dd, hd, (int)vst.size()))) return rc;
+        if ((rc = release_slot(c, slot))) return rc;
+      }
+      for (mfgp_model* m : fpred) {
+        m->v_n = m->NL + m->NH;
+        m->n_full_predict += 1;
+      }
+      for (mfgp_model* m : vst) {
+        m->v_n = m->NL + m->NH;
+        m->n_vstream += 1;
       }
     }
   }

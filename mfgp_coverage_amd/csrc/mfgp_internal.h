@@ -13,6 +13,7 @@ constexpr int TILE = NB * NB;
 constexpr int PRB = 128;  // predict: training rows per left-looking block
 constexpr int PBM = 64;   // predict: grid cells per workgroup
 constexpr int PNT = 256;  // predict: threads per workgroup (4 waves; two workgroups per CU)
+constexpr int KINC = 16;  // incremental append: at most this many new rows per launch
 
 // Hyperparameters in linear scale, derived on the host from the log-scaled
 // vectors of simulator.py:53-56 / 83-84. SF uses the *L fields only.
@@ -35,7 +36,8 @@ struct GPDesc {
   double* A;           // [ld,ld] column-major; lower triangle = L after the factor
   double* Linv;        // [nb][NB*NB] column-major inverses of the diagonal blocks of L
   const double* grid;  // [M,2]
-  double* V;           // predict scratch [ceil(M/BM)][ceil(N/NB)][NB*BM]
+  double* V;           // resident V = L^-1 psi^T: [ceil(M/PBM)][vld][PBM] (tile, row, cell)
+  double* zv;          // [N] z = L^-1 (y - m)
   double* mu;          // [M]
   double* var;         // [M]
   int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
@@ -43,6 +45,10 @@ struct GPDesc {
   const double* srcY;
   int64_t k_new;
   int64_t ld, N, NL, M;
+  int64_t vld;         // rows per V tile (>= prow_blocks(N) * PRB)
+  int64_t n0;          // incremental kernels: rows [n0, N) are new (factor / V rows valid below n0)
+  int64_t vres;        // k_inc_factor: rows of V valid for the current factor (0 = none)
+  int64_t ablk;        // k_inc_factor: 64-row blocks of A / Linv already initialised
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -60,5 +66,8 @@ hipError_t launch_panel_diag(const GPDesc* d, int count, int kb, int64_t max_bel
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s);
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
+hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream_t s);
+hipError_t launch_inc_factor(const GPDesc* d, int count, hipStream_t s);
+hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
 
 }  // namespace mfgp

@@ -661,7 +661,9 @@ __global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, i
 //          V_top = Linv_a acc_top;  V_bot = Linv_b (acc_bot - L_ba V_top))
 //   var_part += colsum(V_I o V_I);  mu_part += V_I^T z_I
 // then mu = m + mu_part (gp:142-143 / gp:432), var = k** - var_part (diag of
-// gp:146 / gp:435-436). z = L^-1 (y - m) is row N of the augmented factor.
+// gp:146 / gp:435-436). z = L^-1 (y - m) is read from zv (row N of the
+// augmented factor, extracted by k_extract_z). Every V block is stored: V stays
+// resident in HBM for the incremental predicts (k_vstream) that follow appends.
 //
 // Staging: global_load_lds_dwordx4 (LDS-DMA) into a 3-stage ring of 16-deep K
 // steps (16 KB of L + 8 KB of V per stage) with two steps in flight, a counted
@@ -761,7 +763,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
   const int64_t nbf = nblocks_factor(N);
   const double* __restrict__ X = d.X;
   const double* __restrict__ Amat = d.A;
-  double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * nrb * (PRB * PBM);
+  double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * d.vld * PBM;   // resident V tile
   double vsum[4] = {0.0, 0.0, 0.0, 0.0}, msum[4] = {0.0, 0.0, 0.0, 0.0};
   // DMA plan of one K step (kc = first factor column / V row of the step):
   //  L image [KS][128]: wave w moves rows k = w + 4j (j < 4), all of parity w&1;
@@ -769,7 +771,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
   //  V image [KS][64]:  wave w moves row pairs p = w + 4j (j < 2), rows 2p + (lane>>5);
   //    src = Vt[(kc + 2p + (lane>>5))*64 + (((lane&31)*2) ^ ((lane>>5)<<4))]
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(Amat, (int64_t)8 * ld * ld);
-  const __amdgpu_buffer_rsrc_t rsV = make_rsrc(Vt, (int64_t)8 * nrb * PRB * PBM);
+  const __amdgpu_buffer_rsrc_t rsV = make_rsrc(Vt, (int64_t)8 * d.vld * PBM);
   const unsigned voffA = (unsigned)(8 * ((2 * lane) ^ ((w & 1) << 4)));
   const unsigned voffV =
       (unsigned)(8 * ((lane >> 5) * PBM + (((lane & 31) * 2) ^ ((lane >> 5) << 4))));
@@ -866,10 +868,9 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
         for (int v = 0; v < 4; ++v) img[swz(w * 32 + mt * 16 + q + 4 * v, nt * 16 + r)] = -acc.c[mt][nt][v];
     if (tid < PRB) {
       const int64_t g = base + tid;
-      zs[tid] = (g < N) ? Amat[g * ld + N] : 0.0;  // z_g = L[N][g]
+      zs[tid] = (g < N) ? d.zv[g] : 0.0;
     }
     __syncthreads();
-    const bool keep = (I + 1 < nrb);
     // V_top = Linv_a * T_top (Linv_a lower triangular: rows p16.. need K < p16 + 16)
     AccH vh;
 #pragma unroll
@@ -884,7 +885,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
       for (int v = 0; v < 4; ++v) {
         const int row = p16 + q + 4 * v, col = nt * 16 + r;
         const double val = vh.c[nt][v];
-        if (keep) gp(Vt)[(base + row) * PBM + col] = val;
+        gp(Vt)[(base + row) * PBM + col] = val;
         if (base + row < N) {
           vsum[nt] += val * val;
           msum[nt] += val * zs[row];
@@ -924,7 +925,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
         for (int v = 0; v < 4; ++v) {
           const int row = 64 + p16 + q + 4 * v, col = nt * 16 + r;
           const double val = vh.c[nt][v];
-          if (keep) gp(Vt)[(base + row) * PBM + col] = val;
+          gp(Vt)[(base + row) * PBM + col] = val;
           if (base + row < N) {
             vsum[nt] += val * val;
             msum[nt] += val * zs[row];
@@ -959,6 +960,419 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
       const double ms = (red[4 * PBM + tid] + red[5 * PBM + tid]) + (red[6 * PBM + tid] + red[7 * PBM + tid]);
       d.mu[c] = ms + h.meanH;
       d.var[c] = h.kss - vs;
+    }
+  }
+}
+
+// z = L^-1 (y - m) out of row N of the augmented factor into zv (after the
+// full factor; the incremental kernels extend zv themselves).
+__global__ __launch_bounds__(NT) void k_extract_z(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (j < d.N) d.zv[j] = d.A[j * d.ld + d.N];
+}
+
+// ---------------------------------------------------------------------------
+// Incremental append. The reference refactors from
+// scratch on every updt / updt_hifi (gp:257-268, gp:531-542 -> gp:254 / gp:529);
+// the factor of the leading rows does not change, so appending rows [n0, N)
+// (k = N - n0 <= KINC hifi rows) to a factor current for rows [0, n0) is the
+// bordered Cholesky step
+//   L21^T = L11^-1 K12,   L22 = chol(K22 - L21 L21^T),   z2 = L22^-1 (r2 - L21 z1)
+// plus the new rows of the diagonal-block inverses. L21^T is a set of V columns:
+// when every new point is a grid cell (the simulator samples only grid cells,
+// sim:705 / sim:875) and V = L11^-1 psi^T is resident for rows < n0, column c of
+// L21^T is V[:, cell(c)] -- psi(cell, X) and K(X, x_new) are the same numbers,
+// same operation order (k_entry vs k_predict's psi). Otherwise L21^T is solved
+// here by blocked forward substitution with the 64x64 inverses (one workgroup,
+// f64 MFMA; slower, but general). One workgroup per GP.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_inc_factor(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.x];
+  const int64_t n0 = d.n0, N = d.N, ld = d.ld, NL = d.NL;
+  const int k = (int)(N - n0);
+  if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
+  const Hyp& h = d.hf;
+  double* __restrict__ A = d.A;
+  const double* __restrict__ X = d.X;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  __shared__ int cell[KINC];
+  __shared__ double red[NT / 64][KINC * KINC + KINC];   // per-wave partial L21 L21^T | L21 z1
+  __shared__ double Ts[NB * KINC];                      // T_I image [64][16]
+  __shared__ double Lb[NB * SP];                        // Linv block, row-major
+  __shared__ double Lrow[NB];
+  if (tid == 0) *d.status = INT_MAX;
+  if (tid < KINC) cell[tid] = INT_MAX;
+  // (0) 64-row blocks entered for the first time: identity padding in A and Linv
+  // (the full predict reads whole blocks; their padding rows must stay finite)
+  const int64_t nbf = nblocks_factor(N);
+  for (int64_t bb = d.ablk; bb < nbf; ++bb) {
+    const int64_t ncols = (bb + 1) * NB;
+    for (int64_t e = tid; e < ncols * NB; e += NT) {
+      const int64_t col = e >> 6;
+      const int64_t row = bb * NB + (e & 63);
+      A[col * ld + row] = (col == row) ? 1.0 : 0.0;
+    }
+    for (int e = tid; e < TILE; e += NT) d.Linv[bb * TILE + e] = ((e & 63) == (e >> 6)) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  // (1) are the new points grid cells with resident V columns?
+  const bool try_v = n0 > 0 && d.vres >= n0 && d.V != nullptr && d.M > 0;
+  if (try_v) {
+    double px[KINC], py[KINC];
+#pragma unroll
+    for (int c = 0; c < KINC; ++c) {
+      px[c] = c < k ? X[2 * (n0 + c)] : __builtin_nan("");
+      py[c] = c < k ? X[2 * (n0 + c) + 1] : __builtin_nan("");
+    }
+    const GLOBAL dv2* g2 = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid));
+    constexpr int SB = 8;   // grid loads in flight per thread
+    for (int64_t e0 = tid; e0 < d.M; e0 += NT * SB) {
+      dv2 gxy[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int64_t e = e0 + (int64_t)u * NT;
+        gxy[u] = g2[e < d.M ? e : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int64_t e = e0 + (int64_t)u * NT;
+#pragma unroll
+        for (int c = 0; c < KINC; ++c)
+          if (e < d.M && gxy[u].x == px[c] && gxy[u].y == py[c]) atomicMin(&cell[c], (int)e);
+      }
+    }
+    __syncthreads();
+  }
+  bool use_v = try_v;
+  for (int c = 0; c < k; ++c) use_v = use_v && cell[c] != INT_MAX;
+  // (2) L21^T -> A[j * ld + n0 + c] (row n0 + c of L, column j). On the grid
+  // path the V columns are gathered in step (3), fused with the Schur sums.
+  if (!use_v) {
+    // left-looking: T_I = K12_I - sum_{J<I} L_IJ W_J;  W_I = Linv_II T_I
+    const int64_t nb0 = (n0 + NB - 1) / NB;
+    for (int64_t I = 0; I < nb0; ++I) {
+      const int64_t i0 = I * NB + w * 16;   // this wave's 16 rows
+      d4 acc;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t row = i0 + q + 4 * v;
+        acc[v] = (row < n0 && r < k) ? k_entry(h, X, NL, row, n0 + r) : 0.0;
+      }
+      for (int64_t J = 0; J < I; ++J) {
+#pragma unroll 4
+        for (int t = 0; t < NB / 4; ++t) {
+          const int64_t kc = J * NB + 4 * t + q;
+          const double a = A[kc * ld + i0 + r];                       // L[i0 + r][kc]
+          const double b = (r < k) ? A[kc * ld + n0 + r] : 0.0;       // W[kc][r]
+          acc = mfma(-a, b, acc);
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) Ts[(w * 16 + q + 4 * v) * KINC + r] = acc[v];
+      __syncthreads();
+      const double* __restrict__ Li = d.Linv + I * TILE;
+      d4 o = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+      for (int t = 0; t < NB / 4; ++t) {
+        const int m = 4 * t + q;
+        o = mfma(Li[m * NB + w * 16 + r], Ts[m * KINC + r], o);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t row = i0 + q + 4 * v;
+        if (row < n0 && r < k) A[row * ld + n0 + r] = o[v];
+      }
+      __syncthreads();   // W_I visible to every wave; Ts free
+    }
+  }
+  __syncthreads();
+  // (3) partial sums of L21 L21^T and L21 z1 over this wave's rows (f64 MFMA);
+  // lane (r, q) holds L21[r][j] for rows j = 4s + q, eight 4-row steps in flight
+  {
+    d4 sacc = {0.0, 0.0, 0.0, 0.0}, uacc = {0.0, 0.0, 0.0, 0.0};
+    const int64_t nst = (n0 + 3) >> 2;
+    constexpr int IU = 8;
+    const int cr = (use_v && r < k) ? cell[r] : 0;
+    // source of L21[r][j]: V column of the grid cell (stride PBM) or row n0 + r of A (stride ld)
+    const double* src = use_v ? d.V + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : A + n0 + (r < k ? r : 0);
+    const int64_t sstride = use_v ? PBM : ld;
+    for (int64_t s0 = w; s0 < nst; s0 += (NT / 64) * IU) {
+      double a[IU], zz[IU];
+#pragma unroll
+      for (int u = 0; u < IU; ++u) {
+        const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
+        const bool ok = j < n0;
+        const int64_t jj = ok ? j : 0;
+        a[u] = gp(src)[jj * sstride];
+        zz[u] = gp(d.zv)[jj];
+        a[u] = (ok && r < k) ? a[u] : 0.0;
+        zz[u] = ok ? zz[u] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < IU; ++u) {
+        const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
+        if (use_v && r < k && j < n0) A[j * ld + n0 + r] = a[u];
+        sacc = mfma(a[u], a[u], sacc);
+        uacc = mfma(a[u], zz[u], uacc);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      red[w][(q + 4 * v) * KINC + r] = sacc[v];
+      if (r == 0) red[w][KINC * KINC + q + 4 * v] = uacc[v];
+    }
+  }
+  __syncthreads();
+  // (4) L22 = chol(K22 - L21 L21^T) and z2, wave 0 (LAPACK dpotf2 order, as in
+  // factor_invert_64; lane r holds row r, DPP row broadcasts)
+  if (w == 0) {
+    double dd[KINC];
+#pragma unroll
+    for (int c = 0; c < KINC; ++c) {
+      const int e = r * KINC + c;
+      const double sv = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+      double v = (r == c) ? 1.0 : 0.0;
+      if (r < k && c < k) v = (c <= r ? k_entry(h, X, NL, n0 + r, n0 + c) : 0.0) - sv;
+      dd[c] = v;
+    }
+    double rdiag = 1.0;
+    int fail = INT_MAX;
+#pragma unroll
+    for (int j = 0; j < KINC; ++j) {
+      double p = bcast16(dd[j], j);
+      const bool pad = j >= k;
+      const bool bad = !pad && !(p > 0.0);
+      fail = bad ? min(fail, (int)(n0 + j + 1)) : fail;
+      p = (pad || bad) ? 1.0 : p;
+      const double rs = rsqrt(p);
+      const double l = (r > j) ? dd[j] * rs : (r == j ? p * rs : 0.0);
+      rdiag = (r == j) ? rs : rdiag;
+      dd[j] = l;
+      const double lu = (r > j) ? l : 0.0;
+#pragma unroll
+      for (int kk = j + 1; kk < KINC; ++kk) dd[kk] -= lu * bcast16(l, kk);
+    }
+    // z2 = L22^-1 (r2 - L21 z1), r2 = y - m_H (new rows are hifi; gp:133 / gp:421)
+    const int e = KINC * KINC + r;
+    double x = 0.0;
+    if (r < k) x = (d.y[n0 + r] - h.meanH) - ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e]));
+#pragma unroll
+    for (int j = 0; j < KINC; ++j) {
+      if (r == j) x *= rdiag;
+      const double zj = bcast16(x, j);
+      if (r > j) x -= dd[j] * zj;
+    }
+    if (lane < k) {
+#pragma unroll
+      for (int c = 0; c < KINC; ++c)
+        if (c <= lane) A[(n0 + c) * ld + n0 + lane] = dd[c];
+      d.zv[n0 + lane] = x;
+    }
+    if (fail != INT_MAX && lane == 0) atomicMin(d.status, fail);
+  }
+  __syncthreads();
+  // (5) new rows of the diagonal-block inverses (rows of a triangular inverse do
+  // not depend on later rows):  Linv[i][c] = -(sum_{m=c}^{i-1} L[i][m] Linv[m][c]) / L[i][i]
+  for (int64_t bb = n0 / NB; bb * NB < N; ++bb) {
+    double* __restrict__ Li = d.Linv + bb * TILE;
+    for (int e = tid; e < TILE; e += NT) {
+      const int m = e & 63, c = e >> 6;
+      Lb[m * SP + c] = Li[c * NB + m];
+    }
+    __syncthreads();
+    const int64_t r0 = n0 > bb * NB ? n0 : bb * NB;
+    const int64_t r1 = N < (bb + 1) * NB ? N : (bb + 1) * NB;
+    for (int64_t gi = r0; gi < r1; ++gi) {
+      const int li = (int)(gi - bb * NB);
+      if (tid < NB) Lrow[tid] = (tid <= li) ? A[(bb * NB + tid) * ld + gi] : 0.0;
+      __syncthreads();
+      if (tid < NB) {
+        const int c = tid;
+        double v = 0.0;
+        if (c < li) {
+          double s0 = 0.0;
+          for (int m = c; m < li; ++m) s0 += Lrow[m] * Lb[m * SP + c];
+          v = -s0 / Lrow[li];
+        } else if (c == li) {
+          v = 1.0 / Lrow[li];
+        }
+        Lb[li * SP + c] = v;
+      }
+      __syncthreads();
+    }
+    for (int e = tid; e < TILE; e += NT) {
+      const int m = e & 63, c = e >> 6;
+      const int64_t gm = bb * NB + m;
+      if (gm >= r0 && gm < r1) Li[c * NB + m] = Lb[m * SP + c];
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Incremental predict: V is resident for rows < n0 and the factor has k = N - n0
+// <= KINC new rows (k = 0: nothing appended since the last predict).
+//   T      = psi_new^T - L21 V_old      (16 x n0 by n0 x 64 per tile, f64 MFMA)
+//   V_new  = L22^-1 T                   -> rows [n0, N) of the resident V
+//   var    = k** - colsum(V o V),  mu = m + V^T z   over all N rows
+// V_old is read once (8 n0 bytes per cell, 16-byte loads, four 4-row MFMA steps
+// in flight per wave): the kernel is HBM-bound. Grid (cell tiles, batch); the
+// lane <-> cell map of the MFMA B operand follows the 16-byte loads:
+// (nt, r) -> cell 2r + (nt & 1) + 32 (nt >> 1).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int vs_cell(int nt, int r) { return 2 * r + (nt & 1) + 32 * (nt >> 1); }
+
+template <bool MMA, bool GUARD>
+__device__ __forceinline__ void vs_round(const GLOBAL dv2* __restrict__ vb, const double* __restrict__ A,
+                                         const double* __restrict__ z, int64_t ld, int64_t n0, int64_t j0, int rr,
+                                         bool arow, int r, d4* acc, double* vs, double* ms) {
+  constexpr int U = 4;
+  dv2 v0[U], v1[U];
+  double zj[U], a[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t j = j0 + 4 * u;
+    const bool ok = !GUARD || j < n0;
+    const int64_t jj = ok ? j : 0;   // clamped, loads stay unconditional
+    v0[u] = vb[jj * (PBM / 2) + r];
+    v1[u] = vb[jj * (PBM / 2) + 16 + r];
+    zj[u] = gp(z)[jj];
+    if (MMA) a[u] = gp(A)[jj * ld + n0 + rr];
+    if (GUARD && !ok) {
+      v0[u] = dv2{0.0, 0.0};
+      v1[u] = dv2{0.0, 0.0};
+      zj[u] = 0.0;
+    }
+    if (MMA) a[u] = (arow && ok) ? a[u] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    vs[0] += v0[u].x * v0[u].x;
+    vs[1] += v0[u].y * v0[u].y;
+    vs[2] += v1[u].x * v1[u].x;
+    vs[3] += v1[u].y * v1[u].y;
+    ms[0] += zj[u] * v0[u].x;
+    ms[1] += zj[u] * v0[u].y;
+    ms[2] += zj[u] * v1[u].x;
+    ms[3] += zj[u] * v1[u].y;
+    if (MMA) {
+      acc[0] = mfma(a[u], v0[u].x, acc[0]);
+      acc[1] = mfma(a[u], v0[u].y, acc[1]);
+      acc[2] = mfma(a[u], v1[u].x, acc[2]);
+      acc[3] = mfma(a[u], v1[u].y, acc[3]);
+    }
+  }
+}
+
+template <bool MMA>
+__device__ __forceinline__ void vs_rounds(const double* __restrict__ Vt, const double* __restrict__ A,
+                                          const double* __restrict__ z, int64_t ld, int64_t n0, int k, int w, int r,
+                                          int q, d4* acc, double* vs, double* ms) {
+  const GLOBAL dv2* vb = reinterpret_cast<const GLOBAL dv2*>(gp(Vt));
+  const int rr = MMA ? (r < k ? r : k - 1) : 0;
+  const bool arow = r < k;
+  const int64_t nfull = n0 >> 6;
+  for (int64_t R = 0; R < nfull; ++R)
+    vs_round<MMA, false>(vb, A, z, ld, n0, R * 64 + w * 16 + q, rr, arow, r, acc, vs, ms);
+  if (nfull * 64 < n0) vs_round<MMA, true>(vb, A, z, ld, n0, nfull * 64 + w * 16 + q, rr, arow, r, acc, vs, ms);
+}
+
+__global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t M = d.M;
+  const int64_t c0 = (int64_t)blockIdx.x * PBM;
+  if (c0 >= M) return;
+  const int64_t n0 = d.n0, N = d.N, ld = d.ld;
+  const int k = (int)(N - n0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * d.vld * PBM;
+  const double* __restrict__ A = d.A;
+  const double* __restrict__ z = d.zv;
+  __shared__ double red[NT / 64][KINC * PBM];   // per-wave partial L21 V_old [row][cell]
+  __shared__ double sred[2][NT / 64][PBM];      // per-wave colsum(V o V), V^T z
+  __shared__ double L22[KINC * KINC + KINC];    // L22 (row-major) | z2
+  d4 acc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
+  double vs[4] = {0.0, 0.0, 0.0, 0.0}, ms[4] = {0.0, 0.0, 0.0, 0.0};
+  // rounds of 64 rows: wave w streams rows 16w.. (four 4-row MFMA steps, 8 KB);
+  // full rounds without guards, then one guarded tail round
+  if (k > 0) vs_rounds<true>(Vt, A, z, ld, n0, k, w, r, q, acc, vs, ms);
+  else vs_rounds<false>(Vt, A, z, ld, n0, k, w, r, q, acc, vs, ms);
+  if (k > 0) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) red[w][(q + 4 * v) * PBM + vs_cell(nt, r)] = acc[nt][v];
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    vs[nt] += __shfl_xor(vs[nt], 16);
+    vs[nt] += __shfl_xor(vs[nt], 32);
+    ms[nt] += __shfl_xor(ms[nt], 16);
+    ms[nt] += __shfl_xor(ms[nt], 32);
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sred[0][w][vs_cell(nt, r)] = vs[nt];
+      sred[1][w][vs_cell(nt, r)] = ms[nt];
+    }
+  }
+  if (tid < KINC * KINC) {
+    const int ra = tid / KINC, cb = tid % KINC;
+    L22[tid] = (ra < k && cb <= ra) ? A[(n0 + cb) * ld + n0 + ra] : 0.0;
+  }
+  if (tid < KINC) L22[KINC * KINC + tid] = tid < k ? z[n0 + tid] : 0.0;
+  __syncthreads();
+  if (tid < PBM) {
+    const int e = tid;
+    const int64_t c = c0 + e;
+    double vsum = (sred[0][0][e] + sred[0][1][e]) + (sred[0][2][e] + sred[0][3][e]);
+    double msum = (sred[1][0][e] + sred[1][1][e]) + (sred[1][2][e] + sred[1][3][e]);
+    const Hyp& h = d.hp;
+    if (k > 0) {
+      const int64_t cc = c < M ? c : M - 1;
+      const double gx = d.grid[2 * cc], gy = d.grid[2 * cc + 1];
+      const double cLx = div_(gx, h.lL), cLy = div_(gy, h.lL);
+      const double cHx = div_(gx, h.lH), cHy = div_(gy, h.lH);
+      double vn[KINC];
+#pragma unroll
+      for (int a = 0; a < KINC; ++a) {
+        vn[a] = 0.0;
+        if (a < k) {
+          const int64_t g = n0 + a;
+          const double tx = d.X[2 * g], ty = d.X[2 * g + 1];
+          const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
+          double psi;
+          if (h.kind == 0) {
+            psi = se_scaled(cLx, cLy, tLx, tLy, h.sL);
+          } else if (g < d.NL) {
+            psi = h.rho * se_scaled(cLx, cLy, tLx, tLy, h.sL);
+          } else {
+#pragma clang fp contract(off)
+            psi = h.rho2 * se_scaled(cLx, cLy, tLx, tLy, h.sL) +
+                  se_scaled(cHx, cHy, div_(tx, h.lH), div_(ty, h.lH), h.sH);
+          }
+          const int ei = a * PBM + e;
+          double t = psi - ((red[0][ei] + red[1][ei]) + (red[2][ei] + red[3][ei]));
+#pragma unroll
+          for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+          vn[a] = t / L22[a * KINC + a];
+          vsum += vn[a] * vn[a];
+          msum += vn[a] * L22[KINC * KINC + a];
+          gp(Vt)[(n0 + a) * PBM + e] = vn[a];
+        }
+      }
+    }
+    if (c < M) {
+      d.mu[c] = msum + h.meanH;
+      d.var[c] = h.kss - vsum;
     }
   }
 }
@@ -1005,6 +1419,19 @@ hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int 
 }
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {
   hipLaunchKernelGGL(k_predict, dim3((unsigned)max_ctiles, count), dim3(PNT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream_t s) {
+  if (max_n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_extract_z, dim3((unsigned)((max_n + NT - 1) / NT), count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_inc_factor(const GPDesc* d, int count, hipStream_t s) {
+  hipLaunchKernelGGL(k_inc_factor, dim3(count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_vstream, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 
