@@ -92,6 +92,7 @@ struct mfgp_model {
   double* A = nullptr;     // [ld,ld]
   double* Linv = nullptr;  // [ld/NB][TILE]
   double* zv = nullptr;     // [cap] z = L^-1 (y - m)
+  double* iscr = nullptr;   // incremental-append scratch (inc_scratch_doubles(cap))
   int* status = nullptr;
   bool factored = false;
   int64_t factor_N = -1;    // rows [0, factor_N) of A / Linv / zv hold the current factor
@@ -211,11 +212,12 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   int64_t cap = std::max<int64_t>({need, m->cap + m->cap / 2, 63});
   int64_t ld = round_up(cap + 1, NB);
   cap = ld - 1;
-  double *X = nullptr, *y = nullptr, *A = nullptr, *Li = nullptr, *zv = nullptr;
+  double *X = nullptr, *y = nullptr, *A = nullptr, *Li = nullptr, *zv = nullptr, *isc = nullptr;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMalloc(&X, sizeof(double) * 2 * cap));
   HIP_TRY(hipMalloc(&y, sizeof(double) * cap));
   HIP_TRY(hipMalloc(&zv, sizeof(double) * cap));
+  HIP_TRY(hipMalloc(&isc, sizeof(double) * inc_scratch_doubles(cap)));
   HIP_TRY(hipMalloc(&A, sizeof(double) * ld * ld));
   HIP_TRY(hipMalloc(&Li, sizeof(double) * (ld / NB) * TILE));
   const int64_t n = m->NL + m->NH;
@@ -236,6 +238,8 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   if (m->A) HIP_TRY(hipFree(m->A));
   if (m->Linv) HIP_TRY(hipFree(m->Linv));
   if (m->zv) HIP_TRY(hipFree(m->zv));
+  if (m->iscr) HIP_TRY(hipFree(m->iscr));
+  m->iscr = isc;
   m->X = X;
   m->y = y;
   m->A = A;
@@ -314,6 +318,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.grid = m->grid;
   d.V = m->V;
   d.zv = m->zv;
+  d.iscr = m->iscr;
   d.mu = nullptr;
   d.var = nullptr;
   d.status = m->status;
@@ -360,11 +365,13 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   return ev_end(c, ev);
 }
 
-int enqueue_inc_factor(mfgp_ctx* c, const GPDesc* dd, int count) {
+int enqueue_inc_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
+  int64_t max_n0 = 0;
+  for (int i = 0; i < count; ++i) max_n0 = std::max(max_n0, hd[i].n0);
   EvPair ev{};
   int rc = ev_begin(c, ev, 1);
   if (rc) return rc;
-  HIP_TRY(launch_inc_factor(dd, count, c->stream));
+  HIP_TRY(launch_inc_factor(dd, count, max_n0, c->stream));
   return ev_end(c, ev);
 }
 
@@ -474,7 +481,8 @@ int update_factor(mfgp_model* m) {
   fill_inc_desc(hd[0], m);
   const GPDesc* dd = nullptr;
   if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
-  if ((rc = enqueue_inc_factor(c, dd, 1))) return rc;
+  HIP_TRY(launch_append(dd, 1, c->stream));   // grid-cell search of the new points
+  if ((rc = enqueue_inc_factor(c, dd, hd, 1))) return rc;
   if ((rc = release_slot(c, slot))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   mark_inc_factor(m);
@@ -632,6 +640,7 @@ void mfgp_model_destroy(mfgp_model* m) {
   if (m->A) (void)hipFree(m->A);
   if (m->Linv) (void)hipFree(m->Linv);
   if (m->zv) (void)hipFree(m->zv);
+  if (m->iscr) (void)hipFree(m->iscr);
   if (m->status) (void)hipFree(m->status);
   if (m->grid) (void)hipFree(m->grid);
   if (m->V) (void)hipFree(m->V);
@@ -850,7 +859,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     off += ki;
     if (!c->incremental) m->factored = false;   // reference behaviour: refactor every update
   }
-  std::vector<mfgp_model*> full, inc, fpred, vst;
+  std::vector<mfgp_model*> order;
+  std::vector<int64_t> oo_ord;
   for (int b0 = 0; b0 < count; b0 += MAXB) {
     const int nb = std::min(MAXB, count - b0);
     if (do_predict) {
@@ -860,96 +870,73 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     int slot;
     GPDesc* hd = nullptr;
     const GPDesc* dd = nullptr;
-    if (dev_src) {
+    if (do_factor) {
+      // one descriptor slot ordered [bordered appends | full refactors | current]:
+      // k_append (copies + grid-cell search) runs over all of them, the factor
+      // kernels over their contiguous sub-ranges
+      order.clear();
+      int ninc = 0, nfull = 0;
+      for (int i = 0; i < nb; ++i)
+        if (!factor_current(models[b0 + i]) && can_inc_factor(models[b0 + i])) order.push_back(models[b0 + i]);
+      ninc = (int)order.size();
+      for (int i = 0; i < nb; ++i)
+        if (!factor_current(models[b0 + i]) && !can_inc_factor(models[b0 + i])) order.push_back(models[b0 + i]);
+      nfull = (int)order.size() - ninc;
+      for (int i = 0; i < nb; ++i)
+        if (factor_current(models[b0 + i])) order.push_back(models[b0 + i]);
       if (!(hd = acquire_slot(c, slot, rc))) return rc;
       for (int i = 0; i < nb; ++i) {
-        fill_desc(hd[i], models[b0 + i]);
-        if (k[b0 + i] > 0) {
-          hd[i].srcX = X + 2 * src_off[b0 + i];
-          hd[i].srcY = y + src_off[b0 + i];
-          hd[i].k_new = k[b0 + i];
+        mfgp_model* m = order[i];
+        if (i < ninc) fill_inc_desc(hd[i], m);
+        else fill_desc(hd[i], m);
+        const int mi = (int)(std::find(models + b0, models + b0 + nb, m) - models);
+        if (dev_src && k[mi] > 0) {
+          hd[i].srcX = X + 2 * src_off[mi];
+          hd[i].srcY = y + src_off[mi];
+          hd[i].k_new = k[mi];
         }
       }
       if ((rc = upload_slot(c, slot, nb, &dd))) return rc;
-      HIP_TRY(launch_append(dd, nb, c->stream));
+      if (dev_src || ninc > 0) HIP_TRY(launch_append(dd, nb, c->stream));
+      if (ninc > 0 && (rc = enqueue_inc_factor(c, dd, hd, ninc))) return rc;
+      if (nfull > 0 && (rc = enqueue_factor(c, dd + ninc, hd + ninc, nfull))) return rc;
       if ((rc = release_slot(c, slot))) return rc;
-    }
-    if (do_factor) {
-      full.clear();
-      inc.clear();
-      for (int i = 0; i < nb; ++i) {
-        mfgp_model* m = models[b0 + i];
-        if (factor_current(m)) continue;
-        (can_inc_factor(m) ? inc : full).push_back(m);
-      }
-      if (!full.empty()) {
-        if (!(hd = acquire_slot(c, slot, rc))) return rc;
-        for (size_t i = 0; i < full.size(); ++i) fill_desc(hd[i], full[i]);
-        if ((rc = upload_slot(c, slot, (int)full.size(), &dd))) return rc;
-        if ((rc = enqueue_factor(c, dd, hd, (int)full.size()))) return rc;
-        if ((rc = release_slot(c, slot))) return rc;
-        for (mfgp_model* m : full) {
-          mark_full_factor(m);
-          c->async_status.push_back(m->status);
-        }
-      }
-      if (!inc.empty()) {
-        if (!(hd = acquire_slot(c, slot, rc))) return rc;
-        for (size_t i = 0; i < inc.size(); ++i) fill_inc_desc(hd[i], inc[i]);
-        if ((rc = upload_slot(c, slot, (int)inc.size(), &dd))) return rc;
-        if ((rc = enqueue_inc_factor(c, dd, (int)inc.size()))) return rc;
-        if ((rc = release_slot(c, slot))) return rc;
-        for (mfgp_model* m : inc) {
-          mark_inc_factor(m);
-          c->async_status.push_back(m->status);
-        }
+      for (int i = 0; i < ninc + nfull; ++i) {
+        if (i < ninc) mark_inc_factor(order[i]);
+        else mark_full_factor(order[i]);
+        c->async_status.push_back(order[i]->status);
       }
     }
     if (do_predict) {
-      fpred.clear();
-      vst.clear();
-      std::vector<int64_t> fo, vo;
-      for (int i = 0; i < nb; ++i) {
-        mfgp_model* m = models[b0 + i];
-        if (m->M == 0) continue;
-        if (can_vstream(m)) {
-          vst.push_back(m);
-          vo.push_back(out_off[b0 + i]);
-        } else {
-          fpred.push_back(m);
-          fo.push_back(out_off[b0 + i]);
+      // one slot ordered [one-pass predicts over resident V | full predicts]
+      order.clear();
+      oo_ord.clear();
+      for (int pass = 0; pass < 2; ++pass)
+        for (int i = 0; i < nb; ++i) {
+          mfgp_model* m = models[b0 + i];
+          if (m->M == 0 || can_vstream(m) != (pass == 0)) continue;
+          order.push_back(m);
+          oo_ord.push_back(out_off[b0 + i]);
         }
-      }
-      if (!fpred.empty()) {
+      int nv = 0;
+      while (nv < (int)order.size() && can_vstream(order[nv])) ++nv;
+      const int np = (int)order.size();
+      if (np > 0) {
         if (!(hd = acquire_slot(c, slot, rc))) return rc;
-        for (size_t i = 0; i < fpred.size(); ++i) {
-          fill_desc(hd[i], fpred[i]);
-          hd[i].mu = mu + fo[i];
-          hd[i].var = var + fo[i];
+        for (int i = 0; i < np; ++i) {
+          fill_desc(hd[i], order[i]);
+          if (i < nv) hd[i].n0 = order[i]->v_n;
+          hd[i].mu = mu + oo_ord[i];
+          hd[i].var = var + oo_ord[i];
         }
-        if ((rc = upload_slot(c, slot, (int)fpred.size(), &dd))) return rc;
-        if ((rc = enqueue_predict(c, dd, hd, (int)fpred.size()))) return rc;
+        if ((rc = upload_slot(c, slot, np, &dd))) return rc;
+        if (nv > 0 && (rc = enqueue_vstream(c, dd, hd, nv))) return rc;
+        if (np > nv && (rc = enqueue_predict(c, dd + nv, hd + nv, np - nv))) return rc;
         if ((rc = release_slot(c, slot))) return rc;
-      }
-      if (!vst.empty()) {
-        if (!(hd = acquire_slot(c, slot, rc))) return rc;
-        for (size_t i = 0; i < vst.size(); ++i) {
-          fill_desc(hd[i], vst[i]);
-          hd[i].n0 = vst[i]->v_n;
-          hd[i].mu = mu + vo[i];
-          hd[i].var = var + vo[i];
+        for (int i = 0; i < np; ++i) {
+          order[i]->v_n = order[i]->NL + order[i]->NH;
+          (i < nv ? order[i]->n_vstream : order[i]->n_full_predict) += 1;
         }
-        if ((rc = upload_slot(c, slot, (int)vst.size(), &dd))) return rc;
-        if ((rc = enqueue_vstream(c, dd, hd, (int)vst.size()))) return rc;
-        if ((rc = release_slot(c, slot))) return rc;
-      }
-      for (mfgp_model* m : fpred) {
-        m->v_n = m->NL + m->NH;
-        m->n_full_predict += 1;
-      }
-      for (mfgp_model* m : vst) {
-        m->v_n = m->NL + m->NH;
-        m->n_vstream += 1;
       }
     }
   }

@@ -14,6 +14,10 @@ constexpr int PRB = 128;  // predict: training rows per left-looking block
 constexpr int PBM = 64;   // predict: grid cells per workgroup
 constexpr int PNT = 256;  // predict: threads per workgroup (4 waves; two workgroups per CU)
 constexpr int KINC = 16;  // incremental append: at most this many new rows per launch
+constexpr int INC_CHUNK = 256;   // rows of L21 per k_inc_l21 workgroup
+constexpr int64_t inc_scratch_doubles(int64_t cap) {
+  return 1 + KINC + ((cap + INC_CHUNK - 1) / INC_CHUNK) * (KINC * KINC + KINC);
+}
 
 // Hyperparameters in linear scale, derived on the host from the log-scaled
 // vectors of simulator.py:53-56 / 83-84. SF uses the *L fields only.
@@ -38,6 +42,7 @@ struct GPDesc {
   const double* grid;  // [M,2]
   double* V;           // resident V = L^-1 psi^T: [ceil(M/PBM)][vld][PBM] (tile, row, cell)
   double* zv;          // [N] z = L^-1 (y - m)
+  double* iscr;        // incremental append scratch: [0] = rows gathered from V, then per-chunk partial sums
   double* mu;          // [M]
   double* var;         // [M]
   int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
@@ -67,7 +72,7 @@ hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, h
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s);
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
 hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream_t s);
-hipError_t launch_inc_factor(const GPDesc* d, int count, hipStream_t s);
+hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
 
 }  // namespace mfgp

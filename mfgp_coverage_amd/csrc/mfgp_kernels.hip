@@ -983,75 +983,141 @@ __global__ __launch_bounds__(NT) void k_extract_z(const GPDesc* __restrict__ des
 // when every new point is a grid cell (the simulator samples only grid cells,
 // sim:705 / sim:875) and V = L11^-1 psi^T is resident for rows < n0, column c of
 // L21^T is V[:, cell(c)] -- psi(cell, X) and K(X, x_new) are the same numbers,
-// same operation order (k_entry vs k_predict's psi). Otherwise L21^T is solved
-// here by blocked forward substitution with the 64x64 inverses (one workgroup,
-// f64 MFMA; slower, but general). One workgroup per GP.
+// same operation order (k_entry vs k_predict's psi). Two launches:
+//   k_inc_l21    (row chunks x GPs): find the cells, gather the V columns into
+//                rows n0.. of A and the chunk's partial L21 L21^T, L21 z1 (MFMA);
+//   k_inc_finish (one workgroup per GP): sum the partials, L22, z2, the new
+//                Linv rows. Off the grid (or without a resident V) k_inc_finish
+//                solves L21^T itself by blocked forward substitution (one
+//                workgroup, f64 MFMA; slower, but general).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_inc_factor(const GPDesc* __restrict__ descs) {
+constexpr int ICH = INC_CHUNK;             // rows of L21 per k_inc_l21 workgroup
+constexpr int ISZ = KINC * KINC + KINC;    // partial sums per chunk: L21 L21^T | L21 z1
+// iscr layout: [0] = 1 if the new points were found on the grid with V resident
+// (k_append), [1 + c] = their cells, [ISC0 + chunk * ISZ ...] = k_inc_l21 partials
+constexpr int ISC0 = 1 + KINC;
+
+// Identity padding for the 64-row blocks [ablk, nbf) entered for the first time,
+// columns [c_lo, c_hi) (the full predict reads whole blocks: padding rows must
+// stay finite), and, with `linv`, their Linv blocks.
+__device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, bool linv) {
+  const int64_t nbf = nblocks_factor(d.N);
+  const int tid = threadIdx.x;
+  for (int64_t bb = d.ablk; bb < nbf; ++bb) {
+    const int64_t c1 = c_hi < (bb + 1) * NB ? c_hi : (bb + 1) * NB;
+    if (c1 > c_lo) {
+      for (int64_t e = tid; e < (c1 - c_lo) * NB; e += NT) {
+        const int64_t col = c_lo + (e >> 6);
+        const int64_t row = bb * NB + (e & 63);
+        d.A[col * d.ld + row] = (col == row) ? 1.0 : 0.0;
+      }
+    }
+    if (linv)
+      for (int e = tid; e < TILE; e += NT) d.Linv[bb * TILE + e] = ((e & 63) == (e >> 6)) ? 1.0 : 0.0;
+  }
+}
+
+// Partial L21 L21^T and L21 z1 over rows [j_lo, j_hi) into red[w][ISZ] (one slot per
+// wave). Lane (r, q) holds L21[r][j], j = 4s + q, eight 4-row steps in flight per
+// wave. With `cell`, L21[r][.] is gathered from the V column of the grid cell and
+// written to row n0 + r of A; otherwise it is read from there.
+__device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo, int64_t j_hi,
+                                  double (*red)[ISZ]) {
+  const int64_t n0 = d.n0, ld = d.ld;
+  const int k = (int)(d.N - n0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  d4 sacc = {0.0, 0.0, 0.0, 0.0}, uacc = {0.0, 0.0, 0.0, 0.0};
+  constexpr int IU = 8;
+  const bool from_v = cell != nullptr;
+  const int cr = (from_v && r < k) ? cell[r] : 0;
+  const double* src = from_v ? d.V + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : d.A + n0 + (r < k ? r : 0);
+  const int64_t sstride = from_v ? PBM : ld;
+  const int64_t s_lo = j_lo >> 2, s_hi = (j_hi + 3) >> 2;   // j_lo is a multiple of 4
+  for (int64_t s0 = s_lo + w; s0 < s_hi; s0 += (NT / 64) * IU) {
+    double a[IU], zz[IU];
+#pragma unroll
+    for (int u = 0; u < IU; ++u) {
+      const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
+      const bool ok = j < j_hi;
+      const int64_t jj = ok ? j : j_lo;
+      a[u] = gp(src)[jj * sstride];
+      zz[u] = gp(d.zv)[jj];
+      a[u] = (ok && r < k) ? a[u] : 0.0;
+      zz[u] = ok ? zz[u] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < IU; ++u) {
+      const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
+      if (from_v && r < k && j < j_hi) d.A[j * ld + n0 + r] = a[u];
+      sacc = mfma(a[u], a[u], sacc);
+      uacc = mfma(a[u], zz[u], uacc);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    red[w][(q + 4 * v) * KINC + r] = sacc[v];
+    if (r == 0) red[w][KINC * KINC + q + 4 * v] = uacc[v];
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_inc_l21(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t n0 = d.n0;
+  const int k = (int)(d.N - n0);
+  if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
+  const int64_t j_lo = (int64_t)blockIdx.x * ICH;
+  if (j_lo >= n0) return;
+  const int64_t j_hi = j_lo + ICH < n0 ? j_lo + ICH : n0;
+  __shared__ int cell[KINC];
+  __shared__ double red[NT / 64][ISZ];
+  inc_init_blocks(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
+  if (threadIdx.x < KINC) cell[threadIdx.x] = (int)d.iscr[1 + threadIdx.x];
+  __syncthreads();
+  if (d.iscr[0] == 0.0) return;   // off the grid: k_inc_finish solves
+  inc_schur_partial(d, cell, j_lo, j_hi, red);
+  __syncthreads();
+  double* __restrict__ part = d.iscr + ISC0 + (int64_t)blockIdx.x * ISZ;
+  for (int e = threadIdx.x; e < ISZ; e += NT) part[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+}
+
+__global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.x];
   const int64_t n0 = d.n0, N = d.N, ld = d.ld, NL = d.NL;
   const int k = (int)(N - n0);
-  if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
+  if (k <= 0 || k > KINC) return;
   const Hyp& h = d.hf;
   double* __restrict__ A = d.A;
   const double* __restrict__ X = d.X;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
-  __shared__ int cell[KINC];
-  __shared__ double red[NT / 64][KINC * KINC + KINC];   // per-wave partial L21 L21^T | L21 z1
-  __shared__ double Ts[NB * KINC];                      // T_I image [64][16]
-  __shared__ double Lb[NB * SP];                        // Linv block, row-major
-  __shared__ double Lrow[NB];
+  __shared__ double red[NT / 64][ISZ];
+  __shared__ double ssum[ISZ];
+  __shared__ double Ts[NB * KINC];      // T_I image [64][16]
+  __shared__ double Lb[NB * SP];        // Linv block, row-major
+  __shared__ double Ln[KINC * SP];      // new rows of L inside the block
   if (tid == 0) *d.status = INT_MAX;
-  if (tid < KINC) cell[tid] = INT_MAX;
-  // (0) 64-row blocks entered for the first time: identity padding in A and Linv
-  // (the full predict reads whole blocks; their padding rows must stay finite)
-  const int64_t nbf = nblocks_factor(N);
-  for (int64_t bb = d.ablk; bb < nbf; ++bb) {
-    const int64_t ncols = (bb + 1) * NB;
-    for (int64_t e = tid; e < ncols * NB; e += NT) {
-      const int64_t col = e >> 6;
-      const int64_t row = bb * NB + (e & 63);
-      A[col * ld + row] = (col == row) ? 1.0 : 0.0;
-    }
-    for (int e = tid; e < TILE; e += NT) d.Linv[bb * TILE + e] = ((e & 63) == (e >> 6)) ? 1.0 : 0.0;
-  }
+  const bool gathered = n0 > 0 && d.iscr[0] != 0.0;
+  inc_init_blocks(d, gathered ? n0 : 0, nblocks_factor(N) * NB, true);
   __syncthreads();
-  // (1) are the new points grid cells with resident V columns?
-  const bool try_v = n0 > 0 && d.vres >= n0 && d.V != nullptr && d.M > 0;
-  if (try_v) {
-    double px[KINC], py[KINC];
+  if (gathered) {
+    const int nch = (int)((n0 + ICH - 1) / ICH);
+    for (int e = tid; e < ISZ; e += NT) {
+      // chunk partials in a fixed order; eight loads in flight per thread
+      double acc = 0.0;
+      for (int c0 = 0; c0 < nch; c0 += 8) {
+        double t[8];
 #pragma unroll
-    for (int c = 0; c < KINC; ++c) {
-      px[c] = c < k ? X[2 * (n0 + c)] : __builtin_nan("");
-      py[c] = c < k ? X[2 * (n0 + c) + 1] : __builtin_nan("");
-    }
-    const GLOBAL dv2* g2 = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid));
-    constexpr int SB = 8;   // grid loads in flight per thread
-    for (int64_t e0 = tid; e0 < d.M; e0 += NT * SB) {
-      dv2 gxy[SB];
+        for (int u = 0; u < 8; ++u) t[u] = (c0 + u < nch) ? gp(d.iscr)[ISC0 + (int64_t)(c0 + u) * ISZ + e] : 0.0;
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const int64_t e = e0 + (int64_t)u * NT;
-        gxy[u] = g2[e < d.M ? e : 0];
+        for (int u = 0; u < 8; ++u) acc += t[u];
       }
-#pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const int64_t e = e0 + (int64_t)u * NT;
-#pragma unroll
-        for (int c = 0; c < KINC; ++c)
-          if (e < d.M && gxy[u].x == px[c] && gxy[u].y == py[c]) atomicMin(&cell[c], (int)e);
-      }
+      ssum[e] = acc;
     }
-    __syncthreads();
-  }
-  bool use_v = try_v;
-  for (int c = 0; c < k; ++c) use_v = use_v && cell[c] != INT_MAX;
-  // (2) L21^T -> A[j * ld + n0 + c] (row n0 + c of L, column j). On the grid
-  // path the V columns are gathered in step (3), fused with the Schur sums.
-  if (!use_v) {
-    // left-looking: T_I = K12_I - sum_{J<I} L_IJ W_J;  W_I = Linv_II T_I
+  } else {
+    // L21^T = L11^-1 K12, left-looking: T_I = K12_I - sum_{J<I} L_IJ W_J;  W_I = Linv_II T_I
     const int64_t nb0 = (n0 + NB - 1) / NB;
     for (int64_t I = 0; I < nb0; ++I) {
       const int64_t i0 = I * NB + w * 16;   // this wave's 16 rows
@@ -1087,55 +1153,19 @@ __global__ __launch_bounds__(NT) void k_inc_factor(const GPDesc* __restrict__ de
       }
       __syncthreads();   // W_I visible to every wave; Ts free
     }
+    inc_schur_partial(d, nullptr, 0, n0, red);
+    __syncthreads();
+    for (int e = tid; e < ISZ; e += NT) ssum[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
   }
   __syncthreads();
-  // (3) partial sums of L21 L21^T and L21 z1 over this wave's rows (f64 MFMA);
-  // lane (r, q) holds L21[r][j] for rows j = 4s + q, eight 4-row steps in flight
-  {
-    d4 sacc = {0.0, 0.0, 0.0, 0.0}, uacc = {0.0, 0.0, 0.0, 0.0};
-    const int64_t nst = (n0 + 3) >> 2;
-    constexpr int IU = 8;
-    const int cr = (use_v && r < k) ? cell[r] : 0;
-    // source of L21[r][j]: V column of the grid cell (stride PBM) or row n0 + r of A (stride ld)
-    const double* src = use_v ? d.V + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : A + n0 + (r < k ? r : 0);
-    const int64_t sstride = use_v ? PBM : ld;
-    for (int64_t s0 = w; s0 < nst; s0 += (NT / 64) * IU) {
-      double a[IU], zz[IU];
-#pragma unroll
-      for (int u = 0; u < IU; ++u) {
-        const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
-        const bool ok = j < n0;
-        const int64_t jj = ok ? j : 0;
-        a[u] = gp(src)[jj * sstride];
-        zz[u] = gp(d.zv)[jj];
-        a[u] = (ok && r < k) ? a[u] : 0.0;
-        zz[u] = ok ? zz[u] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < IU; ++u) {
-        const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
-        if (use_v && r < k && j < n0) A[j * ld + n0 + r] = a[u];
-        sacc = mfma(a[u], a[u], sacc);
-        uacc = mfma(a[u], zz[u], uacc);
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      red[w][(q + 4 * v) * KINC + r] = sacc[v];
-      if (r == 0) red[w][KINC * KINC + q + 4 * v] = uacc[v];
-    }
-  }
-  __syncthreads();
-  // (4) L22 = chol(K22 - L21 L21^T) and z2, wave 0 (LAPACK dpotf2 order, as in
+  // L22 = chol(K22 - L21 L21^T) and z2, wave 0 (LAPACK dpotf2 order, as in
   // factor_invert_64; lane r holds row r, DPP row broadcasts)
   if (w == 0) {
     double dd[KINC];
 #pragma unroll
     for (int c = 0; c < KINC; ++c) {
-      const int e = r * KINC + c;
-      const double sv = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
       double v = (r == c) ? 1.0 : 0.0;
-      if (r < k && c < k) v = (c <= r ? k_entry(h, X, NL, n0 + r, n0 + c) : 0.0) - sv;
+      if (r < k && c < k) v = (c <= r ? k_entry(h, X, NL, n0 + r, n0 + c) : 0.0) - ssum[r * KINC + c];
       dd[c] = v;
     }
     double rdiag = 1.0;
@@ -1156,9 +1186,8 @@ __global__ __launch_bounds__(NT) void k_inc_factor(const GPDesc* __restrict__ de
       for (int kk = j + 1; kk < KINC; ++kk) dd[kk] -= lu * bcast16(l, kk);
     }
     // z2 = L22^-1 (r2 - L21 z1), r2 = y - m_H (new rows are hifi; gp:133 / gp:421)
-    const int e = KINC * KINC + r;
     double x = 0.0;
-    if (r < k) x = (d.y[n0 + r] - h.meanH) - ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e]));
+    if (r < k) x = (d.y[n0 + r] - h.meanH) - ssum[KINC * KINC + r];
 #pragma unroll
     for (int j = 0; j < KINC; ++j) {
       if (r == j) x *= rdiag;
@@ -1174,39 +1203,44 @@ __global__ __launch_bounds__(NT) void k_inc_factor(const GPDesc* __restrict__ de
     if (fail != INT_MAX && lane == 0) atomicMin(d.status, fail);
   }
   __syncthreads();
-  // (5) new rows of the diagonal-block inverses (rows of a triangular inverse do
-  // not depend on later rows):  Linv[i][c] = -(sum_{m=c}^{i-1} L[i][m] Linv[m][c]) / L[i][i]
+  // new rows of the diagonal-block inverses. In block bb, with old rows O and new
+  // rows W (a triangular inverse's rows do not depend on later rows):
+  //   Linv_WO = -L_WW^-1 (L_WO Linv_OO),   Linv_WW = L_WW^-1
+  // thread c: column c of the new rows, by forward substitution over the <= 16 new rows
   for (int64_t bb = n0 / NB; bb * NB < N; ++bb) {
     double* __restrict__ Li = d.Linv + bb * TILE;
+    const int64_t r0 = n0 > bb * NB ? n0 : bb * NB;
+    const int64_t r1 = N < (bb + 1) * NB ? N : (bb + 1) * NB;
+    const int nO = (int)(r0 - bb * NB), nW = (int)(r1 - r0);
     for (int e = tid; e < TILE; e += NT) {
       const int m = e & 63, c = e >> 6;
       Lb[m * SP + c] = Li[c * NB + m];
     }
-    __syncthreads();
-    const int64_t r0 = n0 > bb * NB ? n0 : bb * NB;
-    const int64_t r1 = N < (bb + 1) * NB ? N : (bb + 1) * NB;
-    for (int64_t gi = r0; gi < r1; ++gi) {
-      const int li = (int)(gi - bb * NB);
-      if (tid < NB) Lrow[tid] = (tid <= li) ? A[(bb * NB + tid) * ld + gi] : 0.0;
-      __syncthreads();
-      if (tid < NB) {
-        const int c = tid;
-        double v = 0.0;
-        if (c < li) {
-          double s0 = 0.0;
-          for (int m = c; m < li; ++m) s0 += Lrow[m] * Lb[m * SP + c];
-          v = -s0 / Lrow[li];
-        } else if (c == li) {
-          v = 1.0 / Lrow[li];
-        }
-        Lb[li * SP + c] = v;
-      }
-      __syncthreads();
+    for (int e = tid; e < nW * NB; e += NT) {
+      const int i = e >> 6, m = e & 63;
+      Ln[i * SP + m] = (m <= nO + i) ? A[(bb * NB + m) * ld + r0 + i] : 0.0;
     }
-    for (int e = tid; e < TILE; e += NT) {
-      const int m = e & 63, c = e >> 6;
-      const int64_t gm = bb * NB + m;
-      if (gm >= r0 && gm < r1) Li[c * NB + m] = Lb[m * SP + c];
+    __syncthreads();
+    if (tid < NB) {
+      const int c = tid;
+      double xs[KINC];
+#pragma unroll
+      for (int i = 0; i < KINC; ++i) {
+        xs[i] = 0.0;
+        if (i < nW) {
+          double t;
+          if (c < nO) {
+            t = 0.0;
+            for (int m = c; m < nO; ++m) t -= Ln[i * SP + m] * Lb[m * SP + c];
+          } else {
+            t = (c == nO + i) ? 1.0 : 0.0;
+          }
+#pragma unroll
+          for (int i2 = 0; i2 < i; ++i2) t -= Ln[i * SP + nO + i2] * xs[i2];
+          xs[i] = t / Ln[i * SP + nO + i];
+          Li[c * NB + nO + i] = xs[i];
+        }
+      }
     }
     __syncthreads();
   }
@@ -1377,24 +1411,75 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
   }
 }
 
-// Append the batch's new (device-resident) rows to every model's training set:
-// one launch for the whole batch instead of two copies per model.
-__global__ __launch_bounds__(64) void k_append(const GPDesc* __restrict__ descs) {
+// Append the batch's new (device-resident) rows to every model's training set
+// (one launch for the whole batch instead of two copies per model) and, for GPs
+// on the incremental path with V resident for their leading rows (n0 > 0,
+// vres >= n0), find the new points on the grid: iscr[0] = 1 if all are grid
+// cells, iscr[1 + c] = cell of point c (k_inc_l21 gathers those V columns).
+constexpr int APT = 1024;
+__global__ __launch_bounds__(APT) void k_append(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.x];
-  const int64_t k = d.k_new;
-  if (k <= 0) return;
-  double* X = const_cast<double*>(d.X);
-  double* y = const_cast<double*>(d.y);
-  const int64_t at = d.N - k;
-  for (int64_t e = threadIdx.x; e < 3 * k; e += 64) {
-    if (e < 2 * k) X[2 * at + e] = d.srcX[e];
-    else y[at + e - 2 * k] = d.srcY[e - 2 * k];
+  const int tid = threadIdx.x;
+  const int64_t kn = d.k_new;
+  if (kn > 0 && d.srcX) {
+    double* X = const_cast<double*>(d.X);
+    double* y = const_cast<double*>(d.y);
+    const int64_t at = d.N - kn;
+    for (int64_t e = tid; e < 3 * kn; e += APT) {
+      if (e < 2 * kn) X[2 * at + e] = d.srcX[e];
+      else y[at + e - 2 * kn] = d.srcY[e - 2 * kn];
+    }
   }
+  const int64_t n0 = d.n0;
+  const int k = (int)(d.N - n0);
+  const bool try_v = n0 > 0 && k > 0 && k <= KINC && d.vres >= n0 && d.V != nullptr && d.M > 0;
+  if (!try_v) {
+    if (tid == 0 && d.iscr) d.iscr[0] = 0.0;
+    return;
+  }
+  __shared__ int cell[KINC];
+  if (tid < KINC) cell[tid] = INT_MAX;
+  __syncthreads();   // the copied rows are visible to the whole workgroup
+  double px[KINC], py[KINC];
+#pragma unroll
+  for (int c = 0; c < KINC; ++c) {
+    px[c] = c < k ? d.X[2 * (n0 + c)] : __builtin_nan("");
+    py[c] = c < k ? d.X[2 * (n0 + c) + 1] : __builtin_nan("");
+  }
+  const GLOBAL dv2* g2 = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid));
+  constexpr int SB = 8;   // grid loads in flight per thread
+  for (int64_t e0 = tid; e0 < d.M; e0 += APT * SB) {
+    dv2 gxy[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int64_t e = e0 + (int64_t)u * APT;
+      gxy[u] = g2[e < d.M ? e : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int64_t e = e0 + (int64_t)u * APT;
+      bool hit = false;
+#pragma unroll
+      for (int c = 0; c < KINC; ++c) hit = hit || (gxy[u].x == px[c] && gxy[u].y == py[c]);
+      if (hit && e < d.M) {
+#pragma unroll
+        for (int c = 0; c < KINC; ++c)
+          if (gxy[u].x == px[c] && gxy[u].y == py[c]) atomicMin(&cell[c], (int)e);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    bool ok = true;
+    for (int c = 0; c < k; ++c) ok = ok && cell[c] != INT_MAX;
+    d.iscr[0] = ok ? 1.0 : 0.0;
+  }
+  if (tid < KINC) d.iscr[1 + tid] = (tid < k && cell[tid] != INT_MAX) ? (double)cell[tid] : 0.0;
 }
 
 // ---------------------------------------------------------------------------
 hipError_t launch_append(const GPDesc* d, int count, hipStream_t s) {
-  hipLaunchKernelGGL(k_append, dim3(count), dim3(64), 0, s, d);
+  hipLaunchKernelGGL(k_append, dim3(count), dim3(APT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s) {
@@ -1426,8 +1511,10 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
   hipLaunchKernelGGL(k_extract_z, dim3((unsigned)((max_n + NT - 1) / NT), count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
-hipError_t launch_inc_factor(const GPDesc* d, int count, hipStream_t s) {
-  hipLaunchKernelGGL(k_inc_factor, dim3(count), dim3(NT), 0, s, d);
+hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s) {
+  const int64_t nch = max_n0 > 0 ? (max_n0 + ICH - 1) / ICH : 1;
+  hipLaunchKernelGGL(k_inc_l21, dim3((unsigned)nch, count), dim3(NT), 0, s, d);
+  hipLaunchKernelGGL(k_inc_finish, dim3(count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {
