@@ -514,6 +514,14 @@ int copy_rows(mfgp_model* m, int64_t at, const double* X, const double* y, int64
 extern "C" {
 
 const char* mfgp_last_error(void) { return g_err.c_str(); }
+
+#ifdef MFGP_STAMPS
+// diagnostic builds only (tools/): device buffer for the kernels' phase stamps
+int mfgp_debug_set_stamps(void* p) {
+  HIP_TRY(set_stamps((long long*)p));
+  return MFGP_OK;
+}
+#endif
 const char* mfgp_version(void) { return "mfgp_hip 0.2 gfx950 f64"; }
 
 int mfgp_ctx_create(int device, mfgp_ctx** out) {

@@ -71,6 +71,9 @@ hipError_t launch_panel_diag(const GPDesc* d, int count, int kb, int64_t max_bel
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s);
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
+#ifdef MFGP_STAMPS
+hipError_t set_stamps(long long* p);
+#endif
 hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream_t s);
 hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);

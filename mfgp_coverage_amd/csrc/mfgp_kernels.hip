@@ -1096,12 +1096,37 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
   __shared__ double red[NT / 64][ISZ];
   __shared__ double ssum[ISZ];
   __shared__ double Ts[NB * KINC];      // T_I image [64][16]
-  __shared__ double Lb[NB * SP];        // Linv block, row-major
-  __shared__ double Ln[KINC * SP];      // new rows of L inside the block
+  __shared__ double Lb[NB * NB];        // Linv block bb0 (old rows), row-major [m][c]
+  __shared__ double Ln[KINC * NB];      // new rows of L inside the current block, [i][m]
+  __shared__ double L22s[KINC * KINC];  // L22, row-major
+  __shared__ double K22s[KINC * KINC];  // K22 (+ noise + jitter on the diagonal), row-major
+  __shared__ double Ps[KINC * NB];      // L_WO Linv_OO of the current block, [i][c]
+  const int64_t bb0 = n0 / NB;
+  const int nO0 = (int)(n0 - bb0 * NB);   // old rows in block bb0
+  STAMP(20);
   if (tid == 0) *d.status = INT_MAX;
+  {
+    // one K22 entry per thread (gp:523-529 via k_entry)
+    const int a = tid / KINC, b = tid % KINC;
+    K22s[tid] = (a < k && b <= a) ? k_entry(h, X, NL, n0 + a, n0 + b) : 0.0;
+  }
   const bool gathered = n0 > 0 && d.iscr[0] != 0.0;
   inc_init_blocks(d, gathered ? n0 : 0, nblocks_factor(N) * NB, true);
+  // block bb0's old Linv rows (never a newly initialised block when nO0 > 0),
+  // sixteen loads in flight per thread
+  if (nO0 > 0) {
+    const double* __restrict__ Li = d.Linv + bb0 * TILE;
+    double t[TILE / NT];
+#pragma unroll
+    for (int u = 0; u < TILE / NT; ++u) t[u] = gp(Li)[tid + u * NT];
+#pragma unroll
+    for (int u = 0; u < TILE / NT; ++u) {
+      const int e = tid + u * NT, m = e & 63, c = e >> 6;
+      Lb[m * NB + c] = t[u];
+    }
+  }
   __syncthreads();
+  STAMP(21);
   if (gathered) {
     const int nch = (int)((n0 + ICH - 1) / ICH);
     for (int e = tid; e < ISZ; e += NT) {
@@ -1157,7 +1182,14 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
     __syncthreads();
     for (int e = tid; e < ISZ; e += NT) ssum[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
   }
+  STAMP(22);
+  // new rows' old-column part of block bb0 (L21 entries, in A)
+  for (int e = tid; e < k * NB; e += NT) {
+    const int i = e >> 6, m = e & 63;
+    if (m < nO0) Ln[i * NB + m] = A[(bb0 * NB + m) * ld + n0 + i];
+  }
   __syncthreads();
+  STAMP(23);
   // L22 = chol(K22 - L21 L21^T) and z2, wave 0 (LAPACK dpotf2 order, as in
   // factor_invert_64; lane r holds row r, DPP row broadcasts)
   if (w == 0) {
@@ -1165,9 +1197,10 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
 #pragma unroll
     for (int c = 0; c < KINC; ++c) {
       double v = (r == c) ? 1.0 : 0.0;
-      if (r < k && c < k) v = (c <= r ? k_entry(h, X, NL, n0 + r, n0 + c) : 0.0) - ssum[r * KINC + c];
+      if (r < k && c < k) v = K22s[r * KINC + c] - ssum[r * KINC + c];
       dd[c] = v;
     }
+    const double yr = (r < k) ? d.y[n0 + r] : 0.0;
     double rdiag = 1.0;
     int fail = INT_MAX;
 #pragma unroll
@@ -1187,7 +1220,7 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
     }
     // z2 = L22^-1 (r2 - L21 z1), r2 = y - m_H (new rows are hifi; gp:133 / gp:421)
     double x = 0.0;
-    if (r < k) x = (d.y[n0 + r] - h.meanH) - ssum[KINC * KINC + r];
+    if (r < k) x = (yr - h.meanH) - ssum[KINC * KINC + r];
 #pragma unroll
     for (int j = 0; j < KINC; ++j) {
       if (r == j) x *= rdiag;
@@ -1196,31 +1229,56 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
     }
     if (lane < k) {
 #pragma unroll
-      for (int c = 0; c < KINC; ++c)
+      for (int c = 0; c < KINC; ++c) {
+        L22s[lane * KINC + c] = (c <= lane) ? dd[c] : 0.0;
         if (c <= lane) A[(n0 + c) * ld + n0 + lane] = dd[c];
+      }
       d.zv[n0 + lane] = x;
     }
     if (fail != INT_MAX && lane == 0) atomicMin(d.status, fail);
   }
   __syncthreads();
+  STAMP(24);
   // new rows of the diagonal-block inverses. In block bb, with old rows O and new
   // rows W (a triangular inverse's rows do not depend on later rows):
   //   Linv_WO = -L_WW^-1 (L_WO Linv_OO),   Linv_WW = L_WW^-1
   // thread c: column c of the new rows, by forward substitution over the <= 16 new rows
-  for (int64_t bb = n0 / NB; bb * NB < N; ++bb) {
+  for (int64_t bb = bb0; bb * NB < N; ++bb) {
     double* __restrict__ Li = d.Linv + bb * TILE;
     const int64_t r0 = n0 > bb * NB ? n0 : bb * NB;
     const int64_t r1 = N < (bb + 1) * NB ? N : (bb + 1) * NB;
     const int nO = (int)(r0 - bb * NB), nW = (int)(r1 - r0);
-    for (int e = tid; e < TILE; e += NT) {
-      const int m = e & 63, c = e >> 6;
-      Lb[m * SP + c] = Li[c * NB + m];
-    }
+    const int a0 = (int)(r0 - n0);   // first new row of this block, as a row of L22
+    // L22 part of the new rows (columns n0.. of this block)
     for (int e = tid; e < nW * NB; e += NT) {
       const int i = e >> 6, m = e & 63;
-      Ln[i * SP + m] = (m <= nO + i) ? A[(bb * NB + m) * ld + r0 + i] : 0.0;
+      const int64_t col = bb * NB + m;
+      if (col >= n0) {
+        const int b = (int)(col - n0);
+        Ln[i * NB + m] = (b <= a0 + i) ? L22s[(a0 + i) * KINC + b] : 0.0;
+      } else if (bb != bb0) {
+        Ln[i * NB + m] = A[col * ld + r0 + i];
+      }
     }
     __syncthreads();
+    // P = L_WO Linv_OO: element (i, c) per thread, Linv_OO lower triangular (its
+    // upper part is stored as zeros), so the sum runs over all old rows m
+    if (nO > 0) {
+      for (int e = tid; e < nW * NB; e += NT) {
+        const int i = e >> 6, c = e & 63;
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+        int m = 0;
+        for (; m + 4 <= nO; m += 4) {
+          p0 += Ln[i * NB + m] * Lb[m * NB + c];
+          p1 += Ln[i * NB + m + 1] * Lb[(m + 1) * NB + c];
+          p2 += Ln[i * NB + m + 2] * Lb[(m + 2) * NB + c];
+          p3 += Ln[i * NB + m + 3] * Lb[(m + 3) * NB + c];
+        }
+        for (; m < nO; ++m) p0 += Ln[i * NB + m] * Lb[m * NB + c];
+        Ps[i * NB + c] = (p0 + p1) + (p2 + p3);
+      }
+      __syncthreads();
+    }
     if (tid < NB) {
       const int c = tid;
       double xs[KINC];
@@ -1228,22 +1286,17 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
       for (int i = 0; i < KINC; ++i) {
         xs[i] = 0.0;
         if (i < nW) {
-          double t;
-          if (c < nO) {
-            t = 0.0;
-            for (int m = c; m < nO; ++m) t -= Ln[i * SP + m] * Lb[m * SP + c];
-          } else {
-            t = (c == nO + i) ? 1.0 : 0.0;
-          }
+          double t = (c < nO) ? -Ps[i * NB + c] : ((c == nO + i) ? 1.0 : 0.0);
 #pragma unroll
-          for (int i2 = 0; i2 < i; ++i2) t -= Ln[i * SP + nO + i2] * xs[i2];
-          xs[i] = t / Ln[i * SP + nO + i];
+          for (int i2 = 0; i2 < i; ++i2) t -= Ln[i * NB + nO + i2] * xs[i2];
+          xs[i] = t / Ln[i * NB + nO + i];
           Li[c * NB + nO + i] = xs[i];
         }
       }
     }
     __syncthreads();
   }
+  STAMP(25);
 }
 
 // ---------------------------------------------------------------------------
@@ -1478,6 +1531,9 @@ __global__ __launch_bounds__(APT) void k_append(const GPDesc* __restrict__ descs
 }
 
 // ---------------------------------------------------------------------------
+#ifdef MFGP_STAMPS
+hipError_t set_stamps(long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
+#endif
 hipError_t launch_append(const GPDesc* d, int count, hipStream_t s) {
   hipLaunchKernelGGL(k_append, dim3(count), dim3(APT), 0, s, d);
   return hipGetLastError();
