@@ -58,8 +58,10 @@ int mfgp_ctx_synchronize(mfgp_ctx* ctx);
  * Results agree with the full path to rounding. 0 = refactor and recompute V
  * on every update, as the reference does. */
 int mfgp_ctx_set_incremental(mfgp_ctx* ctx, int enable);
-/* Kernel timing (HIP events around every predict-kernel launch: fused predict
- * or one-pass incremental predict). */
+/* Kernel timing with HIP events on the launch stream: enable = 1 times every
+ * predict-kernel launch (fused predict or one-pass incremental predict) and
+ * every factor stage; 2 times the predict launches only (each event pair is a
+ * few microseconds of stream time); 0 = off. */
 int mfgp_ctx_enable_timing(mfgp_ctx* ctx, int enable);
 /* Sum of predict-kernel durations (ms) and launch count since the last reset;
  * also the same for the factor stage (assemble + blocked Cholesky). */

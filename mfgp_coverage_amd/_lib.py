@@ -136,8 +136,9 @@ class Context:
         or full refactor + full V recompute on every update (the reference's work)."""
         check(lib().mfgp_ctx_set_incremental(self.handle, 1 if on else 0))
 
-    def enable_timing(self, on=True):
-        check(lib().mfgp_ctx_enable_timing(self.handle, 1 if on else 0))
+    def enable_timing(self, on=True, predict_only=False):
+        """HIP-event timing of the predict launches (and, unless predict_only, the factor stages)."""
+        check(lib().mfgp_ctx_enable_timing(self.handle, (2 if predict_only else 1) if on else 0))
 
     def reset_timing(self):
         check(lib().mfgp_ctx_reset_timing(self.handle))

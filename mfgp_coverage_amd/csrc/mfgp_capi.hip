@@ -64,8 +64,8 @@ struct mfgp_ctx {
   // workspace (V scratch + device outputs for host-pointer calls)
   double* ws = nullptr;
   size_t ws_bytes = 0;
-  // timing
-  bool timing = false;
+  // timing: 0 off, 1 predict + factor launches, 2 predict launches only
+  int timing = 0;
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
   double t_predict = 0.0, t_factor = 0.0;
@@ -157,7 +157,8 @@ hipEvent_t ev_get(mfgp_ctx* c) {
 }
 
 int ev_begin(mfgp_ctx* c, EvPair& p, int kind) {
-  if (!c->timing) return MFGP_OK;
+  p.a = p.b = nullptr;
+  if (!c->timing || (c->timing == 2 && kind != 0)) return MFGP_OK;
   p.a = ev_get(c);
   p.b = ev_get(c);
   p.kind = kind;
@@ -166,7 +167,7 @@ int ev_begin(mfgp_ctx* c, EvPair& p, int kind) {
 }
 
 int ev_end(mfgp_ctx* c, EvPair& p) {
-  if (!c->timing) return MFGP_OK;
+  if (!p.a) return MFGP_OK;
   HIP_TRY(hipEventRecord(p.b, c->stream));
   c->pending.push_back(p);
   return MFGP_OK;
@@ -591,7 +592,7 @@ int mfgp_ctx_set_incremental(mfgp_ctx* c, int enable) {
 
 int mfgp_ctx_enable_timing(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
-  c->timing = enable != 0;
+  c->timing = (enable == 2) ? 2 : (enable != 0 ? 1 : 0);
   return MFGP_OK;
 }
 
@@ -867,23 +868,24 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     off += ki;
     if (!c->incremental) m->factored = false;   // reference behaviour: refactor every update
   }
-  std::vector<mfgp_model*> order;
+  std::vector<mfgp_model*> order, porder;
   std::vector<int64_t> oo_ord;
-  for (int b0 = 0; b0 < count; b0 += MAXB) {
-    const int nb = std::min(MAXB, count - b0);
+  constexpr int CB = MAXB / 2;   // one descriptor slot per sub-batch: [factor order | predict order]
+  for (int b0 = 0; b0 < count; b0 += CB) {
+    const int nb = std::min(CB, count - b0);
     if (do_predict) {
       for (int i = 0; i < nb; ++i)
         if (models[b0 + i]->M > 0 && (rc = ensure_v(models[b0 + i]))) return rc;
     }
     int slot;
-    GPDesc* hd = nullptr;
-    const GPDesc* dd = nullptr;
+    GPDesc* hd = acquire_slot(c, slot, rc);
+    if (!hd) return rc;
+    // factor descriptors, ordered [bordered appends | full refactors | current]:
+    // k_append (copies + grid-cell search) runs over all of them, the factor
+    // kernels over their contiguous sub-ranges
+    int ninc = 0, nfull = 0;
+    order.clear();
     if (do_factor) {
-      // one descriptor slot ordered [bordered appends | full refactors | current]:
-      // k_append (copies + grid-cell search) runs over all of them, the factor
-      // kernels over their contiguous sub-ranges
-      order.clear();
-      int ninc = 0, nfull = 0;
       for (int i = 0; i < nb; ++i)
         if (!factor_current(models[b0 + i]) && can_inc_factor(models[b0 + i])) order.push_back(models[b0 + i]);
       ninc = (int)order.size();
@@ -892,7 +894,6 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       nfull = (int)order.size() - ninc;
       for (int i = 0; i < nb; ++i)
         if (factor_current(models[b0 + i])) order.push_back(models[b0 + i]);
-      if (!(hd = acquire_slot(c, slot, rc))) return rc;
       for (int i = 0; i < nb; ++i) {
         mfgp_model* m = order[i];
         if (i < ninc) fill_inc_desc(hd[i], m);
@@ -904,48 +905,48 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
           hd[i].k_new = k[mi];
         }
       }
-      if ((rc = upload_slot(c, slot, nb, &dd))) return rc;
-      if (dev_src || ninc > 0) HIP_TRY(launch_append(dd, nb, c->stream));
-      if (ninc > 0 && (rc = enqueue_inc_factor(c, dd, hd, ninc))) return rc;
-      if (nfull > 0 && (rc = enqueue_factor(c, dd + ninc, hd + ninc, nfull))) return rc;
-      if ((rc = release_slot(c, slot))) return rc;
-      for (int i = 0; i < ninc + nfull; ++i) {
+      for (int i = 0; i < ninc + nfull; ++i) {   // host bookkeeping of the factors enqueued below
         if (i < ninc) mark_inc_factor(order[i]);
         else mark_full_factor(order[i]);
         c->async_status.push_back(order[i]->status);
       }
     }
+    // predict descriptors (state after the factor step), ordered
+    // [one-pass predicts over resident V | full predicts]
+    int nv = 0, np = 0;
     if (do_predict) {
-      // one slot ordered [one-pass predicts over resident V | full predicts]
-      order.clear();
+      porder.clear();
       oo_ord.clear();
       for (int pass = 0; pass < 2; ++pass)
         for (int i = 0; i < nb; ++i) {
           mfgp_model* m = models[b0 + i];
           if (m->M == 0 || can_vstream(m) != (pass == 0)) continue;
-          order.push_back(m);
+          porder.push_back(m);
           oo_ord.push_back(out_off[b0 + i]);
         }
-      int nv = 0;
-      while (nv < (int)order.size() && can_vstream(order[nv])) ++nv;
-      const int np = (int)order.size();
-      if (np > 0) {
-        if (!(hd = acquire_slot(c, slot, rc))) return rc;
-        for (int i = 0; i < np; ++i) {
-          fill_desc(hd[i], order[i]);
-          if (i < nv) hd[i].n0 = order[i]->v_n;
-          hd[i].mu = mu + oo_ord[i];
-          hd[i].var = var + oo_ord[i];
-        }
-        if ((rc = upload_slot(c, slot, np, &dd))) return rc;
-        if (nv > 0 && (rc = enqueue_vstream(c, dd, hd, nv))) return rc;
-        if (np > nv && (rc = enqueue_predict(c, dd + nv, hd + nv, np - nv))) return rc;
-        if ((rc = release_slot(c, slot))) return rc;
-        for (int i = 0; i < np; ++i) {
-          order[i]->v_n = order[i]->NL + order[i]->NH;
-          (i < nv ? order[i]->n_vstream : order[i]->n_full_predict) += 1;
-        }
+      np = (int)porder.size();
+      while (nv < np && can_vstream(porder[nv])) ++nv;
+      for (int i = 0; i < np; ++i) {
+        GPDesc& pd = hd[nb + i];
+        fill_desc(pd, porder[i]);
+        if (i < nv) pd.n0 = porder[i]->v_n;
+        pd.mu = mu + oo_ord[i];
+        pd.var = var + oo_ord[i];
       }
+    }
+    const GPDesc* dd = nullptr;
+    if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
+    if (do_factor) {
+      if (dev_src || ninc > 0) HIP_TRY(launch_append(dd, nb, c->stream));
+      if (ninc > 0 && (rc = enqueue_inc_factor(c, dd, hd, ninc))) return rc;
+      if (nfull > 0 && (rc = enqueue_factor(c, dd + ninc, hd + ninc, nfull))) return rc;
+    }
+    if (nv > 0 && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
+    if (np > nv && (rc = enqueue_predict(c, dd + nb + nv, hd + nb + nv, np - nv))) return rc;
+    if ((rc = release_slot(c, slot))) return rc;
+    for (int i = 0; i < np; ++i) {
+      porder[i]->v_n = porder[i]->NL + porder[i]->NH;
+      (i < nv ? porder[i]->n_vstream : porder[i]->n_full_predict) += 1;
     }
   }
   if (flags & MFGP_ASYNC) return MFGP_OK;
