@@ -163,9 +163,9 @@ def main():
         def step(s):
             for mdl in models:
                 mdl.truncate(NH0)
+            # VarMax of every seed (np.amax(cov), simulator.py:1014) fused into the predict epilogue
             _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), ks, mu.data_ptr(),
-                                      var.data_ptr(), asynchronous=True)
-            varmax[s] = var.view(B, M).amax(dim=1)
+                                      var.data_ptr(), asynchronous=True, vmax_ptr=varmax[s].data_ptr())
 
         def aggregate(traj):
             _, agg_mean, agg_std = gather_trajectories(traj, world)   # the single RCCL exchange

@@ -115,6 +115,14 @@ int mfgp_get_factor(mfgp_model* m, double* L_out);
  * order). One set of launches serves the whole batch. flags: MFGP_ASYNC. */
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y,
                               const int64_t* k, double* mu, double* var, int flags);
+/* mfgp_batch_append_predict plus fused reductions of each model's variance:
+ * var_max[i] = np.amax of the posterior covariance (its largest diagonal entry,
+ * simulator.py:672, 842, 1014) and var_argmax[i] = the first cell attaining it
+ * (the argmax of compute_sample_points, sim:352). Either may be NULL; both are
+ * device memory, written in stream order (no host round trip). */
+int mfgp_batch_append_predict_ex(mfgp_model** models, int count, const double* X, const double* y,
+                                 const int64_t* k, double* mu, double* var, double* var_max,
+                                 int64_t* var_argmax, int flags);
 /* The two halves of mfgp_batch_append_predict (append + refactor only; predict
  * from the current factors only). mfgp_batch_predict needs a current factor. */
 int mfgp_batch_append_factor(mfgp_model** models, int count, const double* X, const double* y,

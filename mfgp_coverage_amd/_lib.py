@@ -30,6 +30,9 @@ SIGNATURES = {
     "mfgp_ctx_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "mfgp_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "mfgp_ctx_set_incremental": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mfgp_batch_append_predict_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "mfgp_model_stats": (ctypes.c_int, [ctypes.c_void_p, _c_int64_p, ctypes.c_int]),
     "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int64_p, _c_double_p, _c_int64_p]),
@@ -244,18 +247,26 @@ class Model:
         check(lib().mfgp_truncate(self.handle, int(n_keep_hifi)))
 
 
-def batch_append_predict(models, X, y, k, mu_ptr, var_ptr, asynchronous=False):
+def batch_append_predict(models, X, y, k, mu_ptr, var_ptr, asynchronous=False, vmax_ptr=None, vargmax_ptr=None):
     """Batched update+predict over device-resident models.
 
     X, y: integer device (or host) addresses of the concatenated new rows;
-    k: per-model row counts; mu_ptr/var_ptr: device addresses of [sum M] outputs.
+    k: per-model row counts; mu_ptr/var_ptr: device addresses of [sum M] outputs;
+    vmax_ptr / vargmax_ptr: optional device addresses of [n] float64 / int64 outputs
+    (fused np.amax / np.argmax of each model's variance).
     """
     n = len(models)
     arr = (ctypes.c_void_p * n)(*[m.handle.value for m in models])
     ks = (ctypes.c_int64 * n)(*[int(v) for v in k])
-    rc = lib().mfgp_batch_append_predict(arr, n, ctypes.c_void_p(X), ctypes.c_void_p(y), ks,
-                                         ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
-                                         ASYNC if asynchronous else 0)
+    if vmax_ptr is None and vargmax_ptr is None:
+        rc = lib().mfgp_batch_append_predict(arr, n, ctypes.c_void_p(X), ctypes.c_void_p(y), ks,
+                                             ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
+                                             ASYNC if asynchronous else 0)
+    else:
+        rc = lib().mfgp_batch_append_predict_ex(arr, n, ctypes.c_void_p(X), ctypes.c_void_p(y), ks,
+                                                ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
+                                                ctypes.c_void_p(vmax_ptr), ctypes.c_void_p(vargmax_ptr),
+                                                ASYNC if asynchronous else 0)
     check(rc)
 
 

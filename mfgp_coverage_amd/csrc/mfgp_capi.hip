@@ -105,6 +105,7 @@ struct mfgp_model {
   // resident V = L^-1 psi^T [vtiles][vld][PBM]; rows [0, v_n) valid for the current factor and grid
   double* V = nullptr;
   int64_t vld = 0, vtiles = 0, v_n = 0;
+  double* tred = nullptr;     // [vtiles][2] per-tile (max, argmax) of var
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0;
 };
@@ -275,6 +276,11 @@ int ensure_v(mfgp_model* m) {
   if (m->V) HIP_TRY(hipFree(m->V));
   m->V = V;
   m->vld = vld;
+  if (tiles > m->vtiles || !m->tred) {
+    if (m->tred) HIP_TRY(hipFree(m->tred));
+    m->tred = nullptr;
+    HIP_TRY(hipMalloc(&m->tred, sizeof(double) * 2 * tiles));
+  }
   m->vtiles = tiles;
   return MFGP_OK;
 }
@@ -322,6 +328,9 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.iscr = m->iscr;
   d.mu = nullptr;
   d.var = nullptr;
+  d.vmax = nullptr;
+  d.vargmax = nullptr;
+  d.tred = m->tred;
   d.status = m->status;
   d.srcX = nullptr;
   d.srcY = nullptr;
@@ -653,6 +662,7 @@ void mfgp_model_destroy(mfgp_model* m) {
   if (m->status) (void)hipFree(m->status);
   if (m->grid) (void)hipFree(m->grid);
   if (m->V) (void)hipFree(m->V);
+  if (m->tred) (void)hipFree(m->tred);
   delete m;
 }
 
@@ -834,7 +844,8 @@ int mfgp_get_factor(mfgp_model* m, double* L_out) {
 // per kind: bordered appends (k_inc_factor) and full refactors side by side,
 // then one-pass predicts over the resident V (k_vstream) and full predicts.
 static int batch_run(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
-                     double* mu, double* var, int flags, bool do_factor, bool do_predict) {
+                     double* mu, double* var, double* vmax, int64_t* vargmax, int flags, bool do_factor,
+                     bool do_predict) {
   if (!models || count <= 0) return set_err(MFGP_ERR_ARG, "empty batch");
   mfgp_ctx* c = models[0]->ctx;
   int rc = MFGP_OK;
@@ -932,6 +943,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         if (i < nv) pd.n0 = porder[i]->v_n;
         pd.mu = mu + oo_ord[i];
         pd.var = var + oo_ord[i];
+        const int64_t mi = std::find(models + b0, models + b0 + nb, porder[i]) - models;
+        if (vmax) pd.vmax = vmax + mi;
+        if (vargmax) pd.vargmax = vargmax + mi;
       }
     }
     const GPDesc* dd = nullptr;
@@ -943,6 +957,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     }
     if (nv > 0 && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
     if (np > nv && (rc = enqueue_predict(c, dd + nb + nv, hd + nb + nv, np - nv))) return rc;
+    if (np > 0 && (vmax || vargmax)) HIP_TRY(launch_var_argmax(dd + nb, np, c->stream));
     if ((rc = release_slot(c, slot))) return rc;
     for (int i = 0; i < np; ++i) {
       porder[i]->v_n = porder[i]->NL + porder[i]->NH;
@@ -955,16 +970,24 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
 
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                               double* mu, double* var, int flags) {
-  return batch_run(models, count, X, y, k, mu, var, flags, true, true);
+  return batch_run(models, count, X, y, k, mu, var, nullptr, nullptr, flags, true, true);
+}
+
+int mfgp_batch_append_predict_ex(mfgp_model** models, int count, const double* X, const double* y,
+                                 const int64_t* k, double* mu, double* var, double* var_max, int64_t* var_argmax,
+                                 int flags) {
+  if ((var_max && !is_device_ptr(var_max)) || (var_argmax && !is_device_ptr(var_argmax)))
+    return set_err(MFGP_ERR_ARG, "var_max / var_argmax must be device memory");
+  return batch_run(models, count, X, y, k, mu, var, var_max, var_argmax, flags, true, true);
 }
 
 int mfgp_batch_append_factor(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                              int flags) {
-  return batch_run(models, count, X, y, k, nullptr, nullptr, flags, true, false);
+  return batch_run(models, count, X, y, k, nullptr, nullptr, nullptr, nullptr, flags, true, false);
 }
 
 int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, int flags) {
-  return batch_run(models, count, nullptr, nullptr, nullptr, mu, var, flags, false, true);
+  return batch_run(models, count, nullptr, nullptr, nullptr, mu, var, nullptr, nullptr, flags, false, true);
 }
 
 }  // extern "C"

@@ -743,6 +743,55 @@ __device__ __forceinline__ void half_mma(const double* frag, const double* __res
   }
 }
 
+// Fused np.amax / np.argmax of a GP's variance (simulator.py:672, 842, 1014 and
+// the argmax of compute_sample_points, sim:352): every cell tile publishes its
+// (max, first argmax) from its epilogue; k_var_argmax reduces the tiles (the
+// kernel boundary orders the partials -- a device-scope fence per tile would
+// write back the XCD's L2 each time). Called by wave 0 of the tile's workgroup,
+// lane l holding cell c0 + l (valid if inside the grid).
+__device__ __forceinline__ void argmax_pair(double& bv, int64_t& bi, double ov, int64_t oi) {
+  if (ov > bv || (ov == bv && oi < bi)) {
+    bv = ov;
+    bi = oi;
+  }
+}
+
+__device__ void var_argmax_tile(const GPDesc& d, double v, int64_t c, bool valid) {
+  const int lane = threadIdx.x & 63;
+  double bv = valid ? v : -__builtin_inf();
+  int64_t bi = valid ? c : INT64_MAX;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  if (lane == 0) {
+    d.tred[2 * blockIdx.x] = bv;
+    d.tred[2 * blockIdx.x + 1] = (double)bi;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_var_argmax(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.x];
+  if (d.M <= 0 || (!d.vmax && !d.vargmax)) return;
+  const int64_t ntiles = ntiles_grid(d.M);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ double sv[NT / 64];
+  __shared__ int64_t si[NT / 64];
+  double bv = -__builtin_inf();
+  int64_t bi = INT64_MAX;
+  for (int64_t t = tid; t < ntiles; t += NT) argmax_pair(bv, bi, d.tred[2 * t], (int64_t)d.tred[2 * t + 1]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  if (lane == 0) {
+    sv[w] = bv;
+    si[w] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int j = 1; j < NT / 64; ++j) argmax_pair(bv, bi, sv[j], si[j]);
+    if (d.vmax) *d.vmax = bv;
+    if (d.vargmax) *d.vargmax = bi;
+  }
+}
+
 __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
   const int64_t M = d.M;
@@ -955,12 +1004,14 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
   __syncthreads();
   if (tid < PBM) {
     const int64_t c = c0 + tid;
+    const double vs = (red[0 * PBM + tid] + red[1 * PBM + tid]) + (red[2 * PBM + tid] + red[3 * PBM + tid]);
+    const double ms = (red[4 * PBM + tid] + red[5 * PBM + tid]) + (red[6 * PBM + tid] + red[7 * PBM + tid]);
+    const double vc = h.kss - vs;
     if (c < M) {
-      const double vs = (red[0 * PBM + tid] + red[1 * PBM + tid]) + (red[2 * PBM + tid] + red[3 * PBM + tid]);
-      const double ms = (red[4 * PBM + tid] + red[5 * PBM + tid]) + (red[6 * PBM + tid] + red[7 * PBM + tid]);
       d.mu[c] = ms + h.meanH;
-      d.var[c] = h.kss - vs;
+      d.var[c] = vc;
     }
+    if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M);
   }
 }
 
@@ -1457,10 +1508,12 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
         }
       }
     }
+    const double vc = h.kss - vsum;
     if (c < M) {
       d.mu[c] = msum + h.meanH;
-      d.var[c] = h.kss - vsum;
+      d.var[c] = vc;
     }
+    if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M);
   }
 }
 
@@ -1571,6 +1624,10 @@ hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStre
   const int64_t nch = max_n0 > 0 ? (max_n0 + ICH - 1) / ICH : 1;
   hipLaunchKernelGGL(k_inc_l21, dim3((unsigned)nch, count), dim3(NT), 0, s, d);
   hipLaunchKernelGGL(k_inc_finish, dim3(count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_var_argmax(const GPDesc* d, int count, hipStream_t s) {
+  hipLaunchKernelGGL(k_var_argmax, dim3(count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {

@@ -258,8 +258,14 @@ def test_batched_device_incremental_headline_pattern(full_ctx):
                 mdl.truncate(NH0)
             mu_d = torch.empty(B * M, dtype=torch.float64, device="cuda")
             var_d = torch.empty(B * M, dtype=torch.float64, device="cuda")
+            vmax = torch.full((B,), -1.0, dtype=torch.float64, device="cuda")
+            varg = torch.full((B,), -1, dtype=torch.int64, device="cuda")
             _lib.batch_append_predict(models, Xd.data_ptr(), yd.data_ptr(), [k] * B, mu_d.data_ptr(),
-                                      var_d.data_ptr())
+                                      var_d.data_ptr(), vmax_ptr=vmax.data_ptr(), vargmax_ptr=varg.data_ptr())
+            v = var_d.cpu().numpy().reshape(B, M)
+            # fused np.amax / np.argmax (k_vstream and k_predict epilogues)
+            np.testing.assert_array_equal(vmax.cpu().numpy(), v.max(1))
+            np.testing.assert_array_equal(varg.cpu().numpy(), v.argmax(1))
             outs.append((mu_d.cpu().numpy(), var_d.cpu().numpy()))
         (mu, var), (mu_f, var_f) = outs
         assert _err(mu, var, mu_f, var_f, HYP_MF) < 1e-8
