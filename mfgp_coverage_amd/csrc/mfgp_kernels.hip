@@ -1375,8 +1375,10 @@ __device__ __forceinline__ void vs_round(const GLOBAL dv2* __restrict__ vb, cons
     const int64_t j = j0 + 4 * u;
     const bool ok = !GUARD || j < n0;
     const int64_t jj = ok ? j : 0;   // clamped, loads stay unconditional
-    v0[u] = vb[jj * (PBM / 2) + r];
-    v1[u] = vb[jj * (PBM / 2) + 16 + r];
+    // V is read once per update and is far larger than the Infinity Cache:
+    // non-temporal loads (measured 6.3 vs 5.7 TB/s for the whole kernel)
+    v0[u] = __builtin_nontemporal_load(vb + jj * (PBM / 2) + r);
+    v1[u] = __builtin_nontemporal_load(vb + jj * (PBM / 2) + 16 + r);
     zj[u] = gp(z)[jj];
     if (MMA) a[u] = gp(A)[jj * ld + n0 + rr];
     if (GUARD && !ok) {
