@@ -491,7 +491,6 @@ int update_factor(mfgp_model* m) {
   fill_inc_desc(hd[0], m);
   const GPDesc* dd = nullptr;
   if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
-  HIP_TRY(launch_append(dd, 1, c->stream));   // grid-cell search of the new points
   if ((rc = enqueue_inc_factor(c, dd, hd, 1))) return rc;
   if ((rc = release_slot(c, slot))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -892,8 +891,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     GPDesc* hd = acquire_slot(c, slot, rc);
     if (!hd) return rc;
     // factor descriptors, ordered [bordered appends | full refactors | current]:
-    // k_append (copies + grid-cell search) runs over all of them, the factor
-    // kernels over their contiguous sub-ranges
+    // the factor kernels run over their contiguous sub-ranges (k_inc_l21 lands
+    // the device-resident rows of the bordered appends, k_append those of the
+    // full refactors)
     int ninc = 0, nfull = 0;
     order.clear();
     if (do_factor) {
@@ -951,7 +951,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
     if (do_factor) {
-      if (dev_src || ninc > 0) HIP_TRY(launch_append(dd, nb, c->stream));
+      if (dev_src && nfull > 0) HIP_TRY(launch_append(dd + ninc, nfull, c->stream));
       if (ninc > 0 && (rc = enqueue_inc_factor(c, dd, hd, ninc))) return rc;
       if (nfull > 0 && (rc = enqueue_factor(c, dd + ninc, hd + ninc, nfull))) return rc;
     }

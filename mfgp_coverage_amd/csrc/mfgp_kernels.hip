@@ -1053,18 +1053,18 @@ constexpr int ISC0 = 1 + KINC;
 // stay finite), and, with `linv`, their Linv blocks.
 __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, bool linv) {
   const int64_t nbf = nblocks_factor(d.N);
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, nthr = blockDim.x;
   for (int64_t bb = d.ablk; bb < nbf; ++bb) {
     const int64_t c1 = c_hi < (bb + 1) * NB ? c_hi : (bb + 1) * NB;
     if (c1 > c_lo) {
-      for (int64_t e = tid; e < (c1 - c_lo) * NB; e += NT) {
+      for (int64_t e = tid; e < (c1 - c_lo) * NB; e += nthr) {
         const int64_t col = c_lo + (e >> 6);
         const int64_t row = bb * NB + (e & 63);
         d.A[col * d.ld + row] = (col == row) ? 1.0 : 0.0;
       }
     }
     if (linv)
-      for (int e = tid; e < TILE; e += NT) d.Linv[bb * TILE + e] = ((e & 63) == (e >> 6)) ? 1.0 : 0.0;
+      for (int e = tid; e < TILE; e += nthr) d.Linv[bb * TILE + e] = ((e & 63) == (e >> 6)) ? 1.0 : 0.0;
   }
 }
 
@@ -1072,6 +1072,7 @@ __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, boo
 // wave). Lane (r, q) holds L21[r][j], j = 4s + q, eight 4-row steps in flight per
 // wave. With `cell`, L21[r][.] is gathered from the V column of the grid cell and
 // written to row n0 + r of A; otherwise it is read from there.
+template <int NW>
 __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo, int64_t j_hi,
                                   double (*red)[ISZ]) {
   const int64_t n0 = d.n0, ld = d.ld;
@@ -1086,11 +1087,11 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
   const double* src = from_v ? d.V + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : d.A + n0 + (r < k ? r : 0);
   const int64_t sstride = from_v ? PBM : ld;
   const int64_t s_lo = j_lo >> 2, s_hi = (j_hi + 3) >> 2;   // j_lo is a multiple of 4
-  for (int64_t s0 = s_lo + w; s0 < s_hi; s0 += (NT / 64) * IU) {
+  for (int64_t s0 = s_lo + w; s0 < s_hi; s0 += NW * IU) {
     double a[IU], zz[IU];
 #pragma unroll
     for (int u = 0; u < IU; ++u) {
-      const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
+      const int64_t j = 4 * (s0 + NW * u) + q;
       const bool ok = j < j_hi;
       const int64_t jj = ok ? j : j_lo;
       a[u] = gp(src)[jj * sstride];
@@ -1100,7 +1101,7 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
     }
 #pragma unroll
     for (int u = 0; u < IU; ++u) {
-      const int64_t j = 4 * (s0 + (NT / 64) * u) + q;
+      const int64_t j = 4 * (s0 + NW * u) + q;
       if (from_v && r < k && j < j_hi) d.A[j * ld + n0 + r] = a[u];
       sacc = mfma(a[u], a[u], sacc);
       uacc = mfma(a[u], zz[u], uacc);
@@ -1113,24 +1114,90 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
   }
 }
 
-__global__ __launch_bounds__(NT) void k_inc_l21(const GPDesc* __restrict__ descs) {
+// cell[c] = first grid index equal to new point c (INT_MAX if none); all NTHR
+// threads of the workgroup take part, SB grid loads in flight per thread.
+template <int NTHR>
+__device__ void find_cells(const GPDesc& d, const double* px, const double* py, int* cell) {
+  const int tid = threadIdx.x;
+  const GLOBAL dv2* g2 = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid));
+  constexpr int SB = 8;
+  for (int64_t e0 = tid; e0 < d.M; e0 += (int64_t)NTHR * SB) {
+    dv2 gxy[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int64_t e = e0 + (int64_t)u * NTHR;
+      gxy[u] = g2[e < d.M ? e : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int64_t e = e0 + (int64_t)u * NTHR;
+      bool hit = false;
+#pragma unroll
+      for (int c = 0; c < KINC; ++c) hit = hit || (gxy[u].x == px[c] && gxy[u].y == py[c]);
+      if (hit && e < d.M) {
+#pragma unroll
+        for (int c = 0; c < KINC; ++c)
+          if (gxy[u].x == px[c] && gxy[u].y == py[c]) atomicMin(&cell[c], (int)e);
+      }
+    }
+  }
+}
+
+// Grid (row chunks, GPs), 512 threads: find the new points on the grid, gather
+// their V columns into rows n0.. of A and sum this chunk's partials. Chunk 0
+// also lands device-resident new rows in X / y and publishes iscr[0]
+// (1 = the V columns were gathered; 0 = k_inc_finish solves for L21).
+constexpr int LNT = 512;
+__global__ __launch_bounds__(LNT) void k_inc_l21(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
-  const int64_t n0 = d.n0;
-  const int k = (int)(d.N - n0);
+  const int64_t n0 = d.n0, N = d.N;
+  const int k = (int)(N - n0);
   if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
+  const int tid = threadIdx.x;
+  const int64_t kn = d.k_new, at = N - kn;   // rows [at, N) arrive from srcX / srcY
+  if (blockIdx.x == 0 && kn > 0 && d.srcX) {
+    for (int64_t e = tid; e < 3 * kn; e += LNT) {
+      if (e < 2 * kn) const_cast<double*>(d.X)[2 * at + e] = d.srcX[e];
+      else const_cast<double*>(d.y)[at + e - 2 * kn] = d.srcY[e - 2 * kn];
+    }
+  }
+  const bool try_v = n0 > 0 && d.vres >= n0 && d.V != nullptr && d.M > 0;
+  if (!try_v) {
+    if (blockIdx.x == 0 && tid == 0) d.iscr[0] = 0.0;
+    return;
+  }
   const int64_t j_lo = (int64_t)blockIdx.x * ICH;
   if (j_lo >= n0) return;
   const int64_t j_hi = j_lo + ICH < n0 ? j_lo + ICH : n0;
   __shared__ int cell[KINC];
-  __shared__ double red[NT / 64][ISZ];
-  inc_init_blocks(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
-  if (threadIdx.x < KINC) cell[threadIdx.x] = (int)d.iscr[1 + threadIdx.x];
+  __shared__ double red[LNT / 64][ISZ];
+  if (tid < KINC) cell[tid] = INT_MAX;
+  double px[KINC], py[KINC];
+#pragma unroll
+  for (int c = 0; c < KINC; ++c) {
+    const int64_t row = n0 + c;
+    const double* src = (d.srcX && row >= at) ? d.srcX + 2 * (row - at) : d.X + 2 * row;
+    px[c] = c < k ? src[0] : __builtin_nan("");
+    py[c] = c < k ? src[1] : __builtin_nan("");
+  }
   __syncthreads();
-  if (d.iscr[0] == 0.0) return;   // off the grid: k_inc_finish solves
-  inc_schur_partial(d, cell, j_lo, j_hi, red);
+  find_cells<LNT>(d, px, py, cell);
+  __syncthreads();
+  bool use_v = true;
+  for (int c = 0; c < k; ++c) use_v = use_v && cell[c] != INT_MAX;
+  if (blockIdx.x == 0 && tid == 0) d.iscr[0] = use_v ? 1.0 : 0.0;
+  if (!use_v) return;   // off the grid: k_inc_finish solves
+  inc_init_blocks(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
+  __syncthreads();
+  inc_schur_partial<LNT / 64>(d, cell, j_lo, j_hi, red);
   __syncthreads();
   double* __restrict__ part = d.iscr + ISC0 + (int64_t)blockIdx.x * ISZ;
-  for (int e = threadIdx.x; e < ISZ; e += NT) part[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+  for (int e = tid; e < ISZ; e += LNT) {
+    double acc = 0.0;
+#pragma unroll
+    for (int w = 0; w < LNT / 64; ++w) acc += red[w][e];
+    part[e] = acc;
+  }
 }
 
 __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ descs) {
@@ -1229,7 +1296,7 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
       }
       __syncthreads();   // W_I visible to every wave; Ts free
     }
-    inc_schur_partial(d, nullptr, 0, n0, red);
+    inc_schur_partial<NT / 64>(d, nullptr, 0, n0, red);
     __syncthreads();
     for (int e = tid; e < ISZ; e += NT) ssum[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
   }
@@ -1519,70 +1586,20 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
   }
 }
 
-// Append the batch's new (device-resident) rows to every model's training set
-// (one launch for the whole batch instead of two copies per model) and, for GPs
-// on the incremental path with V resident for their leading rows (n0 > 0,
-// vres >= n0), find the new points on the grid: iscr[0] = 1 if all are grid
-// cells, iscr[1 + c] = cell of point c (k_inc_l21 gathers those V columns).
-constexpr int APT = 1024;
-__global__ __launch_bounds__(APT) void k_append(const GPDesc* __restrict__ descs) {
+// Append the batch's new (device-resident) rows to every model's training set:
+// one launch for the whole batch instead of two copies per model (full-refactor
+// path; k_inc_l21 lands the rows of the bordered appends itself).
+__global__ __launch_bounds__(64) void k_append(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.x];
-  const int tid = threadIdx.x;
   const int64_t kn = d.k_new;
-  if (kn > 0 && d.srcX) {
-    double* X = const_cast<double*>(d.X);
-    double* y = const_cast<double*>(d.y);
-    const int64_t at = d.N - kn;
-    for (int64_t e = tid; e < 3 * kn; e += APT) {
-      if (e < 2 * kn) X[2 * at + e] = d.srcX[e];
-      else y[at + e - 2 * kn] = d.srcY[e - 2 * kn];
-    }
+  if (kn <= 0 || !d.srcX) return;
+  double* X = const_cast<double*>(d.X);
+  double* y = const_cast<double*>(d.y);
+  const int64_t at = d.N - kn;
+  for (int64_t e = threadIdx.x; e < 3 * kn; e += 64) {
+    if (e < 2 * kn) X[2 * at + e] = d.srcX[e];
+    else y[at + e - 2 * kn] = d.srcY[e - 2 * kn];
   }
-  const int64_t n0 = d.n0;
-  const int k = (int)(d.N - n0);
-  const bool try_v = n0 > 0 && k > 0 && k <= KINC && d.vres >= n0 && d.V != nullptr && d.M > 0;
-  if (!try_v) {
-    if (tid == 0 && d.iscr) d.iscr[0] = 0.0;
-    return;
-  }
-  __shared__ int cell[KINC];
-  if (tid < KINC) cell[tid] = INT_MAX;
-  __syncthreads();   // the copied rows are visible to the whole workgroup
-  double px[KINC], py[KINC];
-#pragma unroll
-  for (int c = 0; c < KINC; ++c) {
-    px[c] = c < k ? d.X[2 * (n0 + c)] : __builtin_nan("");
-    py[c] = c < k ? d.X[2 * (n0 + c) + 1] : __builtin_nan("");
-  }
-  const GLOBAL dv2* g2 = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid));
-  constexpr int SB = 8;   // grid loads in flight per thread
-  for (int64_t e0 = tid; e0 < d.M; e0 += APT * SB) {
-    dv2 gxy[SB];
-#pragma unroll
-    for (int u = 0; u < SB; ++u) {
-      const int64_t e = e0 + (int64_t)u * APT;
-      gxy[u] = g2[e < d.M ? e : 0];
-    }
-#pragma unroll
-    for (int u = 0; u < SB; ++u) {
-      const int64_t e = e0 + (int64_t)u * APT;
-      bool hit = false;
-#pragma unroll
-      for (int c = 0; c < KINC; ++c) hit = hit || (gxy[u].x == px[c] && gxy[u].y == py[c]);
-      if (hit && e < d.M) {
-#pragma unroll
-        for (int c = 0; c < KINC; ++c)
-          if (gxy[u].x == px[c] && gxy[u].y == py[c]) atomicMin(&cell[c], (int)e);
-      }
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    bool ok = true;
-    for (int c = 0; c < k; ++c) ok = ok && cell[c] != INT_MAX;
-    d.iscr[0] = ok ? 1.0 : 0.0;
-  }
-  if (tid < KINC) d.iscr[1 + tid] = (tid < k && cell[tid] != INT_MAX) ? (double)cell[tid] : 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1590,7 +1607,7 @@ __global__ __launch_bounds__(APT) void k_append(const GPDesc* __restrict__ descs
 hipError_t set_stamps(long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
 #endif
 hipError_t launch_append(const GPDesc* d, int count, hipStream_t s) {
-  hipLaunchKernelGGL(k_append, dim3(count), dim3(APT), 0, s, d);
+  hipLaunchKernelGGL(k_append, dim3(count), dim3(64), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s) {
@@ -1624,7 +1641,7 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
 }
 hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s) {
   const int64_t nch = max_n0 > 0 ? (max_n0 + ICH - 1) / ICH : 1;
-  hipLaunchKernelGGL(k_inc_l21, dim3((unsigned)nch, count), dim3(NT), 0, s, d);
+  hipLaunchKernelGGL(k_inc_l21, dim3((unsigned)nch, count), dim3(LNT), 0, s, d);
   hipLaunchKernelGGL(k_inc_finish, dim3(count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
