@@ -128,6 +128,16 @@ int mfgp_batch_append_predict_ex(mfgp_model** models, int count, const double* X
 int mfgp_batch_append_factor(mfgp_model** models, int count, const double* X, const double* y,
                              const int64_t* k, int flags);
 int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, int flags);
+/* compute_sample_points (simulator.py:326-374), the Choi planner's sample-set
+ * selection, on the device: on a copy of `model` (the model is unchanged),
+ * repeatedly append the grid cell of maximal posterior variance (first argmax)
+ * with its posterior mean as the observation, until the maximal variance is
+ * <= threshold or max_points points were chosen. points: [max_points, 2], host
+ * or device; *count = points chosen. Each iteration is a 1-row bordered append
+ * and a one-pass predict; the loop runs in chunks on the device (one host
+ * synchronisation per 32 iterations). Needs the grid set and incremental
+ * updates enabled. */
+int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, double* points, int64_t* count);
 /* Keep only the first n_keep_hifi hifi rows (no refactor; benchmark reset). */
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi);
 

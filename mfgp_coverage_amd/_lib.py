@@ -34,6 +34,8 @@ SIGNATURES = {
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "mfgp_model_stats": (ctypes.c_int, [ctypes.c_void_p, _c_int64_p, ctypes.c_int]),
+    "mfgp_sample_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p,
+                                          _c_int64_p]),
     "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int64_p, _c_double_p, _c_int64_p]),
     "mfgp_ctx_reset_timing": (ctypes.c_int, [ctypes.c_void_p]),
@@ -242,6 +244,14 @@ class Model:
         check(lib().mfgp_model_stats(self.handle, out, 6))
         keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream")
         return dict(zip(keys, (int(v) for v in out)))
+
+    def sample_points(self, threshold, max_points):
+        """compute_sample_points (simulator.py:326-374) on a device copy of this model:
+        the [n, 2] grid cells chosen until max var <= threshold (at most max_points)."""
+        pts = np.empty((max(int(max_points), 1), 2), dtype=np.float64)
+        n = ctypes.c_int64(0)
+        check(lib().mfgp_sample_points(self.handle, float(threshold), int(max_points), ptr(pts), ctypes.byref(n)))
+        return pts[:n.value].copy()
 
     def truncate(self, n_keep_hifi):
         check(lib().mfgp_truncate(self.handle, int(n_keep_hifi)))

@@ -331,6 +331,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.vmax = nullptr;
   d.vargmax = nullptr;
   d.tred = m->tred;
+  d.gate = nullptr;
   d.status = m->status;
   d.srcX = nullptr;
   d.srcY = nullptr;
@@ -966,6 +967,108 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
   }
   if (flags & MFGP_ASYNC) return MFGP_OK;
   return mfgp_ctx_synchronize(c);
+}
+
+// compute_sample_points (simulator.py:326-374) as a device loop. Each iteration
+// is k_choi_select (argmax cell + its mean -> new hifi row, or stop), a 1-row
+// bordered append and a one-pass predict with the fused argmax, all gated by a
+// device flag, so chunks of iterations are enqueued without a host round trip;
+// the host reads the flag once per chunk and truncates the rows that a stopped
+// loop did not append (the leading rows' factor and V stay valid).
+int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, double* points, int64_t* count) {
+  int rc = check_model(model);
+  if (rc) return rc;
+  if (!count || (max_points > 0 && !points)) return set_err(MFGP_ERR_ARG, "null output");
+  if (max_points < 0) return set_err(MFGP_ERR_ARG, "negative max_points");
+  if (model->M <= 0) return set_err(MFGP_ERR_ARG, "no grid: call mfgp_set_grid first");
+  *count = 0;
+  mfgp_ctx* c = model->ctx;
+  if (!c->incremental) return set_err(MFGP_ERR_ARG, "mfgp_sample_points needs incremental updates enabled");
+  if ((rc = update_factor(model))) return rc;
+  mfgp_model* t = nullptr;   // the reference works on a deep copy (sim:339)
+  if ((rc = mfgp_clone(model, &t))) return rc;
+  const int64_t M = t->M;
+  // workspace: mu, var [M] | vmax | vargmax | state {gate, count} | points [max_points][2]
+  const size_t nd = 2 * (size_t)M + 4 + 2 * (size_t)std::max<int64_t>(max_points, 1);
+  if ((rc = ensure_ws(c, sizeof(double) * nd))) {
+    mfgp_model_destroy(t);
+    return rc;
+  }
+  double* mu_s = c->ws;
+  double* var_s = mu_s + M;
+  double* vmax = var_s + M;
+  int64_t* vargmax = reinterpret_cast<int64_t*>(vmax + 1);
+  int64_t* state = vargmax + 1;
+  double* pts = reinterpret_cast<double*>(state + 2);
+  int* gate = reinterpret_cast<int*>(state);
+  auto fail = [&](int code) {
+    mfgp_model_destroy(t);
+    return code;
+  };
+  // initial posterior of the copy (sim:340-342)
+  if ((rc = batch_run(&t, 1, nullptr, nullptr, nullptr, mu_s, var_s, vmax, vargmax, 0, false, true))) return fail(rc);
+  const int64_t st0[2] = {1, 0};
+  if (hipMemcpyAsync(state, st0, sizeof(st0), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return fail(set_err(MFGP_ERR_DEVICE, "state upload failed"));
+  const int64_t NH0 = t->NH;
+  int64_t done = 0;
+  bool active = true;
+  constexpr int64_t CH = 32;   // iterations per chunk (two descriptors each)
+  while (active && done < max_points) {
+    const int64_t C = std::min<int64_t>(CH, max_points - done);
+    const int64_t N = t->NL + t->NH;
+    if ((rc = ensure_cap(t, N + C)) || (rc = ensure_v(t))) return fail(rc);
+    if (!factor_current(t)) return fail(set_err(MFGP_ERR_DEVICE, "sample_points: factor lost on growth"));
+    int slot;
+    GPDesc* hd = acquire_slot(c, slot, rc);
+    if (!hd) return fail(rc);
+    for (int64_t it = 0; it < C; ++it) {
+      t->NH += 1;   // assume the iteration runs; truncated below if the loop stopped
+      GPDesc& fd = hd[2 * it];
+      fill_inc_desc(fd, t);
+      fd.mu = mu_s;
+      fd.vmax = vmax;
+      fd.vargmax = vargmax;
+      fd.gate = gate;
+      mark_inc_factor(t);
+      GPDesc& pd = hd[2 * it + 1];
+      fill_desc(pd, t);
+      pd.n0 = t->v_n;
+      pd.mu = mu_s;
+      pd.var = var_s;
+      pd.vmax = vmax;
+      pd.vargmax = vargmax;
+      pd.gate = gate;
+      t->v_n = t->NL + t->NH;
+    }
+    const GPDesc* dd = nullptr;
+    if ((rc = upload_slot(c, slot, (int)(2 * C), &dd))) return fail(rc);
+    for (int64_t it = 0; it < C; ++it) {
+      if (hipSuccess != launch_choi_select(dd + 2 * it, threshold, pts, max_points, c->stream) ||
+          hipSuccess != launch_inc_factor(dd + 2 * it, 1, hd[2 * it].n0, c->stream) ||
+          hipSuccess != launch_vstream(dd + 2 * it + 1, 1, ntiles_grid(M), c->stream) ||
+          hipSuccess != launch_var_argmax(dd + 2 * it + 1, 1, c->stream))
+        return fail(set_err(MFGP_ERR_DEVICE, "sample_points: launch failed"));
+    }
+    if ((rc = release_slot(c, slot))) return fail(rc);
+    int64_t st[2] = {0, 0};
+    if (hipMemcpyAsync(st, state, sizeof(st), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      return fail(set_err(MFGP_ERR_DEVICE, "sample_points: state read failed"));
+    active = (int)st[0] != 0;
+    const int64_t ran = st[1] - done;
+    done = st[1];
+    if (ran < C) {
+      // the loop stopped inside this chunk: drop the rows it did not append
+      if ((rc = mfgp_truncate(t, NH0 + done))) return fail(rc);
+    }
+    if ((rc = read_status(t))) return fail(rc);
+  }
+  if (done > 0 && hipMemcpy(points, pts, sizeof(double) * 2 * done, hipMemcpyDefault) != hipSuccess)
+    return fail(set_err(MFGP_ERR_DEVICE, "sample_points: copy out failed"));
+  *count = done;
+  mfgp_model_destroy(t);
+  return MFGP_OK;
 }
 
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,

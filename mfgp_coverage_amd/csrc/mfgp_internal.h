@@ -48,6 +48,7 @@ struct GPDesc {
   double* vmax;        // fused np.amax(var) (or null)
   int64_t* vargmax;    // fused first argmax of var (or null)
   double* tred;        // [ceil(M/PBM)][2] per-tile (max, argmax) partials of var (k_var_argmax)
+  int* gate;           // device loop gate (null = always run); 0 makes the gated kernels no-ops
   int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
   const double* srcX;  // device rows to append at row N - k_new (k_append), or null
   const double* srcY;
@@ -81,5 +82,7 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
 hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
 hipError_t launch_var_argmax(const GPDesc* d, int count, hipStream_t s);
+hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,
+                              hipStream_t s);
 
 }  // namespace mfgp

@@ -771,6 +771,7 @@ __device__ void var_argmax_tile(const GPDesc& d, double v, int64_t c, bool valid
 __global__ __launch_bounds__(NT) void k_var_argmax(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.x];
   if (d.M <= 0 || (!d.vmax && !d.vargmax)) return;
+  if (d.gate && *d.gate == 0) return;
   const int64_t ntiles = ntiles_grid(d.M);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   __shared__ double sv[NT / 64];
@@ -1153,6 +1154,7 @@ __global__ __launch_bounds__(LNT) void k_inc_l21(const GPDesc* __restrict__ desc
   const int64_t n0 = d.n0, N = d.N;
   const int k = (int)(N - n0);
   if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
+  if (d.gate && *d.gate == 0) return;
   const int tid = threadIdx.x;
   const int64_t kn = d.k_new, at = N - kn;   // rows [at, N) arrive from srcX / srcY
   if (blockIdx.x == 0 && kn > 0 && d.srcX) {
@@ -1205,6 +1207,7 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
   const int64_t n0 = d.n0, N = d.N, ld = d.ld, NL = d.NL;
   const int k = (int)(N - n0);
   if (k <= 0 || k > KINC) return;
+  if (d.gate && *d.gate == 0) return;
   const Hyp& h = d.hf;
   double* __restrict__ A = d.A;
   const double* __restrict__ X = d.X;
@@ -1492,6 +1495,7 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
   const int64_t M = d.M;
   const int64_t c0 = (int64_t)blockIdx.x * PBM;
   if (c0 >= M) return;
+  if (d.gate && *d.gate == 0) return;
   const int64_t n0 = d.n0, N = d.N, ld = d.ld;
   const int k = (int)(N - n0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1586,6 +1590,33 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
   }
 }
 
+// One iteration of compute_sample_points (simulator.py:344-370) on the device:
+// the cell of maximal posterior variance (its first occurrence, np.argmax) is
+// appended as hifi row N - 1 with its posterior mean as the observation
+// (sim:352-366), unless the maximal variance is at or below the threshold or
+// max_points rows were chosen -- then the loop is over: *gate = 0 and every
+// gated kernel after it is a no-op. state[1] counts the chosen points.
+__global__ void k_choi_select(const GPDesc* __restrict__ descs, double threshold, double* __restrict__ points,
+                              int64_t max_points) {
+  const GPDesc& d = descs[0];
+  if (threadIdx.x != 0 || *d.gate == 0) return;
+  int64_t* cnt = reinterpret_cast<int64_t*>(d.gate) + 1;
+  const double vmax = *d.vmax;
+  const int64_t j = *d.vargmax;
+  if (!(vmax > threshold) || *cnt >= max_points || j < 0 || j >= d.M) {
+    *d.gate = 0;
+    return;
+  }
+  const int64_t row = d.N - 1;
+  const double gx = d.grid[2 * j], gy = d.grid[2 * j + 1];
+  const_cast<double*>(d.X)[2 * row] = gx;
+  const_cast<double*>(d.X)[2 * row + 1] = gy;
+  const_cast<double*>(d.y)[row] = d.mu[j];
+  points[2 * *cnt] = gx;
+  points[2 * *cnt + 1] = gy;
+  *cnt += 1;
+}
+
 // Append the batch's new (device-resident) rows to every model's training set:
 // one launch for the whole batch instead of two copies per model (full-refactor
 // path; k_inc_l21 lands the rows of the bordered appends itself).
@@ -1643,6 +1674,11 @@ hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStre
   const int64_t nch = max_n0 > 0 ? (max_n0 + ICH - 1) / ICH : 1;
   hipLaunchKernelGGL(k_inc_l21, dim3((unsigned)nch, count), dim3(LNT), 0, s, d);
   hipLaunchKernelGGL(k_inc_finish, dim3(count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_choi_select, dim3(1), dim3(64), 0, s, d, threshold, points, max_points);
   return hipGetLastError();
 }
 hipError_t launch_var_argmax(const GPDesc* d, int count, hipStream_t s) {

@@ -154,7 +154,70 @@ def make_replay_fixtures():
         print("wrote replay", run)
 
 
+def _import_simulator():
+    """simulator.py needs `mlrose` at import (sim:29, used only by the TSP step);
+    a stub module stands in for it. compute_sample_points itself runs unchanged."""
+    sys.modules.setdefault("mlrose", types.ModuleType("mlrose"))
+    import simulator as sim  # noqa: E402  (the reference module)
+    return sim
+
+
+def make_choi_fixture(gp, sim):
+    """3. ``choi_reference.npz``: the reference's own ``compute_sample_points``
+    (simulator.py:326-374, the Choi planner's sample-set selection) on
+    anti_two_corners models and the 32x32 grid. Stored per case: the chosen
+    points in order, and for every step the gap between the largest and the
+    second largest posterior variance the loop's argmax saw (an argmax whose gap is
+    below the parity tolerance is decided by rounding, so the tests compare the
+    sequence only up to the first such step)."""
+    import copy
+    hyp_sf = _csv("anti_two_corners_sf_hyp.csv")[0]
+    hyp_mf = _csv("anti_two_corners_mf_hyp.csv")[0]
+    train = _csv("anti_two_corners_hifi_train.csv")
+    prior = _csv("anti_two_corners_prior.csv")
+    xs = grid32()
+    e2, e1 = np.empty((0, 2)), np.empty((0, 1))
+    out = {"grid": xs, "hyp_sf": hyp_sf, "hyp_mf": hyp_mf, "train": train, "prior": prior}
+    cases = {
+        # name: (builder, threshold as a fraction of the model's current max variance)
+        "sf_n50": (lambda: gp.SFGP(train[:50, :2].copy(), train[:50, 2:3].copy(), 1), hyp_sf, 0.08),
+        "mf_n20": (lambda: gp.MFGP(prior[:, :2].copy(), prior[:, 2:3].copy(), train[:20, :2].copy(),
+                                   train[:20, 2:3].copy(), 1, 1), hyp_mf, 0.08),
+        "mf_prior": (lambda: gp.MFGP(prior[:, :2].copy(), prior[:, 2:3].copy(), e2.copy(), e1.copy(), 1, 1),
+                     hyp_mf, 0.15),
+    }
+    for name, (build, hyp, frac) in cases.items():
+        m = build()
+        m.hyp = hyp.copy()
+        if isinstance(m, gp.SFGP):
+            m.updt_info(m.X, m.y)
+        else:
+            m.updt_info(m.X_L, m.y_L, m.X_H, m.y_H)
+        _, cov = m.predict(xs)
+        thr = frac * float(np.amax(cov))
+        pts = sim.compute_sample_points(m, xs, thr, False)
+        # the same loop again, recording the argmax margins (and checking the points)
+        t = copy.deepcopy(m)
+        mu, cov = t.predict(xs)
+        var = np.diag(cov)
+        gaps = []
+        for p in pts:
+            j = int(np.argmax(var))
+            assert np.array_equal(xs[j], p)
+            srt = np.sort(var)
+            gaps.append(srt[-1] - srt[-2])
+            (t.updt if isinstance(t, gp.SFGP) else t.updt_hifi)(xs[j:j + 1], mu[j:j + 1])
+            mu, cov = t.predict(xs)
+            var = np.diag(cov)
+        out[name + "_threshold"] = np.array(thr)
+        out[name + "_points"] = np.asarray(pts, dtype=np.float64).reshape(-1, 2)
+        out[name + "_gaps"] = np.array(gaps, dtype=np.float64)
+        print(name, "points", len(pts), "min gap", min(gaps) if gaps else None)
+    np.savez_compressed(os.path.join(OUT, "choi_reference.npz"), **out)
+
+
 if __name__ == "__main__":
     gp = _import_reference()
     make_reference_fixture(gp)
     make_replay_fixtures()
+    make_choi_fixture(gp, _import_simulator())

@@ -114,3 +114,39 @@ def test_oracle_replays_logged_runs(run):
             append=lambda m, X, y: m.append(X, y),
             predict_var=lambda m: m.var())
         np.testing.assert_allclose(got, logged, rtol=1e-9)
+
+
+@pytest.mark.parametrize("case", ["sf_n50", "mf_n20", "mf_prior"])
+def test_oracle_sample_points_vs_reference(case):
+    """The oracle's compute_sample_points loop (simulator.py:326-374: argmax of the
+    variance -> append with the posterior mean -> predict) reproduces the
+    reference's own output (choi_reference.npz) up to the first near-tie argmax."""
+    fx = F.load("choi_reference.npz")
+    train, prior, xs = fx["train"], fx["prior"], fx["grid"]
+    mf = case.startswith("mf")
+    hyp = fx["hyp_mf"] if mf else fx["hyp_sf"]
+    n = {"sf_n50": 50, "mf_n20": 20, "mf_prior": 0}[case]
+    XL, yL = prior[:, :2], prior[:, 2]
+    XH, yH = train[:n, :2].copy(), train[:n, 2].copy()
+
+    def predict():
+        if mf:
+            return O.mf_diag(XL, yL, XH, yH, hyp, xs)
+        return O.sf_diag(XH, yH, hyp, xs)
+
+    thr = float(fx[case + "_threshold"])
+    mu, var = predict()
+    pts = []
+    while var.max() > thr:
+        j = int(np.argmax(var))
+        pts.append(xs[j])
+        XH = np.vstack([XH, xs[j:j + 1]])
+        yH = np.concatenate([yH, mu[j:j + 1]])
+        mu, var = predict()
+    ref, gaps = fx[case + "_points"], fx[case + "_gaps"]
+    near = np.flatnonzero(gaps < O.PARITY_TOL * O.prior_variance(hyp))
+    upto = int(near[0]) if near.size else ref.shape[0]
+    pts = np.asarray(pts).reshape(-1, 2)
+    np.testing.assert_array_equal(pts[:upto], ref[:upto])
+    if upto == ref.shape[0]:
+        assert pts.shape[0] == ref.shape[0]
