@@ -141,6 +141,21 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
 /* Keep only the first n_keep_hifi hifi rows (no refactor; benchmark reset). */
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi);
 
+/* Voronoi-cell reductions over the grid (simulator.py:194-323). Cell i is the
+ * closed polygon verts[vstart[i] .. vstart[i+1]) ([.,2], vertices of the
+ * caller's bounded Voronoi region, sim:154-191; at most 256 per cell) with seed
+ * seeds[i]. A grid point belongs to every cell whose polygon contains it by the
+ * reference's in_polygon test (sim:105-124: matplotlib's crossing rule,
+ * reproduced exactly). Per cell, out[6i .. 6i+6) = {points, sum w, sum w*x,
+ * sum w*y, sum |x - seed|^2 * f, max var} and argmax[i] = first grid index of
+ * the max var (-1 if the cell is empty). w (compute_centroids' mu, sim:231-283),
+ * f (compute_loss' truth, sim:194-228) and var (compute_max_var, sim:286-323)
+ * may each be NULL. Arrays may be host or device memory except vstart (host).
+ * Synchronous. */
+int mfgp_cell_reduce(mfgp_ctx* ctx, const double* grid, int64_t M, int ncells, const int* vstart,
+                     const double* verts, const double* seeds, const double* w, const double* f,
+                     const double* var, double* out, int64_t* argmax);
+
 const char* mfgp_last_error(void);
 const char* mfgp_version(void);
 

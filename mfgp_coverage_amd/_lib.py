@@ -34,6 +34,9 @@ SIGNATURES = {
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "mfgp_model_stats": (ctypes.c_int, [ctypes.c_void_p, _c_int64_p, ctypes.c_int]),
+    "mfgp_cell_reduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mfgp_sample_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p,
                                           _c_int64_p]),
     "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -295,3 +298,20 @@ def batch_predict(models, mu_ptr, var_ptr, asynchronous=False):
     arr = (ctypes.c_void_p * n)(*[m.handle.value for m in models])
     check(lib().mfgp_batch_predict(arr, n, ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
                                    ASYNC if asynchronous else 0))
+
+
+def cell_reduce(grid, verts, vstart, seeds, w=None, f=None, var=None, ctx=None):
+    """mfgp_cell_reduce on host arrays -> (out [n, 6], argmax [n]); see include/mfgp_hip.h."""
+    ctx = ctx or context()
+    g = np.ascontiguousarray(grid, dtype=np.float64).reshape(-1, 2)
+    v = np.ascontiguousarray(verts, dtype=np.float64).reshape(-1, 2)
+    vs = np.ascontiguousarray(vstart, dtype=np.int32).reshape(-1)
+    sd = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 2)
+    n = vs.shape[0] - 1
+    arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float64).reshape(-1) for a in (w, f, var)]
+    out = np.empty((max(n, 1), 6), dtype=np.float64)
+    am = np.empty(max(n, 1), dtype=np.int64)
+    check(lib().mfgp_cell_reduce(ctx.handle, ptr(g), g.shape[0], n, ctypes.c_void_p(vs.ctypes.data), ptr(v), ptr(sd),
+                                 *[ptr(a) for a in arrs], ctypes.c_void_p(out.ctypes.data),
+                                 ctypes.c_void_p(am.ctypes.data)))
+    return out[:n], am[:n]

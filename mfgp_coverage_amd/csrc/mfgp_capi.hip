@@ -1071,6 +1071,66 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
   return MFGP_OK;
 }
 
+// Voronoi-cell reductions (simulator.py:194-323) on the device. Inputs may be
+// host or device memory (host ones are staged through the context workspace);
+// outputs likewise. Synchronous.
+int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, const int* vstart, const double* verts,
+                     const double* seeds, const double* w, const double* f, const double* var, double* out,
+                     int64_t* argmax) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (M < 0 || ncells < 0 || (M > 0 && !grid) || (ncells > 0 && (!vstart || !verts || !seeds || !out || !argmax)))
+    return set_err(MFGP_ERR_ARG, "bad cell_reduce arguments");
+  if (M == 0 || ncells == 0) {
+    for (int i = 0; i < ncells; ++i) {
+      for (int j = 0; j < 6; ++j) out[6 * i + j] = (j == 5) ? -HUGE_VAL : 0.0;
+      argmax[i] = -1;
+    }
+    return MFGP_OK;
+  }
+  // vertex counts (the offsets must be readable on the host)
+  if (is_device_ptr(vstart)) return set_err(MFGP_ERR_ARG, "vstart must be host memory");
+  if (vstart[0] != 0) return set_err(MFGP_ERR_ARG, "vstart[0] must be 0");
+  for (int i = 0; i < ncells; ++i)
+    if (vstart[i + 1] - vstart[i] > 256 || vstart[i + 1] < vstart[i])
+      return set_err(MFGP_ERR_ARG, "cell %d: bad vertex count", i);
+  const int64_t nv = vstart[ncells];
+  const int64_t npart = cell_partial_doubles(M, ncells);
+  // workspace layout (doubles): grid 2M | w M | f M | var M | verts 2nv | seeds 2n | part | out 6n | argmax n | vstart
+  const int64_t off_g = 0, off_w = off_g + 2 * M, off_f = off_w + M, off_v = off_f + M, off_vx = off_v + M;
+  const int64_t off_s = off_vx + 2 * nv, off_p = off_s + 2 * ncells, off_o = off_p + npart;
+  const int64_t off_a = off_o + 6 * ncells, off_i = off_a + ncells, total = off_i + (ncells + 2) / 2 + 1;
+  int rc = ensure_ws(c, sizeof(double) * total);
+  if (rc) return rc;
+  double* ws = c->ws;
+  hipStream_t s = c->stream;
+  auto stage = [&](const double* p, int64_t n, int64_t off) -> const double* {
+    if (!p) return nullptr;
+    if (is_device_ptr(p)) return p;
+    if (hipMemcpyAsync(ws + off, p, sizeof(double) * n, hipMemcpyHostToDevice, s) != hipSuccess) return nullptr;
+    return ws + off;
+  };
+  const double* dg = stage(grid, 2 * M, off_g);
+  const double* dw = stage(w, M, off_w);
+  const double* df = stage(f, M, off_f);
+  const double* dv = stage(var, M, off_v);
+  const double* dx = stage(verts, 2 * nv, off_vx);
+  const double* ds = stage(seeds, 2 * ncells, off_s);
+  if (!dg || !dx || !ds || (w && !dw) || (f && !df) || (var && !dv))
+    return set_err(MFGP_ERR_DEVICE, "cell_reduce: staging failed");
+  int* dvs = reinterpret_cast<int*>(ws + off_i);
+  HIP_TRY(hipMemcpyAsync(dvs, vstart, sizeof(int) * (ncells + 1), hipMemcpyHostToDevice, s));
+  const bool dev_out = is_device_ptr(out) && is_device_ptr(argmax);
+  double* o = dev_out ? out : ws + off_o;
+  int64_t* a = dev_out ? argmax : reinterpret_cast<int64_t*>(ws + off_a);
+  HIP_TRY(launch_cell_reduce(dg, M, dx, dvs, ncells, ds, dw, df, dv, ws + off_p, o, a, s));
+  if (!dev_out) {
+    HIP_TRY(hipMemcpyAsync(out, o, sizeof(double) * 6 * ncells, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(argmax, a, sizeof(int64_t) * ncells, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return MFGP_OK;
+}
+
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                               double* mu, double* var, int flags) {
   return batch_run(models, count, X, y, k, mu, var, nullptr, nullptr, flags, true, true);

@@ -82,6 +82,10 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
 hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
 hipError_t launch_var_argmax(const GPDesc* d, int count, hipStream_t s);
+hipError_t launch_cell_reduce(const double* grid, int64_t M, const double* verts, const int* vstart, int ncells,
+                              const double* seeds, const double* w, const double* f, const double* var,
+                              double* part, double* out, int64_t* argmax, hipStream_t s);
+int64_t cell_partial_doubles(int64_t M, int ncells);
 hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,
                               hipStream_t s);
 

@@ -210,3 +210,55 @@ def parity_errors(mu, var, mu_ref, var_ref, kss):
 
 
 PARITY_TOL = 1e-6
+
+
+# ---------------------------------------------------------------------------
+# Voronoi-cell reductions (simulator.py:105-136, 194-323) -- checker for
+# mfgp_cells.hip / geometry.py. Membership is in_polygon (sim:105-124), i.e.
+# matplotlib's Path.contains_points crossing rule, restated here on arrays.
+# ---------------------------------------------------------------------------
+
+def in_polygon(pts, verts):
+    """Crossing-number test of matplotlib's point_in_path for a closed polygon:
+    an edge whose end points straddle the point's y (yflag = vy >= ty) toggles
+    when ((vy1 - ty) * (vx0 - vx1) >= (vx1 - tx) * (vy0 - vy1)) == yflag1."""
+    tx, ty = pts[:, 0], pts[:, 1]
+    inside = np.zeros(pts.shape[0], dtype=bool)
+    n = verts.shape[0]
+    x0, y0 = verts[0]
+    f0 = y0 >= ty
+    for e in range(1, n + 1):
+        x1, y1 = verts[e % n]
+        f1 = y1 >= ty
+        hit = ((y1 - ty) * (x0 - x1) >= (x1 - tx) * (y0 - y1)) == f1
+        inside ^= (f0 != f1) & hit
+        f0, x0, y0 = f1, x1, y1
+    return inside
+
+
+def poly_area(v):
+    """Shoelace area (sim:127-136)."""
+    x, y = v[:, 0], v[:, 1]
+    return 0.5 * np.abs(np.dot(x, np.roll(y, 1)) - np.dot(y, np.roll(x, 1)))
+
+
+def cell_reductions(polys, seeds, xs, w=None, f=None, var=None):
+    """Per cell: (members, centroid, loss term, max var, argmax index) with the
+    reference's formulas (sim:210-221, 255-270, 305-311)."""
+    res = []
+    for v, s in zip(polys, seeds):
+        m = in_polygon(xs, v)
+        area = poly_area(v)
+        pts = xs[m]
+        cen = loss = vmax = amax = None
+        if w is not None:
+            ww = w[m]
+            cen = (np.mean(ww[:, None] * pts, axis=0) * area) / (np.mean(ww) * area)
+        if f is not None:
+            loss = np.mean(np.sum((pts - s) ** 2, axis=1) * f[m]) * area
+        if var is not None and m.any():
+            idx = np.flatnonzero(m)
+            vmax = var[idx].max()
+            amax = int(idx[np.argmax(var[idx])])
+        res.append((m, cen, loss, vmax, amax))
+    return res

@@ -216,8 +216,71 @@ def make_choi_fixture(gp, sim):
     np.savez_compressed(os.path.join(OUT, "choi_reference.npz"), **out)
 
 
+def _voronoi_bounded(sim, seeds, bb):
+    """The reference's voronoi_bounded (sim:154-191). Its np.array(vor.regions)
+    (sim:190) fails on NumPy >= 1.24 for ragged regions; the same call with an
+    object array is what older NumPy did."""
+    real = sim.np.array
+
+    def arr(x, *a, **k):
+        try:
+            return real(x, *a, **k)
+        except ValueError:
+            return real(x, dtype=object)
+    sim.np.array = arr
+    try:
+        return sim.voronoi_bounded(seeds, bb)
+    finally:
+        sim.np.array = real
+
+
+def make_cells_fixture(sim):
+    """4. ``cells_reference.npz``: the reference's own compute_loss,
+    compute_centroids and compute_max_var (sim:194-323) over voronoi_bounded
+    partitions (sim:154-191) of random agent sets on the native 51x51
+    anti_two_corners grid (half of them on grid points, so that grid points lie
+    on cell boundaries), with the reference GP's posterior mean / variance
+    (mf_g51_n50 of atc_reference.npz) as the weights. Stored per case: the
+    seeds, the cell polygons (flattened + offsets), the per-cell point counts of
+    in_polygon, and the three functions' outputs."""
+    truth = _csv("anti_two_corners_hifi.csv")
+    xs = truth[:, :2].copy()
+    ref = np.load(os.path.join(OUT, "atc_reference.npz"))
+    mu, var = ref["mf_g51_n50_mu"], ref["mf_g51_n50_var"]
+    bb = np.array([xs[:, 0].min(), xs[:, 0].max(), xs[:, 1].min(), xs[:, 1].max()])
+    rng = np.random.default_rng(2020)
+    out = {"truth": truth, "mu": mu, "var": var}
+    ncase = 0
+    dense_var = np.diag(var)
+    while ncase < 12:
+        n = int(rng.integers(2, 9))
+        seeds = rng.random((n, 2))
+        if ncase % 2 == 0:
+            seeds = np.round(seeds * 50) / 50
+        vor = _voronoi_bounded(sim, seeds, bb)
+        polys = [vor.vertices[list(c), :] for c in vor.filtered_regions]
+        counts = np.array([sim.in_polygon(xs[:, 0], xs[:, 1], v[:, 0], v[:, 1]).sum() for v in polys])
+        if np.any(counts == 0):
+            continue
+        key = f"c{ncase}"
+        out[key + "_seeds"] = np.asarray(vor.filtered_points, dtype=np.float64)
+        out[key + "_verts"] = np.vstack(polys).astype(np.float64)
+        out[key + "_vstart"] = np.concatenate([[0], np.cumsum([v.shape[0] for v in polys])]).astype(np.int32)
+        out[key + "_counts"] = counts.astype(np.int64)
+        out[key + "_loss"] = np.array(sim.compute_loss(vor, truth))
+        out[key + "_centroids"] = sim.compute_centroids(vor, xs, mu.reshape(-1, 1))
+        am, mv = sim.compute_max_var(vor, truth, dense_var)
+        out[key + "_argmax"], out[key + "_maxvar"] = am, mv
+        ncase += 1
+    out["ncases"] = np.array(ncase)
+    np.savez_compressed(os.path.join(OUT, "cells_reference.npz"), **out)
+    print("wrote cells_reference.npz,", ncase, "partitions")
+
+
 if __name__ == "__main__":
     gp = _import_reference()
     make_reference_fixture(gp)
     make_replay_fixtures()
-    make_choi_fixture(gp, _import_simulator())
+    sim = _import_simulator()
+    make_choi_fixture(gp, sim)
+    make_cells_fixture(sim)

@@ -150,3 +150,27 @@ def test_oracle_sample_points_vs_reference(case):
     np.testing.assert_array_equal(pts[:upto], ref[:upto])
     if upto == ref.shape[0]:
         assert pts.shape[0] == ref.shape[0]
+
+
+def _cells_case(fx, i):
+    verts, vs = fx[f"c{i}_verts"], fx[f"c{i}_vstart"]
+    polys = [verts[vs[j]:vs[j + 1]] for j in range(vs.shape[0] - 1)]
+    return polys, fx[f"c{i}_seeds"]
+
+
+def test_oracle_cell_reductions_vs_reference():
+    """in_polygon / compute_loss / compute_centroids / compute_max_var (sim:105-323)
+    restated on arrays reproduce the reference's outputs on 12 partitions."""
+    fx = F.load("cells_reference.npz")
+    truth, mu, var = fx["truth"], fx["mu"], fx["var"]
+    xs = truth[:, :2]
+    for i in range(int(fx["ncases"])):
+        polys, seeds = _cells_case(fx, i)
+        res = O.cell_reductions(polys, seeds, xs, w=mu, f=truth[:, 2], var=var)
+        np.testing.assert_array_equal([r[0].sum() for r in res], fx[f"c{i}_counts"])
+        lo, hi = xs.min(0), xs.max(0)
+        cen = np.clip(np.array([r[1] for r in res]), lo, hi)
+        np.testing.assert_allclose(cen, fx[f"c{i}_centroids"], rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(sum(r[2] for r in res), fx[f"c{i}_loss"], rtol=1e-13)
+        np.testing.assert_array_equal(np.array([r[3] for r in res]), fx[f"c{i}_maxvar"][:, 0])
+        np.testing.assert_array_equal(xs[[r[4] for r in res]], fx[f"c{i}_argmax"])
