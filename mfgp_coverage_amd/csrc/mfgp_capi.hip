@@ -399,7 +399,12 @@ int enqueue_vstream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
 
 int enqueue_predict(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_ct = 0;
-  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_grid(hd[i].M));
+  for (int i = 0; i < count; ++i) {
+    max_ct = std::max(max_ct, ntiles_grid(hd[i].M));
+    // k_predict addresses A through a 32-bit buffer descriptor: 8 * ld^2 < 2^31
+    if (hd[i].ld > 16383)
+      return set_err(MFGP_ERR_ARG, "fused predict supports N <= 16382 training rows (got %lld)", (long long)hd[i].N);
+  }
   if (max_ct == 0) return MFGP_OK;
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
