@@ -141,6 +141,14 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
 /* Keep only the first n_keep_hifi hifi rows (no refactor; benchmark reset). */
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi);
 
+/* likelihood (gp:81-106 SF / gp:344-385 MF): the negative log-marginal
+ * likelihood of the model's training data under the log-scaled hyperparameters
+ * `hyp` (nhyp = 4 or 9; the model's own .hyp and factor are unchanged), and,
+ * if grad != NULL, its gradient with respect to hyp ([nhyp]; the reference uses
+ * autograd for it in train, gp:108-119 / 388-399). MFGP_ERR_NOT_PD as the
+ * reference's cholesky raising LinAlgError. */
+int mfgp_nlml(mfgp_model* m, const double* hyp, int nhyp, double* nlml, double* grad);
+
 /* Voronoi-cell reductions over the grid (simulator.py:194-323). Cell i is the
  * closed polygon verts[vstart[i] .. vstart[i+1]) ([.,2], vertices of the
  * caller's bounded Voronoi region, sim:154-191; at most 256 per cell) with seed

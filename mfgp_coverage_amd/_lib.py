@@ -34,6 +34,7 @@ SIGNATURES = {
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "mfgp_model_stats": (ctypes.c_int, [ctypes.c_void_p, _c_int64_p, ctypes.c_int]),
+    "mfgp_nlml": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, _c_double_p, ctypes.c_void_p]),
     "mfgp_cell_reduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -255,6 +256,15 @@ class Model:
         n = ctypes.c_int64(0)
         check(lib().mfgp_sample_points(self.handle, float(threshold), int(max_points), ptr(pts), ctypes.byref(n)))
         return pts[:n.value].copy()
+
+    def nlml(self, hyp, grad=False):
+        """likelihood (gp:81-106 / 344-385) of this model's data under `hyp`; with grad, (value, gradient)."""
+        h = np.ascontiguousarray(hyp, dtype=np.float64).reshape(-1)
+        v = ctypes.c_double(0.0)
+        g = np.empty(h.shape[0], dtype=np.float64) if grad else None
+        check(lib().mfgp_nlml(self.handle, ptr(h), int(h.shape[0]), ctypes.byref(v),
+                              ctypes.c_void_p(g.ctypes.data) if grad else None))
+        return (v.value, g) if grad else v.value
 
     def truncate(self, n_keep_hifi):
         check(lib().mfgp_truncate(self.handle, int(n_keep_hifi)))

@@ -1136,6 +1136,94 @@ int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, con
   return MFGP_OK;
 }
 
+// likelihood (gp:81-106 / gp:344-385) and its analytic gradient on the device,
+// for the model's data under the given hyperparameters (the model is unchanged).
+int mfgp_nlml(mfgp_model* m, const double* hyp, int nhyp, double* nlml, double* grad) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (!hyp || nhyp != m->nhyp)
+    return set_err(MFGP_ERR_ARG, "Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)");
+  if (!nlml) return set_err(MFGP_ERR_ARG, "null output");
+  mfgp_ctx* c = m->ctx;
+  const int64_t N = m->NL + m->NH;
+  if (N == 0) {   // empty data: every term is an empty sum
+    *nlml = 0.0;
+    if (grad)
+      for (int p = 0; p < nhyp; ++p) grad[p] = 0.0;
+    return MFGP_OK;
+  }
+  mfgp_model* t = nullptr;   // scratch factor of K(hyp)
+  if ((rc = mfgp_model_create(c, m->kind, MFGP_F64, hyp, nhyp, m->jitter, &t))) return rc;
+  double *Xi = nullptr, *Kv = nullptr, *al = nullptr, *part = nullptr, *val = nullptr;
+  auto done = [&](int code) {
+    if (Xi) (void)hipFree(Xi);
+    if (Kv) (void)hipFree(Kv);
+    if (al) (void)hipFree(al);
+    if (part) (void)hipFree(part);
+    if (val) (void)hipFree(val);
+    mfgp_model_destroy(t);
+    return code;
+  };
+  if ((rc = ensure_cap(t, N))) return done(rc);
+  HIP_TRY(hipMemcpyAsync(t->X, m->X, sizeof(double) * 2 * N, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(t->y, m->y, sizeof(double) * N, hipMemcpyDeviceToDevice, c->stream));
+  t->NL = m->NL;
+  t->NH = m->NH;
+  if ((rc = factor_one(t))) return done(rc);   // LinAlgError as the reference's cholesky (gp:101 / 380)
+  int slot;
+  GPDesc* hd = acquire_slot(c, slot, rc);
+  if (!hd) return done(rc);
+  fill_desc(hd[0], t);
+  const GPDesc* dd = nullptr;
+  if ((rc = upload_slot(c, slot, 1, &dd))) return done(rc);
+  if (hipMalloc(&val, sizeof(double) * 2) != hipSuccess) return done(set_err(MFGP_ERR_DEVICE, "alloc"));
+  if (launch_nlml_value(dd, 1, val, c->stream) != hipSuccess) return done(set_err(MFGP_ERR_DEVICE, "launch"));
+  const int64_t ld = t->ld, np = nlml_partials(N);
+  if (grad) {
+    if (hipMalloc(&Xi, sizeof(double) * ld * ld) != hipSuccess || hipMalloc(&Kv, sizeof(double) * ld * ld) != hipSuccess ||
+        hipMalloc(&al, sizeof(double) * ld) != hipSuccess || hipMalloc(&part, sizeof(double) * np) != hipSuccess)
+      return done(set_err(MFGP_ERR_DEVICE, "nlml: out of device memory"));
+    if (launch_nlml_grad(dd, N, Xi, Kv, al, part, c->stream) != hipSuccess)
+      return done(set_err(MFGP_ERR_DEVICE, "nlml: launch failed"));
+  }
+  if ((rc = release_slot(c, slot))) return done(rc);
+  double v[2] = {0.0, 0.0};
+  std::vector<double> hp, ha;
+  HIP_TRY(hipMemcpyAsync(v, val, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+  if (grad) {
+    hp.resize(np);
+    ha.resize(N);
+    HIP_TRY(hipMemcpyAsync(hp.data(), part, sizeof(double) * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ha.data(), al, sizeof(double) * N, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  // NLML = 1/2 r^T K^-1 r + sum log L_ii + N/2 log(2 pi)   (gp:104-105 / gp:383-384)
+  *nlml = 0.5 * v[1] + v[0] + 0.5 * std::log(2.0 * M_PI) * (double)N;
+  if (grad) {
+    for (int p = 0; p < nhyp; ++p) grad[p] = 0.0;
+    const int64_t ntiles = np / 9;
+    double g9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t tt = 0; tt < ntiles; ++tt)
+      for (int p = 0; p < 9; ++p) g9[p] += hp[tt * 9 + p];
+    // mean terms a^T dr/dh (r = y - m(hyp), gp:89-90 / gp:415-424)
+    const Hyp h = derive_hyp(m->kind, hyp, m->jitter);
+    double sa_lo = 0.0, sa_hi = 0.0;
+    for (int64_t i = 0; i < N; ++i) (i < m->NL ? sa_lo : sa_hi) += ha[i];
+    if (m->kind == MFGP_SF) {
+      grad[0] = -h.meanL * (sa_lo + sa_hi);
+      grad[1] = g9[1];
+      grad[2] = g9[2];
+      grad[3] = g9[3];
+    } else {
+      for (int p = 0; p < 9; ++p) grad[p] = g9[p];
+      grad[0] += -h.meanL * sa_lo - h.rho * h.meanL * sa_hi;
+      grad[3] += -std::exp(hyp[3]) * sa_hi;
+      grad[6] += -h.rho * h.meanL * sa_hi;
+    }
+  }
+  return done(MFGP_OK);
+}
+
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                               double* mu, double* var, int flags) {
   return batch_run(models, count, X, y, k, mu, var, nullptr, nullptr, flags, true, true);

@@ -86,6 +86,10 @@ hipError_t launch_cell_reduce(const double* grid, int64_t M, const double* verts
                               const double* seeds, const double* w, const double* f, const double* var,
                               double* part, double* out, int64_t* argmax, hipStream_t s);
 int64_t cell_partial_doubles(int64_t M, int ncells);
+hipError_t launch_nlml_value(const GPDesc* d, int count, double* out, hipStream_t s);
+hipError_t launch_nlml_grad(const GPDesc* d, int64_t N, double* Xi, double* Kv, double* alpha, double* part,
+                            hipStream_t s);
+int64_t nlml_partials(int64_t N);
 hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,
                               hipStream_t s);
 

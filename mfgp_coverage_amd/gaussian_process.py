@@ -19,9 +19,10 @@ Differences from the reference, all on the output side of the contract:
 * The factorisation is the GPU's; results agree with the reference to the
   tolerance in oracle/gp_oracle.py (mu rel 1e-6, var rel 1e-6 floored at
   1e-6 * k**).
-* Training (``likelihood``/``train``, gp:81-119, 344-399) and the unused extras
+* ``likelihood``/``train`` (gp:81-119, 344-399) run on the GPU with an analytic
+  gradient in place of autograd (``likelihood_and_grad``). The unused extras
   (``ExpectedImprovement``, ``draw_*``, ``pred_var``, ``get_*_var``) are out of
-  scope of this engine (SURVEY.md section 2, rows 1 and 5).
+  scope of this engine (SURVEY.md section 2, row 1).
 """
 from __future__ import annotations
 
@@ -154,6 +155,36 @@ class _DeviceGP:
         self._sync_data()
         self._push_hyp()
         return self._dev().factor()
+
+    def likelihood(self, hyp):
+        """gaussian_process.py:81-106 / 344-385: negative log-marginal likelihood of the
+        training data under `hyp`, on the GPU. (The reference also stores the factor
+        of K(hyp) in self.L as a side effect; here .L always reflects .hyp.)"""
+        self._sync_data()
+        return self._dev().nlml(self._hyp_arg(hyp))
+
+    def likelihood_and_grad(self, hyp):
+        """(NLML, dNLML/dhyp) -- what autograd's value_and_grad(self.likelihood) gives the
+        reference's train (gp:117, 397); the gradient is analytic here."""
+        self._sync_data()
+        return self._dev().nlml(self._hyp_arg(hyp), grad=True)
+
+    def _hyp_arg(self, hyp):
+        h = np.ascontiguousarray(np.asarray(hyp, dtype=np.float64).reshape(-1))
+        if h.shape[0] != self._hyp_vec().shape[0]:
+            raise TypeError("Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)")
+        return h
+
+    def callback(self, params):
+        """gaussian_process.py:219-227 / 483-491."""
+        print("Log likelihood {}".format(self.likelihood(params)))
+
+    def train(self):
+        """gaussian_process.py:108-119 / 388-399: L-BFGS-B on the NLML with its gradient."""
+        from scipy.optimize import minimize
+        result = minimize(self.likelihood_and_grad, self.hyp, jac=True, method="L-BFGS-B",
+                          callback=self.callback)
+        self.hyp = result.x
 
     def __deepcopy__(self, memo):
         new = self.__class__.__new__(self.__class__)

@@ -262,3 +262,75 @@ def cell_reductions(polys, seeds, xs, w=None, f=None, var=None):
             amax = int(idx[np.argmax(var[idx])])
         res.append((m, cen, loss, vmax, amax))
     return res
+
+
+# ---------------------------------------------------------------------------
+# Negative log-marginal likelihood and its gradient (gp:81-106 SF, gp:344-385
+# MF; the reference differentiates it with autograd for L-BFGS-B, gp:108-119 /
+# 388-399) -- checker for mfgp_nlml. Analytic gradient:
+#   NLML = 1/2 r^T K^-1 r + sum log L_ii + N/2 log(2 pi),  r = y - m(hyp)
+#   dNLML/dh = 1/2 tr((K^-1 - a a^T) dK/dh) + a^T dr/dh,   a = K^-1 r
+# ---------------------------------------------------------------------------
+
+def _sq_dist_scaled(x, xp, log_l):
+    lx = np.exp(log_l)
+    d = x[:, None, :] / lx - xp[None, :, :] / lx
+    return np.sum(d ** 2, axis=2)
+
+
+def nlml(X, y, hyp, XL=None, yL=None, jitter=JITTER, grad=False):
+    """SF: X, y = the data, hyp [4]. MF: XL, yL = lofi, X, y = hifi, hyp [9].
+    Returns NLML (and its gradient w.r.t. the log-scaled hyp when grad)."""
+    hyp = np.asarray(hyp, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    if hyp.shape[0] == 4:
+        m, s, lx = np.exp(hyp[0]), np.exp(hyp[1]), hyp[2]
+        sn = np.exp(hyp[3])
+        r2 = _sq_dist_scaled(X, X, lx)
+        E = s * np.exp(-0.5 * r2)
+        N = X.shape[0]
+        K = E + np.eye(N) * sn + np.eye(N) * jitter
+        res = y - m
+        dK = [None, E, E * r2, np.eye(N) * sn]
+        dr = [-m * np.ones(N), None, None, None]
+    else:
+        XL = np.asarray(XL, dtype=np.float64).reshape(-1, 2)
+        yL = np.asarray(yL, dtype=np.float64).reshape(-1)
+        mL, sL, sH = np.exp(hyp[0]), np.exp(hyp[1]), np.exp(hyp[4])
+        rho, snL, snH = np.exp(hyp[6]), np.exp(hyp[7]), np.exp(hyp[8])
+        mH = rho * mL + np.exp(hyp[3])
+        NL, NH = XL.shape[0], X.shape[0]
+        Xa = np.vstack([XL, X])
+        N = NL + NH
+        rL2 = _sq_dist_scaled(Xa, Xa, hyp[2])
+        rH2 = _sq_dist_scaled(Xa, Xa, hyp[5])
+        EL = sL * np.exp(-0.5 * rL2)
+        EH = sH * np.exp(-0.5 * rH2)
+        lo = np.zeros(N, dtype=bool)
+        lo[:NL] = True
+        hi = ~lo
+        cL = np.where(lo[:, None] & lo[None, :], 1.0, np.where(hi[:, None] & hi[None, :], rho ** 2, rho))
+        cH = (hi[:, None] & hi[None, :]).astype(np.float64)
+        dn = np.where(lo, snL, snH)
+        K = cL * EL + cH * EH + np.diag(dn) + np.eye(N) * jitter
+        res = np.concatenate([yL - mL, y - mH])
+        drho = np.where(lo[:, None] & lo[None, :], 0.0, np.where(hi[:, None] & hi[None, :], 2 * rho ** 2, rho))
+        dK = [None, cL * EL, cL * EL * rL2, None, cH * EH, cH * EH * rH2, drho * EL,
+              np.diag(np.where(lo, snL, 0.0)), np.diag(np.where(hi, snH, 0.0))]
+        dr = [np.concatenate([-mL * np.ones(NL), -rho * mL * np.ones(NH)]), None, None,
+              np.concatenate([np.zeros(NL), -np.exp(hyp[3]) * np.ones(NH)]), None, None,
+              np.concatenate([np.zeros(NL), -rho * mL * np.ones(NH)]), None, None]
+    L = np.linalg.cholesky(K)
+    a = np.linalg.solve(L.T, np.linalg.solve(L, res))
+    val = 0.5 * res @ a + np.sum(np.log(np.diag(L))) + 0.5 * np.log(2.0 * np.pi) * res.shape[0]
+    if not grad:
+        return float(val)
+    Kinv = np.linalg.solve(L.T, np.linalg.solve(L, np.eye(L.shape[0])))
+    W = Kinv - np.outer(a, a)
+    g = np.zeros(hyp.shape[0])
+    for p in range(hyp.shape[0]):
+        if dK[p] is not None:
+            g[p] += 0.5 * np.sum(W * dK[p])
+        if dr[p] is not None:
+            g[p] += a @ dr[p]
+    return float(val), g

@@ -277,6 +277,45 @@ def make_cells_fixture(sim):
     print("wrote cells_reference.npz,", ncase, "partitions")
 
 
+def make_nlml_fixture(gp):
+    """5. ``nlml_reference.npz``: the reference's own likelihood (gp:81-106 SF,
+    gp:344-385 MF) on anti_two_corners data at the trained hyperparameters and at
+    moved ones, with its central finite-difference gradient (h = 1e-6; the
+    reference differentiates with autograd, which is absent here)."""
+    train = _csv("anti_two_corners_hifi_train.csv")
+    prior = _csv("anti_two_corners_prior.csv")
+    hyp_sf = _csv("anti_two_corners_sf_hyp.csv")[0]
+    hyp_mf = _csv("anti_two_corners_mf_hyp.csv")[0]
+    rng = np.random.default_rng(7)
+    out = {"train": train, "prior": prior}
+    cases = []
+    for n in (50, 130):
+        for j, h in enumerate((hyp_sf, hyp_sf + np.array([0.0, 0.3, -0.2, 30.0]))):
+            cases.append((f"sf_n{n}_h{j}", "sf", n, h))
+    for n in (30, 90):
+        for j, h in enumerate((hyp_mf, hyp_mf + 0.2 * rng.standard_normal(9) + np.array([0, 0, 0, 0, 0, 0, 0, 0, 20]))):
+            cases.append((f"mf_n{n}_h{j}", "mf", n, h))
+    for name, kind, n, h in cases:
+        X, y = train[:n, :2].copy(), train[:n, 2:3].copy()
+        if kind == "sf":
+            m = gp.SFGP(X, y, 1)
+        else:
+            m = gp.MFGP(prior[:, :2].copy(), prior[:, 2:3].copy(), X, y, 1, 1)
+        val = m.likelihood(h.copy())
+        fd = np.zeros(h.shape[0])
+        for p in range(h.shape[0]):
+            e = np.zeros(h.shape[0])
+            e[p] = 1e-6
+            fd[p] = (m.likelihood(h + e) - m.likelihood(h - e)) / 2e-6
+        out[name + "_hyp"] = h
+        out[name + "_n"] = np.array(n)
+        out[name + "_nlml"] = np.array(val)
+        out[name + "_fdgrad"] = fd
+    out["cases"] = np.array([c[0] for c in cases])
+    np.savez_compressed(os.path.join(OUT, "nlml_reference.npz"), **out)
+    print("wrote nlml_reference.npz,", len(cases), "cases")
+
+
 if __name__ == "__main__":
     gp = _import_reference()
     make_reference_fixture(gp)
@@ -284,3 +323,4 @@ if __name__ == "__main__":
     sim = _import_simulator()
     make_choi_fixture(gp, sim)
     make_cells_fixture(sim)
+    make_nlml_fixture(gp)

@@ -174,3 +174,25 @@ def test_oracle_cell_reductions_vs_reference():
         np.testing.assert_allclose(sum(r[2] for r in res), fx[f"c{i}_loss"], rtol=1e-13)
         np.testing.assert_array_equal(np.array([r[3] for r in res]), fx[f"c{i}_maxvar"][:, 0])
         np.testing.assert_array_equal(xs[[r[4] for r in res]], fx[f"c{i}_argmax"])
+
+
+def _nlml_case(fx, c):
+    h, n = fx[c + "_hyp"], int(fx[c + "_n"])
+    X, y = fx["train"][:n, :2], fx["train"][:n, 2]
+    if c.startswith("sf"):
+        return (X, y, h), {}
+    return (X, y, h), {"XL": fx["prior"][:, :2], "yL": fx["prior"][:, 2]}
+
+
+def test_oracle_nlml_vs_reference():
+    """likelihood (gp:81-106 / 344-385): the oracle's value equals the reference's, and
+    its analytic gradient matches the reference's central finite differences
+    (h = 1e-6; looser where K is nearly singular at the trained noise e^-37.8)."""
+    fx = F.load("nlml_reference.npz")
+    for c in (str(v) for v in fx["cases"]):
+        args, kw = _nlml_case(fx, c)
+        v, g = O.nlml(*args, grad=True, **kw)
+        np.testing.assert_allclose(v, fx[c + "_nlml"], rtol=1e-12)
+        fd = fx[c + "_fdgrad"]
+        tol = 1e-3 if c.endswith("h0") else 1e-5
+        assert np.all(np.abs(g - fd) <= tol * np.maximum(np.abs(fd), 1.0)), (c, g, fd)
