@@ -316,6 +316,17 @@ def make_nlml_fixture(gp):
     print("wrote nlml_reference.npz,", len(cases), "cases")
 
 
+def make_log_headers():
+    """6. ``log_headers.json``: the column headers of the reference's own logs
+    (Data/atc24_choi_hmf_{loss,agent,sample}.csv), for the runner's CSV schemas."""
+    import json
+    out = {}
+    for kind in ("loss", "agent", "sample"):
+        out[kind] = list(pd.read_csv(os.path.join(DATA, f"atc24_choi_hmf_{kind}.csv"), nrows=2).columns)
+    with open(os.path.join(OUT, "log_headers.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     gp = _import_reference()
     make_reference_fixture(gp)
@@ -324,3 +335,4 @@ if __name__ == "__main__":
     make_choi_fixture(gp, sim)
     make_cells_fixture(sim)
     make_nlml_fixture(gp)
+    make_log_headers()
