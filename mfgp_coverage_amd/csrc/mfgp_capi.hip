@@ -105,7 +105,7 @@ struct mfgp_model {
   // resident V = L^-1 psi^T [vtiles][vld][PBM]; rows [0, v_n) valid for the current factor and grid
   double* V = nullptr;
   int64_t vld = 0, vtiles = 0, v_n = 0;
-  double* tred = nullptr;     // [vtiles][2] per-tile (max, argmax) of var
+  double* tred = nullptr;     // [vtiles][2] per-tile (max, argmax) of var, then the tiles' arrival counter
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0;
 };
@@ -277,9 +277,13 @@ int ensure_v(mfgp_model* m) {
   m->V = V;
   m->vld = vld;
   if (tiles > m->vtiles || !m->tred) {
+    // [arrival counter | (max, argmax) per tile]; the counter is zero between
+    // launches (the last tile of each launch resets it)
     if (m->tred) HIP_TRY(hipFree(m->tred));
     m->tred = nullptr;
-    HIP_TRY(hipMalloc(&m->tred, sizeof(double) * 2 * tiles));
+    HIP_TRY(hipMalloc(&m->tred, sizeof(double) * (2 * tiles + 1)));
+    HIP_TRY(hipMemsetAsync(m->tred, 0, sizeof(double) * (2 * tiles + 1), s));
+    HIP_TRY(hipStreamSynchronize(s));
   }
   m->vtiles = tiles;
   return MFGP_OK;
@@ -963,7 +967,6 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     }
     if (nv > 0 && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
     if (np > nv && (rc = enqueue_predict(c, dd + nb + nv, hd + nb + nv, np - nv))) return rc;
-    if (np > 0 && (vmax || vargmax)) HIP_TRY(launch_var_argmax(dd + nb, np, c->stream));
     if ((rc = release_slot(c, slot))) return rc;
     for (int i = 0; i < np; ++i) {
       porder[i]->v_n = porder[i]->NL + porder[i]->NH;
@@ -1051,8 +1054,7 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
     for (int64_t it = 0; it < C; ++it) {
       if (hipSuccess != launch_choi_select(dd + 2 * it, threshold, pts, max_points, c->stream) ||
           hipSuccess != launch_inc_factor(dd + 2 * it, 1, hd[2 * it].n0, c->stream) ||
-          hipSuccess != launch_vstream(dd + 2 * it + 1, 1, ntiles_grid(M), c->stream) ||
-          hipSuccess != launch_var_argmax(dd + 2 * it + 1, 1, c->stream))
+          hipSuccess != launch_vstream(dd + 2 * it + 1, 1, ntiles_grid(M), c->stream))
         return fail(set_err(MFGP_ERR_DEVICE, "sample_points: launch failed"));
     }
     if ((rc = release_slot(c, slot))) return fail(rc);

@@ -47,7 +47,7 @@ struct GPDesc {
   double* var;         // [M]
   double* vmax;        // fused np.amax(var) (or null)
   int64_t* vargmax;    // fused first argmax of var (or null)
-  double* tred;        // [ceil(M/PBM)][2] per-tile (max, argmax) partials of var (k_var_argmax)
+  double* tred;        // [1 + 2 ceil(M/PBM)]: tiles' arrival counter, then per-tile (max, argmax) of var
   int* gate;           // device loop gate (null = always run); 0 makes the gated kernels no-ops
   int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
   const double* srcX;  // device rows to append at row N - k_new (k_append), or null

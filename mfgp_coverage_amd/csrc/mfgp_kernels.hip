@@ -563,11 +563,14 @@ __device__ __forceinline__ void half_mma(const double* frag, const double* __res
 }
 
 // Fused np.amax / np.argmax of a GP's variance (simulator.py:672, 842, 1014 and
-// the argmax of compute_sample_points, sim:352): every cell tile publishes its
-// (max, first argmax) from its epilogue; k_var_argmax reduces the tiles (the
-// kernel boundary orders the partials -- a device-scope fence per tile would
-// write back the XCD's L2 each time). Called by wave 0 of the tile's workgroup,
-// lane l holding cell c0 + l (valid if inside the grid).
+// the argmax of compute_sample_points, sim:352). Every cell tile publishes its
+// (max, first argmax) from its epilogue; the last tile to arrive reduces them.
+// The hand-off avoids device-scope fences (a release fence per workgroup would
+// write back the XCD's L2 each time): the partial is stored with an agent-scope
+// atomic store (write-through), drained with s_waitcnt, then the arrival counter
+// is bumped; the last arriver reads the partials with agent-scope atomic loads
+// and resets the counter for the next launch. Called by wave 0 of the tile's
+// workgroup, lane l holding cell c0 + l (valid if inside the grid).
 __device__ __forceinline__ void argmax_pair(double& bv, int64_t& bi, double ov, int64_t oi) {
   if (ov > bv || (ov == bv && oi < bi)) {
     bv = ov;
@@ -581,9 +584,29 @@ __device__ void var_argmax_tile(const GPDesc& d, double v, int64_t c, bool valid
   int64_t bi = valid ? c : INT64_MAX;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  const int64_t ntiles = ntiles_grid(d.M);
+  unsigned* cnt = reinterpret_cast<unsigned*>(d.tred);   // tred = [counter | (max, argmax) per tile]
+  double* part = d.tred + 1;
+  unsigned old = 0;
   if (lane == 0) {
-    d.tred[2 * blockIdx.x] = bv;
-    d.tred[2 * blockIdx.x + 1] = (double)bi;
+    __hip_atomic_store(part + 2 * blockIdx.x, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 2 * blockIdx.x + 1, (double)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  old = __shfl(old, 0);
+  if (old != (unsigned)(ntiles - 1)) return;
+  bv = -__builtin_inf();
+  bi = INT64_MAX;
+  for (int64_t t = lane; t < ntiles; t += 64)
+    argmax_pair(bv, bi, __hip_atomic_load(part + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                (int64_t)__hip_atomic_load(part + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  if (lane == 0) {
+    if (d.vmax) *d.vmax = bv;
+    if (d.vargmax) *d.vargmax = bi;
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -597,7 +620,7 @@ __global__ __launch_bounds__(NT) void k_var_argmax(const GPDesc* __restrict__ de
   __shared__ int64_t si[NT / 64];
   double bv = -__builtin_inf();
   int64_t bi = INT64_MAX;
-  for (int64_t t = tid; t < ntiles; t += NT) argmax_pair(bv, bi, d.tred[2 * t], (int64_t)d.tred[2 * t + 1]);
+  for (int64_t t = tid; t < ntiles; t += NT) argmax_pair(bv, bi, d.tred[1 + 2 * t], (int64_t)d.tred[2 + 2 * t]);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
   if (lane == 0) {
