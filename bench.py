@@ -121,10 +121,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # ranks map onto the visible GPUs (identity on a full node; the gloo rehearsal
+    # below can stack several ranks on one GPU)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # MFGP_DIST_BACKEND=gloo rehearses the N>1 path (sharding, barriers, the
+    # gather, max-over-ranks) with host-side collectives; the default is RCCL
+    backend = os.environ.get("MFGP_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from mfgp_coverage_amd import _lib, synthetic
     from mfgp_coverage_amd.ensemble import gather_trajectories, shard_seeds
 
@@ -168,6 +177,8 @@ def main():
                                       var.data_ptr(), asynchronous=True, vmax_ptr=varmax[s].data_ptr())
 
         def aggregate(traj):
+            if backend != "nccl":
+                traj = traj.cpu()
             _, agg_mean, agg_std = gather_trajectories(traj, world)   # the single RCCL exchange
             return torch.stack([agg_mean, torch.nan_to_num(agg_std)])
 
@@ -204,7 +215,7 @@ def main():
         ctx.synchronize()
         tb = ctx.timing()
         ctx.enable_timing(False)
-        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         if not os.environ.get("MFGP_LIB"):   # diagnostic library builds compute garbage on purpose
