@@ -12,18 +12,22 @@ all-gathered over RCCL for the loss/variance aggregation of runner.py:144-147.
 
 Two update paths are timed back to back on the same workload, with identical
 results (tests/test_gpu_incremental.py):
-  value          -- the library's default path: bordered-Cholesky append of the
-                    k rows (k_inc_factor) and one pass over the resident
-                    V = L^-1 psi^T for mean/variance at every cell (k_vstream);
+  value          -- the library's default path: ONE launch per step
+                    (k_inc_stream): producer workgroups append the k rows to the
+                    factor (bordered Cholesky; L21 gathered from the resident
+                    V = L^-1 psi^T), the cell tiles stream V once for mean and
+                    variance at every cell, picking L21 / L22 up in-kernel;
   full_recompute -- what the reference does per update: full refactor
                     (k_assemble/potrf/panel/syrk) and V recomputed from scratch
                     (k_predict).
 
 value = (ranks x seeds x steps) / max-over-ranks wall time.
-roofline (value): k_vstream, HBM-bound; algorithmic bytes per launch =
-  B x 8 x [M (n0 + k + 4) + n0 (k + 1)] (V_old read once, V_new + mu + var
-  written, grid read; L21 and z once) over its average launch time (HIP events
-  on the launch stream); peak = MI355X HBM3E 8 TB/s.
+roofline (value): k_inc_stream, HBM-bound; algorithmic bytes per launch =
+  B x 8 x [M (n0 + k + 4) + n0 (3k + 1)] (V_old read once; V_new, mu, var
+  written; grid read; L21 gathered from V, written to A and read back; z once)
+  over its average duration from HIP events on the launch stream, every 8th
+  step of the timed region sampled (an event pair costs a few microseconds of
+  stream time); peak = MI355X HBM3E 8 TB/s.
 roofline (full_recompute): k_predict, MFMA-bound; B x (M N^2 + 4 M N) f64 flops
   per launch; peak = MI355X f64 MFMA spec.
 cpu_baseline: the oracle's diag-only NumPy restatement (Cholesky, triangular
@@ -46,13 +50,15 @@ sys.path.insert(0, ROOT)
 METRIC = "GP posterior updates/sec (128×128 grid, N_train=2048) at 1/2/4/8 MI355X"
 PEAK_F64_TFLOPS = 78.6   # MI355X f64 matrix (= vector) spec
 PEAK_HBM_GBS = 8000.0    # MI355X HBM3E
+TIMING_STRIDE = 8        # events bracket every 8th launch of the timed region
+FUSED = os.environ.get("MFGP_FUSED", "1") != "0"
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--seeds-per-gpu", type=int, default=8)
     p.add_argument("--grid", type=int, default=128)
     p.add_argument("--nl", type=int, default=1024)
@@ -161,6 +167,8 @@ def main():
         ctx = _lib.context() if incremental else _lib.Context(local)
         ctx.set_stream(stream.cuda_stream)
         ctx.set_incremental(incremental)
+        # MFGP_FUSED=0: the append and the predict as two launches (diagnostic)
+        ctx.set_fused(FUSED)
         models = []
         for wl in wls:
             mdl = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
@@ -186,8 +194,9 @@ def main():
             step(s)
         aggregate(varmax[:W].transpose(0, 1).contiguous())   # first-use kernel loads / communicator setup
         ctx.synchronize()
-        # HIP events around the predict launches only inside the timed region
+        # HIP events around every 8th predict launch inside the timed region
         ctx.enable_timing(not os.environ.get("MFGP_NO_TIMING"), predict_only=True)
+        ctx.set_timing_stride(TIMING_STRIDE)
         ctx.reset_timing()
         if world > 1:
             dist.barrier()
@@ -208,6 +217,7 @@ def main():
         tm = ctx.timing()
         # per-stage breakdown: a few more (untimed) steps with every stage bracketed by events
         ctx.enable_timing(True)
+        ctx.set_timing_stride(1)
         ctx.reset_timing()
         nb_steps = min(5, K)
         for s in range(W, W + nb_steps):
@@ -238,12 +248,13 @@ def main():
         elapsed, tm = inc["elapsed"], inc["tm"]
         assert inc["stats"]["inc_factor"] >= K and inc["stats"]["vstream"] >= K, inc["stats"]
         n0 = N - k
-        vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (k + 1))
+        vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (3 * k + 1))
         v_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
         v_gbs = vbytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
         # PMC bytes come from the committed profile of the default configuration
         default_cfg = (G, NL, NH, B, k, a.hyp) == (128, 1024, 1024, 8, 8, "australia8_mf")
-        traffic, traffic_src = pmc_traffic("k_vstream") if default_cfg else (None, None)
+        kern = "k_inc_stream" if FUSED else "k_vstream"
+        traffic, traffic_src = pmc_traffic(kern) if default_cfg else (None, None)
         out = {
             "metric": METRIC,
             "value": world * B * K / elapsed,
@@ -262,15 +273,18 @@ def main():
                             f"{' (BASELINE configs[3])' if default_cfg else ''}: {B} seeds/GPU, "
                             f"{G}x{G} grid (M={M}), N_L={NL} lofi + N_H={NH} hifi ({NH0} + {k} new agent "
                             f"samples appended per update), factor update + mean/var at every cell, fp64",
-                "update": "incremental: bordered-Cholesky append (k_inc_factor) + one pass over the resident "
-                          "V = L^-1 psi^T (k_vstream); full_recompute below is the reference's per-update work",
+                "update": ("incremental, one launch per step (k_inc_stream): bordered-Cholesky append + one "
+                           "pass over the resident V = L^-1 psi^T" if FUSED else
+                           "incremental: bordered-Cholesky append (k_inc_stream) + one pass over the resident "
+                           "V = L^-1 psi^T (k_vstream)") + "; full_recompute below is the reference's per-update work",
                 "seeds_per_gpu": B, "grid": G, "N_train": N, "N_lofi": NL, "N_hifi": NH, "agents": k,
                 "global_seeds": world * B, "parallelism": f"seed-sharded x{world}, 1 RCCL all_gather",
             },
             "roofline": {
                 "bound": "hbm", "achieved": v_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": v_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "k_vstream", "bytes_per_launch": vbytes, "avg_launch_ms": v_ms,
+                "kernel": kern, "bytes_per_launch": vbytes, "avg_launch_ms": v_ms,
+                "timing": f"HIP events around every {TIMING_STRIDE}th launch of the timed region",
             },
             "host_enqueue_ms_per_step": inc["host_ms"],
             "breakdown_ms_per_step": inc["breakdown"],
@@ -279,7 +293,7 @@ def main():
             ft = full["tm"]
             flops = B * (M * N * N + 4 * M * N)
             avg_ms = ft["predict_ms"] / max(1, ft["predict_launches"])
-            achieved = flops / (avg_ms * 1e-3) / 1e12
+            achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else float("nan")
             ftraffic, _ = pmc_traffic("k_predict") if default_cfg else (None, None)
             out["full_recompute"] = {
                 "value": world * B * K / full["elapsed"],

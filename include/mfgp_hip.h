@@ -58,11 +58,20 @@ int mfgp_ctx_synchronize(mfgp_ctx* ctx);
  * Results agree with the full path to rounding. 0 = refactor and recompute V
  * on every update, as the reference does. */
 int mfgp_ctx_set_incremental(mfgp_ctx* ctx, int enable);
+/* With incremental updates: run a batch's bordered appends and the one-pass
+ * predicts that follow them as ONE launch (k_inc_stream: the append's producer
+ * workgroups hand L21 / L22 to the cell tiles inside the kernel). Default on;
+ * 0 = two launches (k_inc_stream for the append alone, then k_vstream). Same
+ * numbers either way. */
+int mfgp_ctx_set_fused(mfgp_ctx* ctx, int enable);
 /* Kernel timing with HIP events on the launch stream: enable = 1 times every
  * predict-kernel launch (fused predict or one-pass incremental predict) and
  * every factor stage; 2 times the predict launches only (each event pair is a
  * few microseconds of stream time); 0 = off. */
 int mfgp_ctx_enable_timing(mfgp_ctx* ctx, int enable);
+/* Bracket only every stride-th eligible launch with events (default 1), so a
+ * timed run samples kernel durations without paying the events on every step. */
+int mfgp_ctx_set_timing_stride(mfgp_ctx* ctx, int64_t stride);
 /* Sum of predict-kernel durations (ms) and launch count since the last reset;
  * also the same for the factor stage (assemble + blocked Cholesky). */
 int mfgp_ctx_get_timing(mfgp_ctx* ctx, double* predict_ms, int64_t* predict_launches,
@@ -104,7 +113,8 @@ int64_t mfgp_model_nl(const mfgp_model* m);
 int64_t mfgp_model_m(const mfgp_model* m);
 /* Path introspection (tests / benchmarks): out[0..n) = {factor rows (-1 = none),
  * resident V rows, full refactors, bordered appends, full predicts, one-pass
- * predicts}. */
+ * predicts, grid lattice axes nx, ny (0 = the grid is not a lattice: appends
+ * locate new points by a scan)}. */
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n);
 /* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
 int mfgp_get_factor(mfgp_model* m, double* L_out);

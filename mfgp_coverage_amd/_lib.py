@@ -30,6 +30,8 @@ SIGNATURES = {
     "mfgp_ctx_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "mfgp_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "mfgp_ctx_set_incremental": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mfgp_ctx_set_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mfgp_ctx_set_timing_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "mfgp_batch_append_predict_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -145,9 +147,17 @@ class Context:
         or full refactor + full V recompute on every update (the reference's work)."""
         check(lib().mfgp_ctx_set_incremental(self.handle, 1 if on else 0))
 
+    def set_fused(self, on=True):
+        """Bordered append + one-pass predict of a batch in one launch (default on)."""
+        check(lib().mfgp_ctx_set_fused(self.handle, 1 if on else 0))
+
     def enable_timing(self, on=True, predict_only=False):
         """HIP-event timing of the predict launches (and, unless predict_only, the factor stages)."""
         check(lib().mfgp_ctx_enable_timing(self.handle, (2 if predict_only else 1) if on else 0))
+
+    def set_timing_stride(self, stride):
+        """Time only every stride-th eligible launch (events sample the kernel durations)."""
+        check(lib().mfgp_ctx_set_timing_stride(self.handle, int(stride)))
 
     def reset_timing(self):
         check(lib().mfgp_ctx_reset_timing(self.handle))
@@ -243,10 +253,12 @@ class Model:
         return lib().mfgp_model_n(self.handle)
 
     def stats(self):
-        """{factor_rows, v_rows, full_factor, inc_factor, full_predict, vstream} (path counters)."""
-        out = (ctypes.c_int64 * 6)()
-        check(lib().mfgp_model_stats(self.handle, out, 6))
-        keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream")
+        """{factor_rows, v_rows, full_factor, inc_factor, full_predict, vstream} (path
+        counters) and the grid's lattice axes {lattice_nx, lattice_ny} (0: not a lattice)."""
+        out = (ctypes.c_int64 * 8)()
+        check(lib().mfgp_model_stats(self.handle, out, 8))
+        keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream",
+                "lattice_nx", "lattice_ny")
         return dict(zip(keys, (int(v) for v in out)))
 
     def sample_points(self, threshold, max_points):

@@ -66,6 +66,7 @@ struct mfgp_ctx {
   size_t ws_bytes = 0;
   // timing: 0 off, 1 predict + factor launches, 2 predict launches only
   int timing = 0;
+  int64_t timing_stride = 1, timing_seq = 0;   // bracket every stride-th eligible launch
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
   double t_predict = 0.0, t_factor = 0.0;
@@ -75,6 +76,7 @@ struct mfgp_ctx {
   // incremental append / predict (bordered Cholesky + resident V); off = always
   // refactor and recompute V from scratch, as the reference does
   bool incremental = true;
+  bool fused = true;          // bordered append + one-pass predict in one launch (k_inc_stream)
 };
 
 struct mfgp_model {
@@ -102,10 +104,13 @@ struct mfgp_model {
   // grid (device)
   int64_t M = 0, Mcap = 0;
   double* grid = nullptr;
+  GridLattice lat{};        // lattice structure of the grid (nx == 0: none)
   // resident V = L^-1 psi^T [vtiles][vld][PBM]; rows [0, v_n) valid for the current factor and grid
   double* V = nullptr;
   int64_t vld = 0, vtiles = 0, v_n = 0;
   double* tred = nullptr;     // [vtiles][2] per-tile (max, argmax) of var, then the tiles' arrival counter
+  unsigned* sync = nullptr;   // k_inc_stream hand-off words {arrivals, L21 ready, L22 ready} (zeroed)
+  unsigned epoch = 0;         // last k_inc_stream epoch of this model
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0;
 };
@@ -160,6 +165,7 @@ hipEvent_t ev_get(mfgp_ctx* c) {
 int ev_begin(mfgp_ctx* c, EvPair& p, int kind) {
   p.a = p.b = nullptr;
   if (!c->timing || (c->timing == 2 && kind != 0)) return MFGP_OK;
+  if (c->timing_seq++ % c->timing_stride != 0) return MFGP_OK;
   p.a = ev_get(c);
   p.b = ev_get(c);
   p.kind = kind;
@@ -327,6 +333,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.A = m->A;
   d.Linv = m->Linv;
   d.grid = m->grid;
+  d.lat = m->lat;
   d.V = m->V;
   d.zv = m->zv;
   d.iscr = m->iscr;
@@ -340,6 +347,10 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.srcX = nullptr;
   d.srcY = nullptr;
   d.k_new = 0;
+  d.sync = nullptr;
+  d.epoch = 0;
+  d.nprod = 0;
+  d.tiles = 0;
   d.ld = m->ld;
   d.N = m->NL + m->NH;
   d.NL = m->NL;
@@ -381,12 +392,12 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
 }
 
 int enqueue_inc_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
-  int64_t max_n0 = 0;
-  for (int i = 0; i < count; ++i) max_n0 = std::max(max_n0, hd[i].n0);
+  int64_t max_np = 0;
+  for (int i = 0; i < count; ++i) max_np = std::max<int64_t>(max_np, hd[i].nprod);
   EvPair ev{};
   int rc = ev_begin(c, ev, 1);
   if (rc) return rc;
-  HIP_TRY(launch_inc_factor(dd, count, max_n0, c->stream));
+  HIP_TRY(launch_inc_factor(dd, count, max_np, c->stream));
   return ev_end(c, ev);
 }
 
@@ -417,12 +428,35 @@ int enqueue_predict(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   return ev_end(c, ev);
 }
 
+int status_error(int st) {
+  if (st == INT_MIN)   // wait_flag gave up (mfgp_kernels.hip): a hand-off inside k_inc_stream never arrived
+    return set_err(MFGP_ERR_DEVICE, "device synchronisation timeout in the fused append+predict launch");
+  return set_err(MFGP_ERR_NOT_PD, "Matrix is not positive definite (leading minor of order %d)", st);
+}
+
 int read_status(mfgp_model* m) {
   int st = INT_MAX;
   HIP_TRY(hipMemcpy(&st, m->status, sizeof(int), hipMemcpyDeviceToHost));
-  if (st != INT_MAX)
-    return set_err(MFGP_ERR_NOT_PD, "Matrix is not positive definite (leading minor of order %d)", st);
+  if (st != INT_MAX) return status_error(st);
   return MFGP_OK;
+}
+
+int ensure_sync(mfgp_model* m) {
+  if (m->sync) return MFGP_OK;
+  HIP_TRY(hipMalloc(&m->sync, 4 * sizeof(unsigned)));
+  HIP_TRY(hipMemsetAsync(m->sync, 0, 4 * sizeof(unsigned), m->ctx->stream));
+  return MFGP_OK;
+}
+
+// Bordered appends and their one-pass predicts in one k_inc_stream launch.
+int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
+  int64_t max_blocks = 0;
+  for (int i = 0; i < count; ++i) max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_grid(hd[i].M));
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 0);
+  if (rc) return rc;
+  HIP_TRY(launch_inc_stream(dd, count, max_blocks, c->stream));
+  return ev_end(c, ev);
 }
 
 bool hyp_same(const mfgp_model* m) {
@@ -463,10 +497,19 @@ void mark_inc_factor(mfgp_model* m) {
   m->ablk = std::max(m->ablk, nblocks_factor(m->factor_N));
 }
 
-void fill_inc_desc(GPDesc& d, mfgp_model* m) {
+// Descriptor of a bordered append of rows [factor_N, N) (k_inc_stream; the
+// caller sets tiles = 1 and the predict outputs to stream the cells too).
+int fill_inc_desc(GPDesc& d, mfgp_model* m) {
+  int rc = ensure_sync(m);
+  if (rc) return rc;
   fill_desc(d, m);
   d.n0 = m->factor_N;
   d.vres = m->V ? m->v_n : 0;
+  d.sync = m->sync;
+  if (++m->epoch == 0) m->epoch = 1;
+  d.epoch = m->epoch;
+  d.nprod = (int)fused_producers(d.n0);
+  return MFGP_OK;
 }
 
 // Factor one model now (synchronous, status checked).
@@ -498,7 +541,7 @@ int update_factor(mfgp_model* m) {
   int rc, slot;
   GPDesc* hd = acquire_slot(c, slot, rc);
   if (!hd) return rc;
-  fill_inc_desc(hd[0], m);
+  if ((rc = fill_inc_desc(hd[0], m))) return rc;
   const GPDesc* dd = nullptr;
   if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
   if ((rc = enqueue_inc_factor(c, dd, hd, 1))) return rc;
@@ -594,8 +637,7 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
   for (int* s : c->async_status) {
     int st = INT_MAX;
     HIP_TRY(hipMemcpy(&st, s, sizeof(int), hipMemcpyDeviceToHost));
-    if (st != INT_MAX && rc == MFGP_OK)
-      rc = set_err(MFGP_ERR_NOT_PD, "Matrix is not positive definite (leading minor of order %d)", st);
+    if (st != INT_MAX && rc == MFGP_OK) rc = status_error(st);
   }
   c->async_status.clear();
   return rc;
@@ -608,9 +650,24 @@ int mfgp_ctx_set_incremental(mfgp_ctx* c, int enable) {
   return MFGP_OK;
 }
 
+int mfgp_ctx_set_fused(mfgp_ctx* c, int enable) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->fused = enable != 0;
+  return MFGP_OK;
+}
+
 int mfgp_ctx_enable_timing(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   c->timing = (enable == 2) ? 2 : (enable != 0 ? 1 : 0);
+  return MFGP_OK;
+}
+
+int mfgp_ctx_set_timing_stride(mfgp_ctx* c, int64_t stride) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (stride < 1) return set_err(MFGP_ERR_ARG, "timing stride must be >= 1");
+  c->timing_stride = stride;
+  c->timing_seq = 0;
   return MFGP_OK;
 }
 
@@ -672,6 +729,7 @@ void mfgp_model_destroy(mfgp_model* m) {
   if (m->grid) (void)hipFree(m->grid);
   if (m->V) (void)hipFree(m->V);
   if (m->tred) (void)hipFree(m->tred);
+  if (m->sync) (void)hipFree(m->sync);
   delete m;
 }
 
@@ -709,6 +767,7 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
     HIP_TRY(hipMalloc(&m->grid, sizeof(double) * 2 * src->M));
     HIP_TRY(hipMemcpyAsync(m->grid, src->grid, sizeof(double) * 2 * src->M, hipMemcpyDeviceToDevice, c->stream));
     m->M = m->Mcap = src->M;
+    m->lat = src->lat;
     // resident V (the Choi planner clones a model and keeps appending to the copy, sim:339)
     if (m->factored && src->V && src->v_n > 0 && src->vld == round_up(m->cap, PRB)) {
       if ((rc = ensure_v(m))) return rc;
@@ -732,6 +791,48 @@ int mfgp_model_set_hyp(mfgp_model* m, const double* hyp, int nhyp, double jitter
   return MFGP_OK;
 }
 
+// Is the grid a lattice of two strictly monotone axes, one coordinate constant
+// along runs of consecutive cells (meshgrid order, either way round)?
+GridLattice detect_lattice(const double* g, int64_t M) {
+  GridLattice L{};
+  if (M < 1 || M > INT_MAX) return L;
+  auto monotone = [](const double* v, int64_t n, int64_t stride) {
+    if (n < 2) return v[0] == v[0];
+    const bool up = v[stride] > v[0];
+    for (int64_t i = 1; i < n; ++i) {
+      const double a = v[(i - 1) * stride], b = v[i * stride];
+      if (!(up ? b > a : b < a)) return false;
+    }
+    return true;
+  };
+  for (int s = 0; s < 2; ++s) {       // s = the coordinate constant along a run
+    const int f = 1 - s;
+    int64_t run = 1;
+    while (run < M && g[2 * run + s] == g[s]) ++run;
+    if (M % run) continue;
+    bool ok = true;
+    for (int64_t i = 0; i < M && ok; ++i)
+      ok = g[2 * i + s] == g[2 * (i - i % run) + s] && g[2 * i + f] == g[2 * (i % run) + f];
+    const int64_t ns = M / run;
+    if (!ok || !monotone(g + s, ns, 2 * run) || !monotone(g + f, run, 2)) continue;
+    // slow axis: values g[2 j run + s], stride run; fast axis: g[2 j + f], stride 1
+    const int64_t xn = s == 0 ? ns : run, xst = s == 0 ? run : 1;
+    const int64_t yn = s == 0 ? run : ns, yst = s == 0 ? 1 : run;
+    const double x0 = g[0], x1 = g[2 * (xn - 1) * xst];
+    const double y0 = g[1], y1 = g[2 * (yn - 1) * yst + 1];
+    L.nx = (int)xn;
+    L.ny = (int)yn;
+    L.sx = xst;
+    L.sy = yst;
+    L.x0 = x0;
+    L.y0 = y0;
+    L.xinv = xn > 1 ? (double)(xn - 1) / (x1 - x0) : 0.0;
+    L.yinv = yn > 1 ? (double)(yn - 1) / (y1 - y0) : 0.0;
+    return L;
+  }
+  return L;
+}
+
 int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
   int rc = check_model(m);
   if (rc) return rc;
@@ -748,6 +849,12 @@ int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
   m->M = M;
   if (M > 0) HIP_TRY(hipMemcpyAsync(m->grid, xs, sizeof(double) * 2 * M, hipMemcpyDefault, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  m->lat = GridLattice{};
+  if (M > 0) {
+    std::vector<double> h(2 * (size_t)M);
+    HIP_TRY(hipMemcpy(h.data(), m->grid, sizeof(double) * 2 * M, hipMemcpyDeviceToHost));
+    m->lat = detect_lattice(h.data(), M);
+  }
   return MFGP_OK;
 }
 
@@ -826,9 +933,9 @@ int64_t mfgp_model_n(const mfgp_model* m) { return m ? m->NL + m->NH : -1; }
 
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
   if (!m || !out) return set_err(MFGP_ERR_ARG, "null model/out");
-  const int64_t v[6] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
-                        m->n_full_predict, m->n_vstream};
-  for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+  const int64_t v[8] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+                        m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny};
+  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
@@ -917,8 +1024,11 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         if (factor_current(models[b0 + i])) order.push_back(models[b0 + i]);
       for (int i = 0; i < nb; ++i) {
         mfgp_model* m = order[i];
-        if (i < ninc) fill_inc_desc(hd[i], m);
-        else fill_desc(hd[i], m);
+        if (i < ninc) {
+          if ((rc = fill_inc_desc(hd[i], m))) return rc;
+        } else {
+          fill_desc(hd[i], m);
+        }
         const int mi = (int)(std::find(models + b0, models + b0 + nb, m) - models);
         if (dev_src && k[mi] > 0) {
           hd[i].srcX = X + 2 * src_off[mi];
@@ -958,14 +1068,30 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         if (vargmax) pd.vargmax = vargmax + mi;
       }
     }
+    // bordered appends whose one-pass predicts follow from the same rows (V
+    // resident up to the old factor) run as one k_inc_stream launch: their
+    // factor descriptors take the predict outputs and the hand-off state
+    bool fuse = c->fused && ninc > 0 && ninc == nv;
+    for (int i = 0; fuse && i < ninc; ++i) fuse = order[i] == porder[i] && hd[i].n0 == porder[i]->v_n;
+    if (fuse) {
+      for (int i = 0; i < ninc; ++i) {
+        GPDesc& fd = hd[i];
+        const GPDesc& pd = hd[nb + i];
+        fd.mu = pd.mu;
+        fd.var = pd.var;
+        fd.vmax = pd.vmax;
+        fd.vargmax = pd.vargmax;
+        fd.tiles = 1;
+      }
+    }
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
     if (do_factor) {
       if (dev_src && nfull > 0) HIP_TRY(launch_append(dd + ninc, nfull, c->stream));
-      if (ninc > 0 && (rc = enqueue_inc_factor(c, dd, hd, ninc))) return rc;
+      if (ninc > 0 && (rc = fuse ? enqueue_inc_stream(c, dd, hd, ninc) : enqueue_inc_factor(c, dd, hd, ninc))) return rc;
       if (nfull > 0 && (rc = enqueue_factor(c, dd + ninc, hd + ninc, nfull))) return rc;
     }
-    if (nv > 0 && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
+    if (nv > 0 && !fuse && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
     if (np > nv && (rc = enqueue_predict(c, dd + nb + nv, hd + nb + nv, np - nv))) return rc;
     if ((rc = release_slot(c, slot))) return rc;
     for (int i = 0; i < np; ++i) {
@@ -1033,11 +1159,15 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
     for (int64_t it = 0; it < C; ++it) {
       t->NH += 1;   // assume the iteration runs; truncated below if the loop stopped
       GPDesc& fd = hd[2 * it];
-      fill_inc_desc(fd, t);
+      if ((rc = fill_inc_desc(fd, t))) return fail(rc);
       fd.mu = mu_s;
       fd.vmax = vmax;
       fd.vargmax = vargmax;
       fd.gate = gate;
+      if (c->fused) {   // the iteration's append and predict in one launch
+        fd.var = var_s;
+        fd.tiles = 1;
+      }
       mark_inc_factor(t);
       GPDesc& pd = hd[2 * it + 1];
       fill_desc(pd, t);
@@ -1052,10 +1182,12 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, (int)(2 * C), &dd))) return fail(rc);
     for (int64_t it = 0; it < C; ++it) {
-      if (hipSuccess != launch_choi_select(dd + 2 * it, threshold, pts, max_points, c->stream) ||
-          hipSuccess != launch_inc_factor(dd + 2 * it, 1, hd[2 * it].n0, c->stream) ||
-          hipSuccess != launch_vstream(dd + 2 * it + 1, 1, ntiles_grid(M), c->stream))
-        return fail(set_err(MFGP_ERR_DEVICE, "sample_points: launch failed"));
+      const bool ok = hipSuccess == launch_choi_select(dd + 2 * it, threshold, pts, max_points, c->stream) &&
+                      (c->fused ? hipSuccess == launch_inc_stream(dd + 2 * it, 1, hd[2 * it].nprod + ntiles_grid(M),
+                                                                   c->stream)
+                                : (hipSuccess == launch_inc_factor(dd + 2 * it, 1, hd[2 * it].nprod, c->stream) &&
+                                   hipSuccess == launch_vstream(dd + 2 * it + 1, 1, ntiles_grid(M), c->stream)));
+      if (!ok) return fail(set_err(MFGP_ERR_DEVICE, "sample_points: launch failed"));
     }
     if ((rc = release_slot(c, slot))) return fail(rc);
     int64_t st[2] = {0, 0};

@@ -160,11 +160,12 @@ __device__ __forceinline__ double div_(double a, double b) {
 }
 
 // K entry (i, j), both < N, jitter and noise included (gp:253-254 / gp:523-529).
-__device__ __forceinline__ double k_entry(const Hyp& h, const double* __restrict__ X, int64_t NL,
-                                          int64_t gi, int64_t gj) {
+// pi / pj: the rows' coordinates (x, y).
+__device__ __forceinline__ double k_entry_pts(const Hyp& h, int64_t NL, int64_t gi, const double* pi, int64_t gj,
+                                              const double* pj) {
 #pragma clang fp contract(off)
-  const double xi = X[2 * gi], yi = X[2 * gi + 1];
-  const double xj = X[2 * gj], yj = X[2 * gj + 1];
+  const double xi = pi[0], yi = pi[1];
+  const double xj = pj[0], yj = pj[1];
   const double kl = se_scaled(div_(xi, h.lL), div_(yi, h.lL), div_(xj, h.lL), div_(yj, h.lL), h.sL);
   double v;
   if (h.kind == 0) {
@@ -184,6 +185,10 @@ __device__ __forceinline__ double k_entry(const Hyp& h, const double* __restrict
     }
   }
   return v;
+}
+__device__ __forceinline__ double k_entry(const Hyp& h, const double* __restrict__ X, int64_t NL, int64_t gi,
+                                          int64_t gj) {
+  return k_entry_pts(h, NL, gi, X + 2 * gi, gj, X + 2 * gj);
 }
 
 __device__ __forceinline__ void tri_index(int64_t t, int& I, int& J) {

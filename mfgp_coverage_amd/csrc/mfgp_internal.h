@@ -14,10 +14,12 @@ constexpr int PRB = 128;  // predict: training rows per left-looking block
 constexpr int PBM = 64;   // predict: grid cells per workgroup
 constexpr int PNT = 256;  // predict: threads per workgroup (4 waves; two workgroups per CU)
 constexpr int KINC = 16;  // incremental append: at most this many new rows per launch
-constexpr int INC_CHUNK = 256;   // rows of L21 per k_inc_l21 workgroup
+constexpr int FUSED_CHUNK = 128; // rows of L21 per k_inc_stream producer workgroup
 constexpr int64_t inc_scratch_doubles(int64_t cap) {
-  return 1 + KINC + ((cap + INC_CHUNK - 1) / INC_CHUNK) * (KINC * KINC + KINC);
+  return 1 + KINC + ((cap + FUSED_CHUNK - 1) / FUSED_CHUNK) * (KINC * KINC + KINC);
 }
+// k_inc_stream producers for a factor current for n0 rows (at least one: the finish)
+inline int64_t fused_producers(int64_t n0) { return n0 > 0 ? (n0 + FUSED_CHUNK - 1) / FUSED_CHUNK : 1; }
 
 // Hyperparameters in linear scale, derived on the host from the log-scaled
 // vectors of simulator.py:53-56 / 83-84. SF uses the *L fields only.
@@ -34,6 +36,15 @@ struct Hyp {
 };
 
 // One GP of a batch. Device pointers; sizes in elements.
+// A grid that is a lattice of two strictly monotone axes (cell e = ix*sx + iy*sy
+// holds (xax[ix], yax[iy])), found by the host at set_grid; nx == 0 = not one.
+// Lets the append kernel locate a grid point with a few probes instead of a scan.
+struct GridLattice {
+  int nx, ny;
+  int64_t sx, sy;
+  double x0, xinv, y0, yinv;   // index estimate: rint((x - x0) * xinv)
+};
+
 struct GPDesc {
   const double* X;     // [N,2] training coords: lofi rows [0,NL), hifi rows [NL,N)
   const double* y;     // [N]
@@ -58,6 +69,11 @@ struct GPDesc {
   int64_t n0;          // incremental kernels: rows [n0, N) are new (factor / V rows valid below n0)
   int64_t vres;        // k_inc_factor: rows of V valid for the current factor (0 = none)
   int64_t ablk;        // k_inc_factor: 64-row blocks of A / Linv already initialised
+  GridLattice lat;     // lattice structure of `grid` (nx == 0: none)
+  unsigned* sync;      // k_inc_stream hand-off: {producer arrivals, L21 ready, L22 / z2 ready}
+  unsigned epoch;      // k_inc_stream: value of this launch's ready flags (never 0)
+  int nprod;           // k_inc_stream: producer workgroups ahead of the cell tiles
+  int tiles;           // k_inc_stream: 1 = the launch also streams the cell tiles (one-pass predict)
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -71,7 +87,6 @@ inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1)
 hipError_t launch_append(const GPDesc* d, int count, hipStream_t s);
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);
 hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStream_t s);
-hipError_t launch_panel_diag(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s);
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
@@ -79,9 +94,11 @@ hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStr
 hipError_t set_stamps(long long* p);
 #endif
 hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream_t s);
-hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s);
+// bordered append (k_inc_stream without cell tiles); max_nprod = max over GPs of nprod
+hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, hipStream_t s);
+// bordered append + one-pass predict in one launch; max_blocks = max over GPs of nprod + cell tiles
+hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
-hipError_t launch_var_argmax(const GPDesc* d, int count, hipStream_t s);
 hipError_t launch_cell_reduce(const double* grid, int64_t M, const double* verts, const int* vstart, int ncells,
                               const double* seeds, const double* w, const double* f, const double* var,
                               double* part, double* out, int64_t* argmax, hipStream_t s);

@@ -36,6 +36,21 @@ __device__ long long* g_stamps;
   do {            \
   } while (0)
 #endif
+// k_inc_stream timeline stamps (GP 0 only; diagnostic builds)
+#ifdef MFGP_STAMPS
+#define FSTAMP(id)                                                                                 \
+  do {                                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x == 0)                                                       \
+      atomicMax((unsigned long long*)&g_stamps[id], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+  } while (0)
+#else
+#define FSTAMP(id) \
+  do {             \
+  } while (0)
+#endif
+#ifndef MFGP_SPIN_SLEEP
+#define MFGP_SPIN_SLEEP 16
+#endif
 
 // (shared device helpers: mfgp_device.h)
 
@@ -356,78 +371,6 @@ __global__ __launch_bounds__(NT) void k_panel(const GPDesc* __restrict__ descs, 
       }
 }
 
-// Step kb of the blocked Cholesky in one launch: every workgroup factors and
-// inverts the diagonal tile (redundantly -- it is latency, not work, that matters
-// here) and then forms one panel tile L_ik = A_ik Linv_kk^T; workgroup 0 also
-// writes L_kk and Linv_kk. Grid (max(1, tiles below), batch). The A_ik tile
-// streams into LDS by DMA while the diagonal factor runs.
-__global__ __launch_bounds__(NT) void k_panel_diag(const GPDesc* __restrict__ descs, int kb) {
-  const GPDesc& d = descs[blockIdx.y];
-  const int64_t N = d.N, ld = d.ld;
-  const int64_t nb = nblocks_factor(N);
-  if (kb >= nb) return;
-  const int64_t ib = kb + 1 + (int64_t)blockIdx.x;
-  const bool do_panel = ib < nb;
-  if (!do_panel && blockIdx.x > 0) return;
-  __shared__ double sh[2 * NB * SP + (NB / DB) * DB * DP + (NB / DB - 1) * DB * DP + TILE];
-  double* const S = sh;
-  double* const R = sh + NB * SP;
-  double* const T = R + NB * SP;
-  double* const U = T + (NB / DB) * DB * DP;
-  double* const As = U + (NB / DB - 1) * DB * DP;   // A_ik image [k][i] (DMA)
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int64_t o = (int64_t)kb * NB;
-  double* __restrict__ A = d.A;
-  if (do_panel) dma_rows64(As, A, ld, ib * NB, o, NB, w, lane);
-  {
-    double v[NB * NB / NT];
-#pragma unroll
-    for (int t = 0; t < NB * NB / NT; ++t) {
-      const int e = tid + t * NT, i = e & 63, j = e >> 6;
-      v[t] = A[(o + j) * ld + o + i];
-    }
-#pragma unroll
-    for (int t = 0; t < NB * NB / NT; ++t) {
-      const int e = tid + t * NT, i = e & 63, j = e >> 6;
-      S[i * SP + j] = (j <= i) ? v[t] : 0.0;
-    }
-  }
-  __syncthreads();
-  factor_invert_64(S, R, T, U, o, N, d.status);
-  if (blockIdx.x == 0) {
-    double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
-#pragma unroll 4
-    for (int e = tid; e < NB * NB; e += NT) {
-      const int i = e & 63, j = e >> 6;
-      A[(o + j) * ld + o + i] = S[i * SP + j];
-      Li[j * NB + i] = R[i * SP + j];
-    }
-  }
-  if (!do_panel) return;
-  __syncthreads();   // S is free
-  // Bs[m][j] = Linv[j][m] (swizzled k-major image in the S region)
-  for (int e = tid; e < NB * NB; e += NT) {
-    const int m = e >> 6, j = e & 63;
-    S[swz(m, j)] = R[j * SP + m];
-  }
-  vm_wait_all();     // the A_ik DMA has landed
-  __syncthreads();
-  Acc acc;
-  acc_zero(acc);
-  tile_mma<false>(As, S, acc, wm, wn, lane);
-  const int r = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
-        A[(o + col) * ld + ib * NB + row] = acc.c[mt][nt][v];
-      }
-}
-
 // Trailing update: A_ij -= L_ik L_jk^T for kb < j <= i (lower tiles only).
 // Trailing tiles t0, t0+1, ... of step kb (t0 = 1 skips tile (kb+1, kb+1), which
 // the look-ahead diagonal kernel updates itself).
@@ -578,7 +521,7 @@ __device__ __forceinline__ void argmax_pair(double& bv, int64_t& bi, double ov, 
   }
 }
 
-__device__ void var_argmax_tile(const GPDesc& d, double v, int64_t c, bool valid) {
+__device__ void var_argmax_tile(const GPDesc& d, double v, int64_t c, bool valid, int64_t tile) {
   const int lane = threadIdx.x & 63;
   double bv = valid ? v : -__builtin_inf();
   int64_t bi = valid ? c : INT64_MAX;
@@ -589,8 +532,8 @@ __device__ void var_argmax_tile(const GPDesc& d, double v, int64_t c, bool valid
   double* part = d.tred + 1;
   unsigned old = 0;
   if (lane == 0) {
-    __hip_atomic_store(part + 2 * blockIdx.x, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(part + 2 * blockIdx.x + 1, (double)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 2 * tile, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 2 * tile + 1, (double)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -607,31 +550,6 @@ __device__ void var_argmax_tile(const GPDesc& d, double v, int64_t c, bool valid
     if (d.vmax) *d.vmax = bv;
     if (d.vargmax) *d.vargmax = bi;
     __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__global__ __launch_bounds__(NT) void k_var_argmax(const GPDesc* __restrict__ descs) {
-  const GPDesc& d = descs[blockIdx.x];
-  if (d.M <= 0 || (!d.vmax && !d.vargmax)) return;
-  if (d.gate && *d.gate == 0) return;
-  const int64_t ntiles = ntiles_grid(d.M);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __shared__ double sv[NT / 64];
-  __shared__ int64_t si[NT / 64];
-  double bv = -__builtin_inf();
-  int64_t bi = INT64_MAX;
-  for (int64_t t = tid; t < ntiles; t += NT) argmax_pair(bv, bi, d.tred[1 + 2 * t], (int64_t)d.tred[2 + 2 * t]);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
-  if (lane == 0) {
-    sv[w] = bv;
-    si[w] = bi;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int j = 1; j < NT / 64; ++j) argmax_pair(bv, bi, sv[j], si[j]);
-    if (d.vmax) *d.vmax = bv;
-    if (d.vargmax) *d.vargmax = bi;
   }
 }
 
@@ -854,7 +772,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
       d.mu[c] = ms + h.meanH;
       d.var[c] = vc;
     }
-    if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M);
+    if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M, blockIdx.x);
   }
 }
 
@@ -877,23 +795,71 @@ __global__ __launch_bounds__(NT) void k_extract_z(const GPDesc* __restrict__ des
 // when every new point is a grid cell (the simulator samples only grid cells,
 // sim:705 / sim:875) and V = L11^-1 psi^T is resident for rows < n0, column c of
 // L21^T is V[:, cell(c)] -- psi(cell, X) and K(X, x_new) are the same numbers,
-// same operation order (k_entry vs k_predict's psi). Two launches:
-//   k_inc_l21    (row chunks x GPs): find the cells, gather the V columns into
-//                rows n0.. of A and the chunk's partial L21 L21^T, L21 z1 (MFMA);
-//   k_inc_finish (one workgroup per GP): sum the partials, L22, z2, the new
-//                Linv rows. Off the grid (or without a resident V) k_inc_finish
-//                solves L21^T itself by blocked forward substitution (one
-//                workgroup, f64 MFMA; slower, but general).
+// same operation order (k_entry vs k_predict's psi). One launch (k_inc_stream,
+// below): producer workgroups over 128-row chunks find the cells, gather the V
+// columns into rows n0.. of A and sum their chunk's L21 L21^T, L21 z1 (MFMA); the
+// last producer to arrive sums the partials and computes L22, z2 and the new
+// Linv rows. Off the grid (or without a resident V) it solves L21^T itself by
+// blocked forward substitution (one workgroup, f64 MFMA; slower, but general).
 // ---------------------------------------------------------------------------
-constexpr int ICH = INC_CHUNK;             // rows of L21 per k_inc_l21 workgroup
+constexpr int FCH = FUSED_CHUNK;           // rows of L21 per producer workgroup
 constexpr int ISZ = KINC * KINC + KINC;    // partial sums per chunk: L21 L21^T | L21 z1
 // iscr layout: [0] = 1 if the new points were found on the grid with V resident
-// (k_append), [1 + c] = their cells, [ISC0 + chunk * ISZ ...] = k_inc_l21 partials
+// (k_append), [ISC0 + chunk * ISZ ...] = the producers' partials
 constexpr int ISC0 = 1 + KINC;
+
+// Data handed between workgroups of ONE launch (k_inc_stream) goes through
+// write-through stores and L2-bypassing loads (relaxed, agent scope); each
+// producer drains its stores (s_waitcnt) before it signals. No fence: a
+// __threadfence writes the whole L2 back. XW = false: plain accesses (the
+// consumers are later launches).
+template <bool XW>
+__device__ __forceinline__ double ldx(const double* p) {
+  if constexpr (XW) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool XW>
+__device__ __forceinline__ void stx(double* p, double v) {
+  if constexpr (XW) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void publish(unsigned* f, unsigned v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait (thread 0, the workgroup joins at the barrier) until *f == v. Bounded:
+// after ~1 s the kernel records a synchronisation failure in *status (reported
+// by the host) and goes on, so a lost signal can never hang the device.
+constexpr int SYNC_FAIL = INT_MIN;
+__device__ void wait_flag(const GPDesc& d, const unsigned* f, unsigned v) {
+  if (threadIdx.x == 0) {
+    int it = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != v) {
+      __builtin_amdgcn_s_sleep(MFGP_SPIN_SLEEP);
+      if (++it == (1 << 22)) {
+        atomicMin(d.status, SYNC_FAIL);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Coordinates / observation of training row `row`: rows landing in this launch
+// ([N - k_new, N), device source) are read from the source itself.
+__device__ __forceinline__ const double* row_pt(const GPDesc& d, int64_t row) {
+  const int64_t at = d.N - d.k_new;
+  return (d.srcX && row >= at) ? d.srcX + 2 * (row - at) : d.X + 2 * row;
+}
+__device__ __forceinline__ double row_obs(const GPDesc& d, int64_t row) {
+  const int64_t at = d.N - d.k_new;
+  return (d.srcY && row >= at) ? d.srcY[row - at] : d.y[row];
+}
 
 // Identity padding for the 64-row blocks [ablk, nbf) entered for the first time,
 // columns [c_lo, c_hi) (the full predict reads whole blocks: padding rows must
 // stay finite), and, with `linv`, their Linv blocks.
+template <bool XW = false>
 __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, bool linv) {
   const int64_t nbf = nblocks_factor(d.N);
   const int tid = threadIdx.x, nthr = blockDim.x;
@@ -903,7 +869,7 @@ __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, boo
       for (int64_t e = tid; e < (c1 - c_lo) * NB; e += nthr) {
         const int64_t col = c_lo + (e >> 6);
         const int64_t row = bb * NB + (e & 63);
-        d.A[col * d.ld + row] = (col == row) ? 1.0 : 0.0;
+        stx<XW>(&d.A[col * d.ld + row], (col == row) ? 1.0 : 0.0);
       }
     }
     if (linv)
@@ -915,7 +881,7 @@ __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, boo
 // wave). Lane (r, q) holds L21[r][j], j = 4s + q, eight 4-row steps in flight per
 // wave. With `cell`, L21[r][.] is gathered from the V column of the grid cell and
 // written to row n0 + r of A; otherwise it is read from there.
-template <int NW>
+template <int NW, bool XW = false>
 __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo, int64_t j_hi,
                                   double (*red)[ISZ]) {
   const int64_t n0 = d.n0, ld = d.ld;
@@ -937,7 +903,7 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
       const int64_t j = 4 * (s0 + NW * u) + q;
       const bool ok = j < j_hi;
       const int64_t jj = ok ? j : j_lo;
-      a[u] = gp(src)[jj * sstride];
+      a[u] = from_v ? gp(src)[jj * sstride] : ldx<XW>(src + jj * sstride);
       zz[u] = gp(d.zv)[jj];
       a[u] = (ok && r < k) ? a[u] : 0.0;
       zz[u] = ok ? zz[u] : 0.0;
@@ -945,7 +911,7 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
 #pragma unroll
     for (int u = 0; u < IU; ++u) {
       const int64_t j = 4 * (s0 + NW * u) + q;
-      if (from_v && r < k && j < j_hi) d.A[j * ld + n0 + r] = a[u];
+      if (from_v && r < k && j < j_hi) stx<XW>(&d.A[j * ld + n0 + r], a[u]);
       sacc = mfma(a[u], a[u], sacc);
       uacc = mfma(a[u], zz[u], uacc);
     }
@@ -986,84 +952,133 @@ __device__ void find_cells(const GPDesc& d, const double* px, const double* py, 
   }
 }
 
-// Grid (row chunks, GPs), 512 threads: find the new points on the grid, gather
-// their V columns into rows n0.. of A and sum this chunk's partials. Chunk 0
-// also lands device-resident new rows in X / y and publishes iscr[0]
-// (1 = the V columns were gathered; 0 = k_inc_finish solves for L21).
-constexpr int LNT = 512;
-__global__ __launch_bounds__(LNT) void k_inc_l21(const GPDesc* __restrict__ descs) {
-  const GPDesc& d = descs[blockIdx.y];
+// Index of grid point (px, py) from the lattice structure: the rounded axis
+// estimate and its neighbours, checked for exact equality (INT_MAX if none).
+// The axes are strictly monotone, so an exact match is the only one.
+__device__ int lattice_cell(const GPDesc& d, double px, double py) {
+  const GridLattice& L = d.lat;
+  if (L.nx <= 0 || !(px == px) || !(py == py)) return INT_MAX;
+  const GLOBAL dv2* g2 = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid));
+  const int ix = (int)rint(fmin(fmax((px - L.x0) * L.xinv, 0.0), (double)(L.nx - 1)));
+  const int iy = (int)rint(fmin(fmax((py - L.y0) * L.yinv, 0.0), (double)(L.ny - 1)));
+  int64_t e[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int cx = ix + t / 3 - 1, cy = iy + t % 3 - 1;
+    e[t] = (cx >= 0 && cx < L.nx && cy >= 0 && cy < L.ny) ? cx * L.sx + cy * L.sy : -1;
+  }
+  dv2 g[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) g[t] = g2[e[t] >= 0 ? e[t] : 0];
+  int hit = INT_MAX;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    if (e[t] >= 0 && g[t].x == px && g[t].y == py) hit = (int)e[t];
+  return hit;
+}
+
+// One producer chunk: land device-resident new rows (chunk 0), find the new
+// points' grid cells, gather their V columns into rows n0.. of A for rows
+// [chunk * ch, +ch) and store the chunk's partials. Returns false when L21 is not
+// a set of V columns (off the grid / no resident V): the finish solves for it.
+// All NTHR threads take part; `cell` and `red` are in LDS.
+__device__ __noinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell, double (*red)[ISZ]) {
+  constexpr int NTHR = NT;
+  constexpr bool XW = true;
   const int64_t n0 = d.n0, N = d.N;
   const int k = (int)(N - n0);
-  if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
-  if (d.gate && *d.gate == 0) return;
   const int tid = threadIdx.x;
   const int64_t kn = d.k_new, at = N - kn;   // rows [at, N) arrive from srcX / srcY
-  if (blockIdx.x == 0 && kn > 0 && d.srcX) {
-    for (int64_t e = tid; e < 3 * kn; e += LNT) {
+  if (chunk == 0 && kn > 0 && d.srcX) {
+    // consumers are later launches (this one reads the sources: row_pt / row_obs)
+    for (int64_t e = tid; e < 3 * kn; e += NTHR) {
       if (e < 2 * kn) const_cast<double*>(d.X)[2 * at + e] = d.srcX[e];
       else const_cast<double*>(d.y)[at + e - 2 * kn] = d.srcY[e - 2 * kn];
     }
   }
   const bool try_v = n0 > 0 && d.vres >= n0 && d.V != nullptr && d.M > 0;
   if (!try_v) {
-    if (blockIdx.x == 0 && tid == 0) d.iscr[0] = 0.0;
-    return;
+    if (chunk == 0 && tid == 0) stx<XW>(d.iscr, 0.0);
+    return false;
   }
-  const int64_t j_lo = (int64_t)blockIdx.x * ICH;
-  if (j_lo >= n0) return;
-  const int64_t j_hi = j_lo + ICH < n0 ? j_lo + ICH : n0;
-  __shared__ int cell[KINC];
-  __shared__ double red[LNT / 64][ISZ];
+  const int64_t j_lo = chunk * ch;
+  const int64_t j_hi = j_lo + ch < n0 ? j_lo + ch : n0;
   if (tid < KINC) cell[tid] = INT_MAX;
-  double px[KINC], py[KINC];
-#pragma unroll
-  for (int c = 0; c < KINC; ++c) {
-    const int64_t row = n0 + c;
-    const double* src = (d.srcX && row >= at) ? d.srcX + 2 * (row - at) : d.X + 2 * row;
-    px[c] = c < k ? src[0] : __builtin_nan("");
-    py[c] = c < k ? src[1] : __builtin_nan("");
+  __syncthreads();
+  // lattice grids: a few probes per point; otherwise (or for a point off the
+  // lattice) every thread scans the grid
+  if (tid < k) {
+    const double* p = row_pt(d, n0 + tid);
+    cell[tid] = lattice_cell(d, p[0], p[1]);
   }
   __syncthreads();
-  find_cells<LNT>(d, px, py, cell);
-  __syncthreads();
+  bool found = true;
+  for (int c = 0; c < k; ++c) found = found && cell[c] != INT_MAX;
+  if (!found) {
+    double px[KINC], py[KINC];
+#pragma unroll
+    for (int c = 0; c < KINC; ++c) {
+      const double* p = row_pt(d, n0 + (c < k ? c : 0));
+      px[c] = c < k ? p[0] : __builtin_nan("");
+      py[c] = c < k ? p[1] : __builtin_nan("");
+    }
+    __syncthreads();
+    if (tid < KINC) cell[tid] = INT_MAX;
+    __syncthreads();
+    find_cells<NTHR>(d, px, py, cell);
+    __syncthreads();
+  }
+  if (XW) FSTAMP(38);   // latest producer with its cells
   bool use_v = true;
   for (int c = 0; c < k; ++c) use_v = use_v && cell[c] != INT_MAX;
-  if (blockIdx.x == 0 && tid == 0) d.iscr[0] = use_v ? 1.0 : 0.0;
-  if (!use_v) return;   // off the grid: k_inc_finish solves
-  inc_init_blocks(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
+  if (chunk == 0 && tid == 0) stx<XW>(d.iscr, use_v ? 1.0 : 0.0);
+  if (!use_v || j_lo >= n0) return use_v;   // off the grid: the finish solves
+  inc_init_blocks<XW>(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
   __syncthreads();
-  inc_schur_partial<LNT / 64>(d, cell, j_lo, j_hi, red);
+  inc_schur_partial<NTHR / 64, XW>(d, cell, j_lo, j_hi, red);
   __syncthreads();
-  double* __restrict__ part = d.iscr + ISC0 + (int64_t)blockIdx.x * ISZ;
-  for (int e = tid; e < ISZ; e += LNT) {
+  if (XW) FSTAMP(39);   // latest producer past its gather
+  double* __restrict__ part = d.iscr + ISC0 + chunk * ISZ;
+  for (int e = tid; e < ISZ; e += NTHR) {
     double acc = 0.0;
 #pragma unroll
-    for (int w = 0; w < LNT / 64; ++w) acc += red[w][e];
-    part[e] = acc;
+    for (int w = 0; w < NTHR / 64; ++w) acc += red[w][e];
+    stx<XW>(part + e, acc);
   }
+  return true;
 }
 
-__global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ descs) {
-  const GPDesc& d = descs[blockIdx.x];
+// LDS of the finish step (doubles; 256 threads):
+//   phase 1 (partials / L21 solve, L22):  red [0,1088) ssum [1088,1360) K22s [1360,1616) Ts [1616,2640)
+//   phase 2 (new Linv rows):              Ln [0,1024) Ps [1024,2048) Lb [2048,4064)
+//   both:                                 L22s [4064,4320)
+constexpr int FIN_LDS = 4320;
+constexpr int LBW = 32;   // Linv_OO columns staged per pass (63 rows x 32 = 2016 doubles)
+
+// The finish of a bordered append for one GP (one workgroup of NT threads): sum
+// the producers' partials (chunks of `ch` rows) or solve L21 (off the grid),
+// L22 = chol(K22 - L21 L21^T), z2, then the new rows of the diagonal-block
+// inverses. FUSED (inside k_inc_stream): signals `sync[1]` once L21 is in A (when
+// this step solved it) and `sync[2]` once L22 / z2 are, with the hand-off
+// accesses of ldx / stx.
+template <bool FUSED>
+__device__ __noinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch) {
   const int64_t n0 = d.n0, N = d.N, ld = d.ld, NL = d.NL;
   const int k = (int)(N - n0);
-  if (k <= 0 || k > KINC) return;
-  if (d.gate && *d.gate == 0) return;
   const Hyp& h = d.hf;
   double* __restrict__ A = d.A;
   const double* __restrict__ X = d.X;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
-  __shared__ double red[NT / 64][ISZ];
-  __shared__ double ssum[ISZ];
-  __shared__ double Ts[NB * KINC];      // T_I image [64][16]
-  __shared__ double Lb[NB * NB];        // Linv block bb0 (old rows), row-major [m][c]
-  __shared__ double Ln[KINC * NB];      // new rows of L inside the current block, [i][m]
-  __shared__ double L22s[KINC * KINC];  // L22, row-major
-  __shared__ double K22s[KINC * KINC];  // K22 (+ noise + jitter on the diagonal), row-major
-  __shared__ double Ps[KINC * NB];      // L_WO Linv_OO of the current block, [i][c]
+  double(*red)[ISZ] = reinterpret_cast<double(*)[ISZ]>(sm);
+  double* ssum = sm + 1088;
+  double* K22s = sm + 1360;   // K22 (+ noise + jitter on the diagonal), row-major
+  double* Ts = sm + 1616;     // T_I image [64][16]
+  double* Ln = sm;            // new rows of L inside the current block, [i][m]
+  double* Ps = sm + 1024;     // L_WO Linv_OO of the current block, [i][c]
+  double* Lb = sm + 2048;     // Linv_OO columns [cb, cb + LBW), [m][c - cb]
+  double* L22s = sm + 4064;   // L22, row-major
   const int64_t bb0 = n0 / NB;
   const int nO0 = (int)(n0 - bb0 * NB);   // old rows in block bb0
   STAMP(20);
@@ -1071,34 +1086,21 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
   {
     // one K22 entry per thread (gp:523-529 via k_entry)
     const int a = tid / KINC, b = tid % KINC;
-    K22s[tid] = (a < k && b <= a) ? k_entry(h, X, NL, n0 + a, n0 + b) : 0.0;
+    K22s[tid] = (a < k && b <= a) ? k_entry_pts(h, NL, n0 + a, row_pt(d, n0 + a), n0 + b, row_pt(d, n0 + b)) : 0.0;
   }
-  const bool gathered = n0 > 0 && d.iscr[0] != 0.0;
-  inc_init_blocks(d, gathered ? n0 : 0, nblocks_factor(N) * NB, true);
-  // block bb0's old Linv rows (never a newly initialised block when nO0 > 0),
-  // sixteen loads in flight per thread
-  if (nO0 > 0) {
-    const double* __restrict__ Li = d.Linv + bb0 * TILE;
-    double t[TILE / NT];
-#pragma unroll
-    for (int u = 0; u < TILE / NT; ++u) t[u] = gp(Li)[tid + u * NT];
-#pragma unroll
-    for (int u = 0; u < TILE / NT; ++u) {
-      const int e = tid + u * NT, m = e & 63, c = e >> 6;
-      Lb[m * NB + c] = t[u];
-    }
-  }
+  const bool gathered = n0 > 0 && ldx<FUSED>(d.iscr) != 0.0;
+  inc_init_blocks<FUSED>(d, gathered ? n0 : 0, nblocks_factor(N) * NB, true);
   __syncthreads();
   STAMP(21);
   if (gathered) {
-    const int nch = (int)((n0 + ICH - 1) / ICH);
+    const int64_t nch = (n0 + ch - 1) / ch;
     for (int e = tid; e < ISZ; e += NT) {
       // chunk partials in a fixed order; eight loads in flight per thread
       double acc = 0.0;
-      for (int c0 = 0; c0 < nch; c0 += 8) {
+      for (int64_t c0 = 0; c0 < nch; c0 += 8) {
         double t[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = (c0 + u < nch) ? gp(d.iscr)[ISC0 + (int64_t)(c0 + u) * ISZ + e] : 0.0;
+        for (int u = 0; u < 8; ++u) t[u] = (c0 + u < nch) ? ldx<FUSED>(d.iscr + ISC0 + (c0 + u) * ISZ + e) : 0.0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += t[u];
       }
@@ -1113,14 +1115,14 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int64_t row = i0 + q + 4 * v;
-        acc[v] = (row < n0 && r < k) ? k_entry(h, X, NL, row, n0 + r) : 0.0;
+        acc[v] = (row < n0 && r < k) ? k_entry_pts(h, NL, row, X + 2 * row, n0 + r, row_pt(d, n0 + r)) : 0.0;
       }
       for (int64_t J = 0; J < I; ++J) {
 #pragma unroll 4
         for (int t = 0; t < NB / 4; ++t) {
           const int64_t kc = J * NB + 4 * t + q;
-          const double a = A[kc * ld + i0 + r];                       // L[i0 + r][kc]
-          const double b = (r < k) ? A[kc * ld + n0 + r] : 0.0;       // W[kc][r]
+          const double a = A[kc * ld + i0 + r];                                // L[i0 + r][kc]
+          const double b = (r < k) ? ldx<FUSED>(&A[kc * ld + n0 + r]) : 0.0;   // W[kc][r]
           acc = mfma(-a, b, acc);
         }
       }
@@ -1137,22 +1139,18 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int64_t row = i0 + q + 4 * v;
-        if (row < n0 && r < k) A[row * ld + n0 + r] = o[v];
+        if (row < n0 && r < k) stx<FUSED>(&A[row * ld + n0 + r], o[v]);
       }
+      if (FUSED) drain_stores();
       __syncthreads();   // W_I visible to every wave; Ts free
     }
-    inc_schur_partial<NT / 64>(d, nullptr, 0, n0, red);
+    inc_schur_partial<NT / 64, FUSED>(d, nullptr, 0, n0, red);
     __syncthreads();
     for (int e = tid; e < ISZ; e += NT) ssum[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
-  }
-  STAMP(22);
-  // new rows' old-column part of block bb0 (L21 entries, in A)
-  for (int e = tid; e < k * NB; e += NT) {
-    const int i = e >> 6, m = e & 63;
-    if (m < nO0) Ln[i * NB + m] = A[(bb0 * NB + m) * ld + n0 + i];
+    if (FUSED && tid == 0) publish(d.sync + 1, d.epoch);   // L21 is in A
   }
   __syncthreads();
-  STAMP(23);
+  STAMP(22);
   // L22 = chol(K22 - L21 L21^T) and z2, wave 0 (LAPACK dpotf2 order, as in
   // factor_invert_64; lane r holds row r, DPP row broadcasts)
   if (w == 0) {
@@ -1163,7 +1161,7 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
       if (r < k && c < k) v = K22s[r * KINC + c] - ssum[r * KINC + c];
       dd[c] = v;
     }
-    const double yr = (r < k) ? d.y[n0 + r] : 0.0;
+    const double yr = (r < k) ? row_obs(d, n0 + r) : 0.0;
     double rdiag = 1.0;
     int fail = INT_MAX;
 #pragma unroll
@@ -1194,11 +1192,23 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
 #pragma unroll
       for (int c = 0; c < KINC; ++c) {
         L22s[lane * KINC + c] = (c <= lane) ? dd[c] : 0.0;
-        if (c <= lane) A[(n0 + c) * ld + n0 + lane] = dd[c];
+        if (c <= lane) stx<FUSED>(&A[(n0 + c) * ld + n0 + lane], dd[c]);
       }
-      d.zv[n0 + lane] = x;
+      stx<FUSED>(&d.zv[n0 + lane], x);
     }
     if (fail != INT_MAX && lane == 0) atomicMin(d.status, fail);
+    if (FUSED) {
+      drain_stores();
+      if (lane == 0) publish(d.sync + 2, d.epoch);   // L22 and z2 are in A / zv
+      if (FUSED) FSTAMP(32);
+    }
+  }
+  __syncthreads();
+  STAMP(23);
+  // new rows' old-column part of block bb0 (L21 entries, in A)
+  for (int e = tid; e < k * NB; e += NT) {
+    const int i = e >> 6, m = e & 63;
+    if (m < nO0) Ln[i * NB + m] = ldx<FUSED>(&A[(bb0 * NB + m) * ld + n0 + i]);
   }
   __syncthreads();
   STAMP(24);
@@ -1220,25 +1230,31 @@ __global__ __launch_bounds__(NT) void k_inc_finish(const GPDesc* __restrict__ de
         const int b = (int)(col - n0);
         Ln[i * NB + m] = (b <= a0 + i) ? L22s[(a0 + i) * KINC + b] : 0.0;
       } else if (bb != bb0) {
-        Ln[i * NB + m] = A[col * ld + r0 + i];
+        Ln[i * NB + m] = ldx<FUSED>(&A[col * ld + r0 + i]);
       }
     }
     __syncthreads();
     // P = L_WO Linv_OO: element (i, c) per thread, Linv_OO lower triangular (its
-    // upper part is stored as zeros), so the sum runs over all old rows m
-    if (nO > 0) {
-      for (int e = tid; e < nW * NB; e += NT) {
-        const int i = e >> 6, c = e & 63;
+    // upper part is stored as zeros), so the sum runs over all old rows m;
+    // Linv_OO is staged through LDS LBW columns at a time
+    for (int cb = 0; cb < nO; cb += LBW) {
+      for (int e = tid; e < nO * LBW; e += NT) {
+        const int c = e / nO, m = e - c * nO;   // consecutive threads: consecutive rows of one column
+        Lb[m * LBW + c] = (cb + c < NB) ? Li[(cb + c) * NB + m] : 0.0;
+      }
+      __syncthreads();
+      for (int e = tid; e < nW * LBW; e += NT) {
+        const int i = e / LBW, c = e % LBW;
         double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
         int m = 0;
         for (; m + 4 <= nO; m += 4) {
-          p0 += Ln[i * NB + m] * Lb[m * NB + c];
-          p1 += Ln[i * NB + m + 1] * Lb[(m + 1) * NB + c];
-          p2 += Ln[i * NB + m + 2] * Lb[(m + 2) * NB + c];
-          p3 += Ln[i * NB + m + 3] * Lb[(m + 3) * NB + c];
+          p0 += Ln[i * NB + m] * Lb[m * LBW + c];
+          p1 += Ln[i * NB + m + 1] * Lb[(m + 1) * LBW + c];
+          p2 += Ln[i * NB + m + 2] * Lb[(m + 2) * LBW + c];
+          p3 += Ln[i * NB + m + 3] * Lb[(m + 3) * LBW + c];
         }
-        for (; m < nO; ++m) p0 += Ln[i * NB + m] * Lb[m * NB + c];
-        Ps[i * NB + c] = (p0 + p1) + (p2 + p3);
+        for (; m < nO; ++m) p0 += Ln[i * NB + m] * Lb[m * LBW + c];
+        Ps[i * NB + cb + c] = (p0 + p1) + (p2 + p3);
       }
       __syncthreads();
     }
@@ -1332,23 +1348,50 @@ __device__ __forceinline__ void vs_rounds(const double* __restrict__ Vt, const d
   if (nfull * 64 < n0) vs_round<MMA, true>(vb, A, z, ld, n0, nfull * 64 + w * 16 + q, rr, arow, r, acc, vs, ms);
 }
 
-__global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs) {
-  const GPDesc& d = descs[blockIdx.y];
+// LDS of one cell tile (doubles): red [4][16 * 64] | sred [2][4][64] | L22 (row-major) | z2
+// | new rows' coordinates [16][2] | the tile's cell coordinates [64][2]
+constexpr int VS_LDS = (NT / 64) * KINC * PBM + 2 * (NT / 64) * PBM + KINC * KINC + KINC + 2 * KINC + 2 * PBM;
+static_assert(VS_LDS >= FIN_LDS, "the fused kernel's LDS holds either step");
+
+// One cell tile of the one-pass predict. FUSED (inside k_inc_stream): L21 is
+// read from A once sync[1] is signalled, L22 / z2 (with ldx) once sync[2] is.
+template <bool FUSED>
+__device__ void vstream_tile(const GPDesc& d, int64_t tile, double* sm) {
   const int64_t M = d.M;
-  const int64_t c0 = (int64_t)blockIdx.x * PBM;
-  if (c0 >= M) return;
-  if (d.gate && *d.gate == 0) return;
+  const int64_t c0 = tile * PBM;
   const int64_t n0 = d.n0, N = d.N, ld = d.ld;
   const int k = (int)(N - n0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
-  double* __restrict__ Vt = d.V + (int64_t)blockIdx.x * d.vld * PBM;
+  double* __restrict__ Vt = d.V + tile * d.vld * PBM;
   const double* __restrict__ A = d.A;
   const double* __restrict__ z = d.zv;
-  __shared__ double red[NT / 64][KINC * PBM];   // per-wave partial L21 V_old [row][cell]
-  __shared__ double sred[2][NT / 64][PBM];      // per-wave colsum(V o V), V^T z
-  __shared__ double L22[KINC * KINC + KINC];    // L22 (row-major) | z2
+  double(*red)[KINC * PBM] = reinterpret_cast<double(*)[KINC * PBM]>(sm);   // per-wave partial L21 V_old
+  double(*sred)[NT / 64][PBM] = reinterpret_cast<double(*)[NT / 64][PBM]>(sm + (NT / 64) * KINC * PBM);
+  double* L22 = sm + (NT / 64) * KINC * PBM + 2 * (NT / 64) * PBM;         // L22 (row-major) | z2
+  double* Xn = L22 + KINC * KINC + KINC;                                     // new rows' (x, y)
+  double* Gc = Xn + 2 * KINC;                                                // cells' (x, y)
+  // the epilogue's inputs are loaded ahead of the stream: a workgroup that
+  // finishes its rows must not then sit out a memory round trip at full load
+  if (k > 0) {
+    if (tid < 2 * KINC) Xn[tid] = (tid / 2 < k) ? row_pt(d, n0 + tid / 2)[tid & 1] : 0.0;
+    if (tid >= NT - 2 * PBM) {
+      const int e = tid - (NT - 2 * PBM);
+      const int64_t cc = c0 + (e >> 1) < M ? c0 + (e >> 1) : M - 1;
+      Gc[e] = d.grid[2 * cc + (e & 1)];
+    }
+    if (!FUSED) {
+      if (tid < KINC * KINC) {
+        const int ra = tid / KINC, cb = tid % KINC;
+        L22[tid] = (ra < k && cb <= ra) ? A[(n0 + cb) * ld + n0 + ra] : 0.0;
+      }
+      if (tid < KINC) L22[KINC * KINC + tid] = tid < k ? z[n0 + tid] : 0.0;
+    }
+  }
+  if (FUSED && tile == 0) FSTAMP(33);
+  if (FUSED && k > 0) wait_flag(d, d.sync + 1, d.epoch);
+  if (FUSED && tile == 0) FSTAMP(34);
   d4 acc[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
@@ -1377,11 +1420,16 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
       sred[1][w][vs_cell(nt, r)] = ms[nt];
     }
   }
-  if (tid < KINC * KINC) {
-    const int ra = tid / KINC, cb = tid % KINC;
-    L22[tid] = (ra < k && cb <= ra) ? A[(n0 + cb) * ld + n0 + ra] : 0.0;
+  if (FUSED && tile == 0) FSTAMP(35);
+  if (FUSED && k > 0) {
+    wait_flag(d, d.sync + 2, d.epoch);
+    if (tid < KINC * KINC) {
+      const int ra = tid / KINC, cb = tid % KINC;
+      L22[tid] = (ra < k && cb <= ra) ? ldx<true>(&A[(n0 + cb) * ld + n0 + ra]) : 0.0;
+    }
+    if (tid < KINC) L22[KINC * KINC + tid] = tid < k ? ldx<true>(&z[n0 + tid]) : 0.0;
   }
-  if (tid < KINC) L22[KINC * KINC + tid] = tid < k ? z[n0 + tid] : 0.0;
+  if (FUSED && tile == 0) FSTAMP(36);
   __syncthreads();
   if (tid < PBM) {
     const int e = tid;
@@ -1390,8 +1438,7 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
     double msum = (sred[1][0][e] + sred[1][1][e]) + (sred[1][2][e] + sred[1][3][e]);
     const Hyp& h = d.hp;
     if (k > 0) {
-      const int64_t cc = c < M ? c : M - 1;
-      const double gx = d.grid[2 * cc], gy = d.grid[2 * cc + 1];
+      const double gx = Gc[2 * e], gy = Gc[2 * e + 1];
       const double cLx = div_(gx, h.lL), cLy = div_(gy, h.lL);
       const double cHx = div_(gx, h.lH), cHy = div_(gy, h.lH);
       double vn[KINC];
@@ -1400,7 +1447,7 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
         vn[a] = 0.0;
         if (a < k) {
           const int64_t g = n0 + a;
-          const double tx = d.X[2 * g], ty = d.X[2 * g + 1];
+          const double tx = Xn[2 * a], ty = Xn[2 * a + 1];
           const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
           double psi;
           if (h.kind == 0) {
@@ -1428,8 +1475,66 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
       d.mu[c] = msum + h.meanH;
       d.var[c] = vc;
     }
-    if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M);
+    if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M, tile);
   }
+  if (FUSED) FSTAMP(37);   // latest tile end
+}
+
+__global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  if ((int64_t)blockIdx.x * PBM >= d.M) return;
+  if (d.gate && *d.gate == 0) return;
+  __shared__ double sm[VS_LDS];
+  vstream_tile<false>(d, blockIdx.x, sm);
+}
+
+// ---------------------------------------------------------------------------
+// The bordered append (k_inc_stream). Grid (GPs, roles); per GP, roles < nprod
+// are producers (inc_produce on FCH-row chunks of L21):
+//   producers : gather L21 into A and their partials, drain, count arrivals
+//               (sync[0]); the last one signals sync[1] (L21 complete, when
+//               gathered), runs inc_finish (signals sync[1] itself when it
+//               solves L21, then sync[2] once L22 / z2 are stored) and resets
+//               sync[0] for the next launch.
+// With d.tiles the same launch also runs the one-pass predict: roles >= nprod
+// stream the cell tiles (vstream_tile<true>), waiting for sync[1] before the
+// first L21 load and for sync[2] before the L22 solve of the epilogue. x = GP,
+// so the linear dispatch order is every GP's producer 0, then producer 1, ...,
+// then the cell tiles round-robin over the GPs: producers are dispatched before
+// any tile that waits for them and are therefore resident (no deadlock); the
+// waits are bounded anyway (wait_flag). The flags hold the launch's epoch (host
+// counter, never 0), so they need no reset. Without tiles nothing waits.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_inc_stream(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.x];
+  const int k = (int)(d.N - d.n0);
+  if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
+  if (d.gate && *d.gate == 0) return;
+  __shared__ double sm[VS_LDS];
+  const int64_t np = d.nprod, role = blockIdx.y;
+  if (role >= np) {
+    const int64_t tile = role - np;
+    if (d.tiles && tile * PBM < d.M) vstream_tile<true>(d, tile, sm);
+    return;
+  }
+  __shared__ int cell[KINC];
+  __shared__ unsigned last;
+  if (role == 0) FSTAMP(30);
+  const bool gathered = inc_produce(d, role, FCH, cell, reinterpret_cast<double(*)[ISZ]>(sm));
+  FSTAMP(40);   // latest producer done storing (before the drain)
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(d.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (old == (unsigned)(np - 1)) ? 1u : 0u;
+    if (last) {
+      __hip_atomic_store(d.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (gathered) publish(d.sync + 1, d.epoch);   // every chunk of L21 is in A
+    }
+  }
+  FSTAMP(31);   // latest producer arrival
+  __syncthreads();
+  if (last) inc_finish<true>(d, sm, FCH);   // the hand-off accesses: tiles may stream concurrently
 }
 
 // One iteration of compute_sample_points (simulator.py:344-370) on the device:
@@ -1491,10 +1596,6 @@ hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStr
   hipLaunchKernelGGL(k_potrf_diag, dim3(count), dim3(NT), 0, s, d, kb, upd);
   return hipGetLastError();
 }
-hipError_t launch_panel_diag(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s) {
-  hipLaunchKernelGGL(k_panel_diag, dim3((unsigned)(max_below > 0 ? max_below : 1), count), dim3(NT), 0, s, d, kb);
-  return hipGetLastError();
-}
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s) {
   hipLaunchKernelGGL(k_panel, dim3((unsigned)max_below, count), dim3(NT), 0, s, d, kb);
   return hipGetLastError();
@@ -1512,10 +1613,8 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
   hipLaunchKernelGGL(k_extract_z, dim3((unsigned)((max_n + NT - 1) / NT), count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
-hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_n0, hipStream_t s) {
-  const int64_t nch = max_n0 > 0 ? (max_n0 + ICH - 1) / ICH : 1;
-  hipLaunchKernelGGL(k_inc_l21, dim3((unsigned)nch, count), dim3(LNT), 0, s, d);
-  hipLaunchKernelGGL(k_inc_finish, dim3(count), dim3(NT), 0, s, d);
+hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, hipStream_t s) {
+  hipLaunchKernelGGL(k_inc_stream, dim3(count, (unsigned)max_nprod), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,
@@ -1523,8 +1622,8 @@ hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points,
   hipLaunchKernelGGL(k_choi_select, dim3(1), dim3(64), 0, s, d, threshold, points, max_points);
   return hipGetLastError();
 }
-hipError_t launch_var_argmax(const GPDesc* d, int count, hipStream_t s) {
-  hipLaunchKernelGGL(k_var_argmax, dim3(count), dim3(NT), 0, s, d);
+hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_inc_stream, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {

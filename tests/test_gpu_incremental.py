@@ -235,14 +235,26 @@ def test_incremental_not_pd_raises():
     assert m.stats()["inc_factor"] == 1
 
 
-def test_batched_device_incremental_headline_pattern(full_ctx):
-    """Batched device-source appends (k_append + k_inc_factor + k_vstream) over four MF
-    GPs with the benchmark's truncate/append step, against the full-recompute path and,
-    on the last step, the oracle."""
+@pytest.fixture(scope="module")
+def split_ctx():
+    """Incremental, but appends and predicts as separate launch groups."""
+    from mfgp_coverage_amd import _lib
+    c = _lib.Context(0)
+    c.set_fused(False)
+    return c
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_batched_device_incremental_headline_pattern(full_ctx, split_ctx, fused):
+    """Batched device-source appends over four MF GPs with the benchmark's
+    truncate/append step -- one k_inc_stream launch streaming the cells too
+    (fused) or k_inc_stream + k_vstream -- against the full-recompute path and, on the last
+    step, the oracle. GP 2 samples off the grid: its L21 is solved inside the
+    launch before the cell tiles may read it."""
     import torch
     from mfgp_coverage_amd import _lib
     G, NL, NH0, k, B = 48, 400, 500, 8, 4
-    ctx = _lib.context()
+    ctx = _lib.context() if fused else split_ctx
     cases = [_points(G, NL + NH0 + 4 * k, seed=100 + b, ongrid=(b != 2)) for b in range(B)]
     inc = [_model(ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0] for Xs, X, y in cases]
     full = [_model(full_ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0] for Xs, X, y in cases]
@@ -297,3 +309,99 @@ def test_headline_size_incremental_vs_full(full_ctx):
         assert _err(mu, var, mu_f, var_f, HYP_MF) < 1e-8
         assert np.all(var > -1e-12)
     assert a.stats()["vstream"] == 2
+
+
+@pytest.mark.parametrize("layout", ["x_major", "y_major", "warped", "shuffled", "line"])
+def test_grid_layouts_locate_new_points(layout):
+    """The append kernel finds a new point's grid cell (whose V column it gathers)
+    by lattice probes when the grid is a meshgrid of monotone axes, in either
+    order and with uneven spacing, and by a scan otherwise; both must pick the
+    same cell, so every layout streams and matches the oracle."""
+    from mfgp_coverage_amd import _lib
+    rng = np.random.default_rng(17)
+    gx = np.linspace(0.0, 1.0, 40)
+    gy = np.linspace(-0.5, 0.7, 33)[::-1]                       # decreasing axis
+    if layout == "warped":
+        gx = gx ** 2.2
+    if layout == "line":
+        Xs = np.column_stack([gx, np.full_like(gx, 0.25)])
+    elif layout == "y_major":
+        Xs = np.array([(a, b) for b in gy for a in gx])
+    else:
+        Xs = np.array([(a, b) for a in gx for b in gy])
+    if layout == "shuffled":
+        Xs = Xs[rng.permutation(Xs.shape[0])]
+    n0 = min(120, Xs.shape[0] - 16)
+    idx = rng.choice(Xs.shape[0], n0 + 16, replace=False)
+    X = Xs[idx]
+    y = _field(X, rng)
+    m, hyp = _model(_lib.context(), "sf", X[:n0], y[:n0], 0, Xs)
+    st = m.stats()
+    lattice = layout != "shuffled"
+    assert (st["lattice_nx"] > 0) == lattice, st
+    if layout == "line":
+        assert (st["lattice_nx"], st["lattice_ny"]) == (40, 1)
+    elif lattice:
+        assert (st["lattice_nx"], st["lattice_ny"]) == (40, 33)
+    m.predict()
+    for a, b in ((n0, n0 + 9), (n0 + 9, n0 + 16)):
+        m.append(X[a:b], y[a:b])
+        mu, var = m.predict()
+        mu_r, var_r = _ref("sf", X[:b], y[:b], 0, Xs, hyp)
+        assert _err(mu, var, mu_r, var_r, hyp) < TOL
+    st = m.stats()
+    assert st["inc_factor"] == 2 and st["vstream"] == 2
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_batched_ragged_fused_append_predict(full_ctx, split_ctx, fused):
+    """k_inc_stream over GPs with different producer counts and cell-tile counts:
+    new rows entering a fresh 64-row block (n0 = 256), straddling one (n0 = 127),
+    KINC = 16 rows at once and a single row; device sources; the fused VarMax."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    ctx = _lib.context() if fused else split_ctx
+    specs = [(48, 100, 156, 8), (40, 50, 250, 16), (32, 30, 90, 1), (33, 60, 67, 5)]   # G, NL, NH0, k
+    steps = 3
+    cases = [_points(G, NL + NH0 + steps * k, seed=300 + i, ongrid=True) for i, (G, NL, NH0, k) in enumerate(specs)]
+    inc = [_model(ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0]
+           for (Xs, X, y), (G, NL, NH0, k) in zip(cases, specs)]
+    full = [_model(full_ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0]
+            for (Xs, X, y), (G, NL, NH0, k) in zip(cases, specs)]
+    Ms = [c[0].shape[0] for c in cases]
+    off = np.concatenate([[0], np.cumsum(Ms)])
+    for step in range(steps):
+        Xn, yn = [], []
+        for (Xs, X, y), (G, NL, NH0, k) in zip(cases, specs):
+            lo = NL + NH0 + step * k
+            Xn.append(X[lo:lo + k])
+            yn.append(y[lo:lo + k])
+        Xd = torch.from_numpy(np.ascontiguousarray(np.vstack(Xn))).cuda()
+        yd = torch.from_numpy(np.ascontiguousarray(np.concatenate(yn))).cuda()
+        outs = []
+        for models in (inc, full):
+            for mdl, sp in zip(models, specs):
+                mdl.truncate(sp[2])
+            mu_d = torch.empty(int(off[-1]), dtype=torch.float64, device="cuda")
+            var_d = torch.empty(int(off[-1]), dtype=torch.float64, device="cuda")
+            vmax = torch.full((len(specs),), -1.0, dtype=torch.float64, device="cuda")
+            _lib.batch_append_predict(models, Xd.data_ptr(), yd.data_ptr(), [sp[3] for sp in specs],
+                                      mu_d.data_ptr(), var_d.data_ptr(), vmax_ptr=vmax.data_ptr())
+            v = var_d.cpu().numpy()
+            np.testing.assert_array_equal(vmax.cpu().numpy(), [v[off[i]:off[i + 1]].max() for i in range(len(specs))])
+            outs.append((mu_d.cpu().numpy(), v))
+        (mu, var), (mu_f, var_f) = outs
+        for i in range(len(specs)):
+            s_ = slice(off[i], off[i + 1])
+            assert _err(mu[s_], var[s_], mu_f[s_], var_f[s_], HYP_MF) < 1e-8, (step, i)
+    for i, ((Xs, X, y), (G, NL, NH0, k)) in enumerate(zip(cases, specs)):
+        lo = NL + NH0 + (steps - 1) * k
+        Xr = np.vstack([X[:NL + NH0], X[lo:lo + k]])
+        yr = np.concatenate([y[:NL + NH0], y[lo:lo + k]])
+        mu_r, var_r = _ref("mf", Xr, yr, NL, Xs, HYP_MF)
+        s_ = slice(off[i], off[i + 1])
+        assert _err(mu[s_], var[s_], mu_r, var_r, HYP_MF) < TOL
+        # the factor itself equals a fresh Cholesky of the same rows
+        np.testing.assert_allclose(inc[i].factor(), full[i].factor(), rtol=1e-6, atol=1e-9)
+        st = inc[i].stats()
+        assert st["inc_factor"] == steps and st["vstream"] == steps - 1, st

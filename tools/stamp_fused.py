@@ -1,7 +1,8 @@
-"""Diagnostic: phase stamps (s_memtime) of the incremental kernels (build_diag/libmfgp_stamps.so)."""
+"""Diagnostic: timeline of one k_inc_stream launch for GP 0 (s_memrealtime, 100 MHz),
+from a -DMFGP_STAMPS build named by argv[1] (default build_diag/libmfgp_stamps.so)."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MFGP_LIB"] = os.path.join(ROOT, "build_diag", "libmfgp_stamps.so")
+os.environ["MFGP_LIB"] = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build_diag", "libmfgp_stamps.so")
 sys.path.insert(0, ROOT)
 import numpy as np
 import torch
@@ -28,13 +29,21 @@ for wl in wls:
     models.append(m)
 mu = torch.empty(B * M, dtype=torch.float64, device=dev)
 var = torch.empty(B * M, dtype=torch.float64, device=dev)
+vmax = torch.empty(T, B, dtype=torch.float64, device=dev)
 for s in range(T):
     for m in models:
         m.truncate(NH0)
-    _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr())
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    st.zero_()
+    torch.cuda.synchronize()
+    _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
+                              vmax_ptr=vmax[s].data_ptr())
+    torch.cuda.synchronize()
 v = st.cpu().numpy()
-names = {21: "init+Lb", 22: "ssum", 23: "Ln", 24: "chol+z2", 25: "linv"}
-for i in range(21, 26):
-    print(f"{names[i]:10s} {v[i] - v[i-1]:8d} ticks")
-print("total", v[25] - v[20])
+t0 = v[30]
+names = {30: "producer 0 start", 38: "producers: cells found", 39: "producers: gathered", 40: "producers: partials stored",
+         31: "last producer arrival", 32: "L22/z2 published", 33: "tile 0 start",
+         34: "tile 0 past wait 1", 35: "tile 0 streamed", 36: "tile 0 past wait 2", 37: "last tile end"}
+for i in (30, 38, 39, 40, 31, 32, 33, 34, 35, 36, 37):
+    print(f"{names[i]:24s} {(v[i] - t0) / 100.0:9.2f} us")
+print(models[0].stats())
