@@ -111,6 +111,9 @@ struct mfgp_model {
   double* tred = nullptr;     // [vtiles][2] per-tile (max, argmax) of var, then the tiles' arrival counter
   unsigned* sync = nullptr;   // k_inc_stream hand-off words {arrivals, L21 ready, L22 ready} (zeroed)
   unsigned epoch = 0;         // last k_inc_stream epoch of this model
+  // the compact bordered rows in iscr (inc_l21c_offset) hold rows [l21c_n0, l21c_N)
+  // bordered onto l21c_n0 factor rows (-1: none)
+  int64_t l21c_n0 = -1, l21c_N = -1;
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0;
 };
@@ -248,6 +251,7 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   if (m->zv) HIP_TRY(hipFree(m->zv));
   if (m->iscr) HIP_TRY(hipFree(m->iscr));
   m->iscr = isc;
+  m->l21c_N = -1;
   m->X = X;
   m->y = y;
   m->A = A;
@@ -283,12 +287,13 @@ int ensure_v(mfgp_model* m) {
   m->V = V;
   m->vld = vld;
   if (tiles > m->vtiles || !m->tred) {
-    // [arrival counter | (max, argmax) per tile]; the counter is zero between
-    // launches (the last tile of each launch resets it)
+    // [arrival counter | (max, argmax) per 64-cell tile (k_predict) or per 32-cell
+    // wave group (one-pass predicts)]; the counter is zero between launches (the
+    // last arriver of each launch resets it)
     if (m->tred) HIP_TRY(hipFree(m->tred));
     m->tred = nullptr;
-    HIP_TRY(hipMalloc(&m->tred, sizeof(double) * (2 * tiles + 1)));
-    HIP_TRY(hipMemsetAsync(m->tred, 0, sizeof(double) * (2 * tiles + 1), s));
+    HIP_TRY(hipMalloc(&m->tred, sizeof(double) * (4 * tiles + 1)));
+    HIP_TRY(hipMemsetAsync(m->tred, 0, sizeof(double) * (4 * tiles + 1), s));
     HIP_TRY(hipStreamSynchronize(s));
   }
   m->vtiles = tiles;
@@ -337,6 +342,8 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.V = m->V;
   d.zv = m->zv;
   d.iscr = m->iscr;
+  d.l21c = m->iscr ? m->iscr + inc_l21c_offset(m->cap) : nullptr;
+  d.l22r = m->iscr ? m->iscr + inc_l22r_offset(m->cap) : nullptr;
   d.mu = nullptr;
   d.var = nullptr;
   d.vmax = nullptr;
@@ -351,6 +358,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.epoch = 0;
   d.nprod = 0;
   d.tiles = 0;
+  d.l21c_ok = 0;
   d.ld = m->ld;
   d.N = m->NL + m->NH;
   d.NL = m->NL;
@@ -403,7 +411,7 @@ int enqueue_inc_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
 
 int enqueue_vstream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_ct = 0;
-  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_grid(hd[i].M));
+  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_wg(hd[i].M));
   if (max_ct == 0) return MFGP_OK;
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
@@ -451,7 +459,7 @@ int ensure_sync(mfgp_model* m) {
 // Bordered appends and their one-pass predicts in one k_inc_stream launch.
 int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_blocks = 0;
-  for (int i = 0; i < count; ++i) max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_grid(hd[i].M));
+  for (int i = 0; i < count; ++i) max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_wg(hd[i].M));
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
@@ -489,6 +497,7 @@ void mark_full_factor(mfgp_model* m) {
   m->factor_jitter = m->jitter;
   m->ablk = std::max(m->ablk, nblocks_factor(m->factor_N));
   m->v_n = 0;   // V belonged to the previous factor
+  m->l21c_N = -1;
 }
 
 void mark_inc_factor(mfgp_model* m) {
@@ -509,7 +518,17 @@ int fill_inc_desc(GPDesc& d, mfgp_model* m) {
   if (++m->epoch == 0) m->epoch = 1;
   d.epoch = m->epoch;
   d.nprod = (int)fused_producers(d.n0);
+  d.l21c_ok = 1;   // the producers write the compact rows for (n0, N)
+  m->l21c_n0 = d.n0;
+  m->l21c_N = d.N;
   return MFGP_OK;
+}
+
+// One-pass predict over the V rows [0, v_n): the compact rows serve it when the
+// last bordered append wrote them for exactly these rows.
+void set_vstream_rows(GPDesc& d, const mfgp_model* m) {
+  d.n0 = m->v_n;
+  d.l21c_ok = (m->l21c_n0 == m->v_n && m->l21c_N == m->NL + m->NH) ? 1 : 0;
 }
 
 // Factor one model now (synchronous, status checked).
@@ -916,7 +935,7 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   hd[0].mu = c->ws;
   hd[0].var = hd[0].mu + m->M;
   const bool vst = can_vstream(m);
-  hd[0].n0 = m->v_n;
+  set_vstream_rows(hd[0], m);
   const GPDesc* dd = nullptr;
   if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
   if ((rc = vst ? enqueue_vstream(c, dd, hd, 1) : enqueue_predict(c, dd, hd, 1))) return rc;
@@ -1060,7 +1079,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; i < np; ++i) {
         GPDesc& pd = hd[nb + i];
         fill_desc(pd, porder[i]);
-        if (i < nv) pd.n0 = porder[i]->v_n;
+        if (i < nv) set_vstream_rows(pd, porder[i]);
         pd.mu = mu + oo_ord[i];
         pd.var = var + oo_ord[i];
         const int64_t mi = std::find(models + b0, models + b0 + nb, porder[i]) - models;
@@ -1171,7 +1190,7 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
       mark_inc_factor(t);
       GPDesc& pd = hd[2 * it + 1];
       fill_desc(pd, t);
-      pd.n0 = t->v_n;
+      set_vstream_rows(pd, t);
       pd.mu = mu_s;
       pd.var = var_s;
       pd.vmax = vmax;
@@ -1183,10 +1202,10 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
     if ((rc = upload_slot(c, slot, (int)(2 * C), &dd))) return fail(rc);
     for (int64_t it = 0; it < C; ++it) {
       const bool ok = hipSuccess == launch_choi_select(dd + 2 * it, threshold, pts, max_points, c->stream) &&
-                      (c->fused ? hipSuccess == launch_inc_stream(dd + 2 * it, 1, hd[2 * it].nprod + ntiles_grid(M),
+                      (c->fused ? hipSuccess == launch_inc_stream(dd + 2 * it, 1, hd[2 * it].nprod + ntiles_wg(M),
                                                                    c->stream)
                                 : (hipSuccess == launch_inc_factor(dd + 2 * it, 1, hd[2 * it].nprod, c->stream) &&
-                                   hipSuccess == launch_vstream(dd + 2 * it + 1, 1, ntiles_grid(M), c->stream)));
+                                   hipSuccess == launch_vstream(dd + 2 * it + 1, 1, ntiles_wg(M), c->stream)));
       if (!ok) return fail(set_err(MFGP_ERR_DEVICE, "sample_points: launch failed"));
     }
     if ((rc = release_slot(c, slot))) return fail(rc);

@@ -15,9 +15,15 @@ constexpr int PBM = 64;   // predict: grid cells per workgroup
 constexpr int PNT = 256;  // predict: threads per workgroup (4 waves; two workgroups per CU)
 constexpr int KINC = 16;  // incremental append: at most this many new rows per launch
 constexpr int FUSED_CHUNK = 128; // rows of L21 per k_inc_stream producer workgroup
-constexpr int64_t inc_scratch_doubles(int64_t cap) {
-  return 1 + KINC + ((cap + FUSED_CHUNK - 1) / FUSED_CHUNK) * (KINC * KINC + KINC);
+// iscr: [0] gathered flag | per-chunk partials | (at inc_l21c_offset, 128-byte
+// aligned) the compact bordered rows L21c [cap][KINC]: row j holds L21[0..k)[j],
+// then z1[j] at k (k < KINC), then zeros -- the cell tiles' MFMA A operand
+constexpr int64_t inc_l21c_offset(int64_t cap) {
+  return ((1 + KINC + ((cap + FUSED_CHUNK - 1) / FUSED_CHUNK) * (KINC * KINC + KINC)) + 15) / 16 * 16;
 }
+// then (128-byte aligned) the L22 record: L22 row-major [KINC][KINC] | z2 [KINC]
+constexpr int64_t inc_l22r_offset(int64_t cap) { return (inc_l21c_offset(cap) + cap * KINC + 15) / 16 * 16; }
+constexpr int64_t inc_scratch_doubles(int64_t cap) { return inc_l22r_offset(cap) + KINC * KINC + KINC; }
 // k_inc_stream producers for a factor current for n0 rows (at least one: the finish)
 inline int64_t fused_producers(int64_t n0) { return n0 > 0 ? (n0 + FUSED_CHUNK - 1) / FUSED_CHUNK : 1; }
 
@@ -54,6 +60,8 @@ struct GPDesc {
   double* V;           // resident V = L^-1 psi^T: [ceil(M/PBM)][vld][PBM] (tile, row, cell)
   double* zv;          // [N] z = L^-1 (y - m)
   double* iscr;        // incremental append scratch: [0] = rows gathered from V, then per-chunk partial sums
+  double* l21c;        // compact bordered rows [cap][KINC] inside iscr (inc_l21c_offset)
+  double* l22r;        // L22 (row-major) | z2 of the last bordered append, inside iscr (inc_l22r_offset)
   double* mu;          // [M]
   double* var;         // [M]
   double* vmax;        // fused np.amax(var) (or null)
@@ -74,6 +82,7 @@ struct GPDesc {
   unsigned epoch;      // k_inc_stream: value of this launch's ready flags (never 0)
   int nprod;           // k_inc_stream: producer workgroups ahead of the cell tiles
   int tiles;           // k_inc_stream: 1 = the launch also streams the cell tiles (one-pass predict)
+  int l21c_ok;         // one-pass predict: l21c holds the rows [n0, N) bordered onto V's n0 rows
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -81,6 +90,8 @@ struct GPDesc {
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
 inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
 inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1) / PBM; }
+// one-pass predict workgroups: 128 cells (two V tiles), 32 per wave
+inline __host__ __device__ int64_t ntiles_wg(int64_t M) { return (M + 2 * PBM - 1) / (2 * PBM); }
 inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1) / PRB; }
 
 // Launchers (mfgp_kernels.hip). `d` points to `count` descriptors in device memory.

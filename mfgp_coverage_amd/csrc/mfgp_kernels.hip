@@ -43,9 +43,23 @@ __device__ long long* g_stamps;
     if (threadIdx.x == 0 && blockIdx.x == 0)                                                       \
       atomicMax((unsigned long long*)&g_stamps[id], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
   } while (0)
+// per-workgroup k_inc_stream trace: g_stamps[64 + 8 * (linear WG id) + slot]
+#define WTRACE(slot)                                                                                 \
+  do {                                                                                               \
+    if (threadIdx.x == 0) {                                                                          \
+      long long* wt_ = g_stamps + 64 + 8 * (blockIdx.y * gridDim.x + blockIdx.x);                     \
+      wt_[slot] = __builtin_amdgcn_s_memrealtime();                                                  \
+      if ((slot) == 0)                                                                               \
+        wt_[7] = ((long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |                       \
+                 (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                                \
+    }                                                                                                \
+  } while (0)
 #else
 #define FSTAMP(id) \
   do {             \
+  } while (0)
+#define WTRACE(slot) \
+  do {               \
   } while (0)
 #endif
 #ifndef MFGP_SPIN_SLEEP
@@ -802,6 +816,9 @@ __global__ __launch_bounds__(NT) void k_extract_z(const GPDesc* __restrict__ des
 // Linv rows. Off the grid (or without a resident V) it solves L21^T itself by
 // blocked forward substitution (one workgroup, f64 MFMA; slower, but general).
 // ---------------------------------------------------------------------------
+#ifndef MFGP_INC_WAVES
+#define MFGP_INC_WAVES 4   // k_inc_stream waves per SIMD (occupancy; 5 measured 1-5 % slower)
+#endif
 constexpr int FCH = FUSED_CHUNK;           // rows of L21 per producer workgroup
 constexpr int ISZ = KINC * KINC + KINC;    // partial sums per chunk: L21 L21^T | L21 z1
 // iscr layout: [0] = 1 if the new points were found on the grid with V resident
@@ -903,7 +920,11 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
       const int64_t j = 4 * (s0 + NW * u) + q;
       const bool ok = j < j_hi;
       const int64_t jj = ok ? j : j_lo;
+#ifndef MFGP_DIAG_NOGATHER   // diagnostic build: no V-column loads (timing only)
       a[u] = from_v ? gp(src)[jj * sstride] : ldx<XW>(src + jj * sstride);
+#else
+      a[u] = from_v ? 1.0 : ldx<XW>(src + jj * sstride);
+#endif
       zz[u] = gp(d.zv)[jj];
       a[u] = (ok && r < k) ? a[u] : 0.0;
       zz[u] = ok ? zz[u] : 0.0;
@@ -912,6 +933,10 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
     for (int u = 0; u < IU; ++u) {
       const int64_t j = 4 * (s0 + NW * u) + q;
       if (from_v && r < k && j < j_hi) stx<XW>(&d.A[j * ld + n0 + r], a[u]);
+      // compact rows for the cell tiles: L21 | z1 at row k | zeros
+#ifndef MFGP_DIAG_NOPSTORE   // diagnostic build: no compact-row stores (timing only)
+      if (j < j_hi) stx<XW>(&d.l21c[j * KINC + r], r < k ? a[u] : (r == k ? zz[u] : 0.0));
+#endif
       sacc = mfma(a[u], a[u], sacc);
       uacc = mfma(a[u], zz[u], uacc);
     }
@@ -1050,10 +1075,11 @@ __device__ __noinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t
 
 // LDS of the finish step (doubles; 256 threads):
 //   phase 1 (partials / L21 solve, L22):  red [0,1088) ssum [1088,1360) K22s [1360,1616) Ts [1616,2640)
-//   phase 2 (new Linv rows):              Ln [0,1024) Ps [1024,2048) Lb [2048,4064)
-//   both:                                 L22s [4064,4320)
-constexpr int FIN_LDS = 4320;
-constexpr int LBW = 32;   // Linv_OO columns staged per pass (63 rows x 32 = 2016 doubles)
+//   phase 2 (new Linv rows):              Ln [0,1024) Ps [1024,2048) Lb [2048,3056)
+//   both:                                 L22s [3056,3312)
+// (26.5 KB: five workgroups of k_inc_stream fit a CU)
+constexpr int FIN_LDS = 3312;
+constexpr int LBW = 16;   // Linv_OO columns staged per pass (63 rows x 16 = 1008 doubles)
 
 // The finish of a bordered append for one GP (one workgroup of NT threads): sum
 // the producers' partials (chunks of `ch` rows) or solve L21 (off the grid),
@@ -1078,7 +1104,7 @@ __device__ __noinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch)
   double* Ln = sm;            // new rows of L inside the current block, [i][m]
   double* Ps = sm + 1024;     // L_WO Linv_OO of the current block, [i][c]
   double* Lb = sm + 2048;     // Linv_OO columns [cb, cb + LBW), [m][c - cb]
-  double* L22s = sm + 4064;   // L22, row-major
+  double* L22s = sm + 3056;   // L22, row-major
   const int64_t bb0 = n0 / NB;
   const int nO0 = (int)(n0 - bb0 * NB);   // old rows in block bb0
   STAMP(20);
@@ -1145,6 +1171,7 @@ __device__ __noinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch)
       __syncthreads();   // W_I visible to every wave; Ts free
     }
     inc_schur_partial<NT / 64, FUSED>(d, nullptr, 0, n0, red);
+    if (FUSED) drain_stores();   // the compact rows, before sync[1]
     __syncthreads();
     for (int e = tid; e < ISZ; e += NT) ssum[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
     if (FUSED && tid == 0) publish(d.sync + 1, d.epoch);   // L21 is in A
@@ -1193,13 +1220,17 @@ __device__ __noinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch)
       for (int c = 0; c < KINC; ++c) {
         L22s[lane * KINC + c] = (c <= lane) ? dd[c] : 0.0;
         if (c <= lane) stx<FUSED>(&A[(n0 + c) * ld + n0 + lane], dd[c]);
+        // the record the cell workgroups read (no line of it is read before sync[2])
+        stx<FUSED>(&d.l22r[lane * KINC + c], (c <= lane) ? dd[c] : 0.0);
       }
       stx<FUSED>(&d.zv[n0 + lane], x);
+      stx<FUSED>(&d.l22r[KINC * KINC + lane], x);
     }
     if (fail != INT_MAX && lane == 0) atomicMin(d.status, fail);
     if (FUSED) {
       drain_stores();
       if (lane == 0) publish(d.sync + 2, d.epoch);   // L22 and z2 are in A / zv
+      WTRACE(3);
       if (FUSED) FSTAMP(32);
     }
   }
@@ -1281,211 +1312,446 @@ __device__ __noinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch)
 // ---------------------------------------------------------------------------
 // Incremental predict: V is resident for rows < n0 and the factor has k = N - n0
 // <= KINC new rows (k = 0: nothing appended since the last predict).
-//   T      = psi_new^T - L21 V_old      (16 x n0 by n0 x 64 per tile, f64 MFMA)
+//   T      = psi_new^T - L21 V_old      (16 x n0 by n0 x 32 per wave, f64 MFMA)
 //   V_new  = L22^-1 T                   -> rows [n0, N) of the resident V
 //   var    = k** - colsum(V o V),  mu = m + V^T z   over all N rows
-// V_old is read once (8 n0 bytes per cell, 16-byte loads, four 4-row MFMA steps
-// in flight per wave): the kernel is HBM-bound. Grid (cell tiles, batch); the
-// lane <-> cell map of the MFMA B operand follows the 16-byte loads:
-// (nt, r) -> cell 2r + (nt & 1) + 32 (nt >> 1).
+// V_old is read once: the kernel is HBM-bound. A workgroup covers 128 cells (two
+// 64-cell V tiles) and each of its waves owns 32 cells over ALL n0 rows, so the
+// stream needs no LDS and no barrier and a workgroup streams once per launch:
+// at the headline size every cell workgroup is resident at once (one round, no
+// tile-to-tile transitions, whose startup and epilogue round trips under full
+// load left half the chip idle in the middle of the launch).
+// Lane (r, q) of a wave: cells 2r, 2r + 1 of the wave's 32 (one 16-byte load per
+// row), rows 4s + q of row step s; MFMA B operand = the cells' values, A operand =
+// L21c[row][r] (rows r < k of L21, z1 at r = k, zeros above), so MFMA output row
+// a is T (seeded with -psi_new) and row k is V_old^T z1. A ring of WS_S stages of
+// WS_U row steps keeps WS_S - 1 stages of loads in flight while one is consumed.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int vs_cell(int nt, int r) { return 2 * r + (nt & 1) + 32 * (nt >> 1); }
+constexpr int WS_CELLS = 32;            // cells per wave
+constexpr int WS_WG = 4 * WS_CELLS;     // cells per workgroup (two V tiles; ntiles_wg)
+// LDS of a cell workgroup (doubles): L22 (row-major) | z2 | new rows' (x, y) | cells' (x, y)
+constexpr int VS_LDS = KINC * KINC + KINC + 2 * KINC + 2 * WS_WG;
+static_assert(WS_WG == 2 * PBM, "a cell workgroup is two V tiles");
+#ifndef MFGP_WS_U
+#define MFGP_WS_U 2
+#endif
+#ifndef MFGP_WS_S
+#define MFGP_WS_S 4
+#endif
+constexpr int WS_U = MFGP_WS_U, WS_S = MFGP_WS_S;
+static_assert(WS_S >= 2, "a ring of at least two stages");
 
-template <bool MMA, bool GUARD>
-__device__ __forceinline__ void vs_round(const GLOBAL dv2* __restrict__ vb, const double* __restrict__ A,
-                                         const double* __restrict__ z, int64_t ld, int64_t n0, int64_t j0, int rr,
-                                         bool arow, int r, d4* acc, double* vs, double* ms) {
-  constexpr int U = 4;
-  dv2 v0[U], v1[U];
-  double zj[U], a[U];
+// psi of grid cell (gx, gy) against new training row g at (tx, ty): SF k, MF
+// [rho k_L | rho^2 k_L + k_H] by the row's fidelity (gp:426-429), in the
+// reference's operation order (as k_predict's psi)
+__device__ __forceinline__ double psi_new(const Hyp& h, int64_t NL, int64_t g, double gx, double gy, double tx,
+                                          double ty) {
+#pragma clang fp contract(off)
+  const double cLx = div_(gx, h.lL), cLy = div_(gy, h.lL);
+  const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
+  if (h.kind == 0) return se_scaled(cLx, cLy, tLx, tLy, h.sL);
+  if (g < NL) return h.rho * se_scaled(cLx, cLy, tLx, tLy, h.sL);
+  return h.rho2 * se_scaled(cLx, cLy, tLx, tLy, h.sL) +
+         se_scaled(div_(gx, h.lH), div_(gy, h.lH), div_(tx, h.lH), div_(ty, h.lH), h.sH);
+}
+
+// MODE 0: k = 0 (no MFMA; V^T z by VALU). MODE 1: MFMA on L21 read from A (row
+// stride ld, lanes r >= k masked), V^T z by VALU (k = KINC, or the compact rows
+// are not for these rows). MODE 2: MFMA on the compact rows, V^T z1 = row k.
+// Row steps per stage by mode: the rare modes carry z (and mask) registers and
+// take one step per stage to stay inside the occupancy's register budget.
+template <int MODE>
+constexpr int ws_u() { return MODE == 2 ? WS_U : (MODE == 1 ? 1 : 2); }
+template <int MODE>
+constexpr int ws_s() { return MODE == 2 ? WS_S : (MODE == 1 ? 4 : 3); }
+
+template <int MODE>
+struct WsStage {
+  dv2 v[ws_u<MODE>()];
+  double a[ws_u<MODE>()], z[ws_u<MODE>()];
+};
+
+template <int MODE>
+struct WsSrc {
+  const GLOBAL dv2* vb;       // this lane's cells, row 0
+  const GLOBAL double* ab;    // A operand, row 0 (MODE >= 1)
+  int64_t astride;
+  const GLOBAL double* zb;    // z, row 0 (MODE <= 1)
+  int64_t n0;
+};
+
+// Rows j0 + 4u (u < WS_U) of this lane; GUARD clamps rows >= n0 to row 0.
+template <int MODE, bool GUARD>
+__device__ __forceinline__ void ws_load(WsStage<MODE>& s, const WsSrc<MODE>& src, int64_t j0) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
+  for (int u = 0; u < ws_u<MODE>(); ++u) {
     const int64_t j = j0 + 4 * u;
-    const bool ok = !GUARD || j < n0;
-    const int64_t jj = ok ? j : 0;   // clamped, loads stay unconditional
-    // V is read once per update and is far larger than the Infinity Cache:
-    // non-temporal loads (measured 6.3 vs 5.7 TB/s for the whole kernel)
-    v0[u] = __builtin_nontemporal_load(vb + jj * (PBM / 2) + r);
-    v1[u] = __builtin_nontemporal_load(vb + jj * (PBM / 2) + 16 + r);
-    zj[u] = gp(z)[jj];
-    if (MMA) a[u] = gp(A)[jj * ld + n0 + rr];
-    if (GUARD && !ok) {
-      v0[u] = dv2{0.0, 0.0};
-      v1[u] = dv2{0.0, 0.0};
-      zj[u] = 0.0;
-    }
-    if (MMA) a[u] = (arow && ok) ? a[u] : 0.0;
+    const int64_t jj = (!GUARD || j < src.n0) ? j : 0;   // clamped, loads stay unconditional
+    // V is read once per update and is far larger than the Infinity Cache
+    s.v[u] = __builtin_nontemporal_load(src.vb + jj * (PBM / 2));
+#ifndef MFGP_DIAG_NOL21   // diagnostic build: no L21 loads (timing only)
+    if (MODE >= 1) s.a[u] = src.ab[jj * src.astride];
+#else
+    if (MODE >= 1) s.a[u] = 0.5;
+#endif
+    if (MODE <= 1) s.z[u] = src.zb[jj];
   }
+}
+
+// MODE 0 (the re-predict of an unchanged model) sums each cell's rows in four
+// classes, (row mod 64) / 16, combined as ((0 + 1) + (2 + 3)) at the end: the
+// order of k_predict's four waves, so a second predict() returns the same bits.
+template <int MODE, bool GUARD>
+__device__ __forceinline__ void ws_use(WsStage<MODE>& s, int64_t j0, int64_t n0, bool arow, d4* acc, double* vs,
+                                       double* ms) {
+  const int cls = MODE == 0 ? (int)((j0 & 63) >> 4) : 0;   // uniform: j0 = 4t + q
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    vs[0] += v0[u].x * v0[u].x;
-    vs[1] += v0[u].y * v0[u].y;
-    vs[2] += v1[u].x * v1[u].x;
-    vs[3] += v1[u].y * v1[u].y;
-    ms[0] += zj[u] * v0[u].x;
-    ms[1] += zj[u] * v0[u].y;
-    ms[2] += zj[u] * v1[u].x;
-    ms[3] += zj[u] * v1[u].y;
-    if (MMA) {
-      acc[0] = mfma(a[u], v0[u].x, acc[0]);
-      acc[1] = mfma(a[u], v0[u].y, acc[1]);
-      acc[2] = mfma(a[u], v1[u].x, acc[2]);
-      acc[3] = mfma(a[u], v1[u].y, acc[3]);
+  for (int u = 0; u < ws_u<MODE>(); ++u) {
+    if (GUARD && j0 + 4 * u >= n0) {
+      s.v[u] = dv2{0.0, 0.0};
+      s.a[u] = 0.0;
+      s.z[u] = 0.0;
+    }
+    if (MODE == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c == cls) {   // explicit fma: k_predict's contracted a += x * y
+          vs[2 * c] = __builtin_fma(s.v[u].x, s.v[u].x, vs[2 * c]);
+          vs[2 * c + 1] = __builtin_fma(s.v[u].y, s.v[u].y, vs[2 * c + 1]);
+          ms[2 * c] = __builtin_fma(s.v[u].x, s.z[u], ms[2 * c]);
+          ms[2 * c + 1] = __builtin_fma(s.v[u].y, s.z[u], ms[2 * c + 1]);
+        }
+      continue;
+    }
+    vs[0] += s.v[u].x * s.v[u].x;
+    vs[1] += s.v[u].y * s.v[u].y;
+    if (MODE <= 1) {
+      ms[0] += s.z[u] * s.v[u].x;
+      ms[1] += s.z[u] * s.v[u].y;
+    }
+    if (MODE >= 1) {
+      const double a = (MODE == 1 && !arow) ? 0.0 : s.a[u];
+#ifndef MFGP_DIAG_NOMMA   // diagnostic build: the stream without its MFMAs (timing only)
+      acc[0] = mfma(a, s.v[u].x, acc[0]);
+      acc[1] = mfma(a, s.v[u].y, acc[1]);
+#else
+      acc[0][0] += a;
+#endif
     }
   }
 }
 
-template <bool MMA>
-__device__ __forceinline__ void vs_rounds(const double* __restrict__ Vt, const double* __restrict__ A,
-                                          const double* __restrict__ z, int64_t ld, int64_t n0, int k, int w, int r,
-                                          int q, d4* acc, double* vs, double* ms) {
-  const GLOBAL dv2* vb = reinterpret_cast<const GLOBAL dv2*>(gp(Vt));
-  const int rr = MMA ? (r < k ? r : k - 1) : 0;
-  const bool arow = r < k;
-  const int64_t nfull = n0 >> 6;
-  for (int64_t R = 0; R < nfull; ++R)
-    vs_round<MMA, false>(vb, A, z, ld, n0, R * 64 + w * 16 + q, rr, arow, r, acc, vs, ms);
-  if (nfull * 64 < n0) vs_round<MMA, true>(vb, A, z, ld, n0, nfull * 64 + w * 16 + q, rr, arow, r, acc, vs, ms);
+// The epilogue's L22 record, fetched during the stream: the sync[2] flag is read
+// halfway (fused launches), the record itself at three quarters if the flag was
+// up, so the epilogue skips both round trips (the finish publishes long before).
+struct WsPrefetch {
+  const unsigned* flag;   // null: nothing to prefetch
+  unsigned epoch;
+  const double* rec;      // KINC * KINC + KINC doubles
+  unsigned fval;
+  double r0, r1;          // rec[tid], rec[tid + NT] (tid + NT < record size)
+  bool have;
+};
+
+__device__ __forceinline__ void ws_prefetch(WsPrefetch& pf, int64_t t, int64_t T) {
+  if (!pf.flag) return;
+  const int tid = threadIdx.x;
+  if (t == T / 2) pf.fval = __hip_atomic_load(pf.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == (3 * T) / 4) {
+    pf.have = pf.fval == pf.epoch;
+    if (pf.have) {
+      // plain loads: no line of the record is read in this launch before sync[2]
+      pf.r0 = pf.rec[tid];
+      pf.r1 = tid + NT < KINC * KINC + KINC ? pf.rec[tid + NT] : 0.0;
+    }
+  }
 }
 
-// LDS of one cell tile (doubles): red [4][16 * 64] | sred [2][4][64] | L22 (row-major) | z2
-// | new rows' coordinates [16][2] | the tile's cell coordinates [64][2]
-constexpr int VS_LDS = (NT / 64) * KINC * PBM + 2 * (NT / 64) * PBM + KINC * KINC + KINC + 2 * KINC + 2 * PBM;
-static_assert(VS_LDS >= FIN_LDS, "the fused kernel's LDS holds either step");
+// The whole row range [0, n0) of this lane's cells: full stages pipelined, the
+// ragged last stage guarded.
+template <int MODE>
+__device__ __forceinline__ void ws_stream(const WsSrc<MODE>& src, int q, bool arow, d4* acc, double* vs,
+                                          double* ms, WsPrefetch& pf) {
+  constexpr int64_t RS = 4 * ws_u<MODE>();   // rows per stage
+  constexpr int SS = ws_s<MODE>();           // stages in the ring
+  const int64_t n0 = src.n0;
+  const int64_t T = n0 / RS;         // full stages
+  WsStage<MODE> st[SS];
+#pragma unroll
+  for (int s = 0; s < SS - 1; ++s)
+    if (s < T) ws_load<MODE, false>(st[s], src, s * RS + q);
+  int64_t t = 0;
+  // steady state (sched_barrier keeps each stage's loads ahead of the use after it)
+  for (; t + 2 * SS - 1 <= T; t += SS) {
+#ifndef MFGP_WS_NOPRIO
+    // the workgroups of a CU stream at unequal rates (the memory pipe favours the
+    // oldest waves: 195 / 250 / 309 / 339 us for the four slots of a CU, measured),
+    // so priority falls as a wave advances and the waves of a CU finish closer
+    // together (3 stays with the producers and the finish, which the streams wait for)
+    if (t >= (2 * T) / 3) __builtin_amdgcn_s_setprio(0);
+    else if (t >= T / 3) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(2);
+#endif
+#pragma unroll
+    for (int s = 0; s < SS; ++s) ws_prefetch(pf, t + s, T);
+#pragma unroll
+    for (int s = 0; s < SS; ++s) {
+      ws_load<MODE, false>(st[(s + SS - 1) % SS], src, (t + s + SS - 1) * RS + q);
+      __builtin_amdgcn_sched_barrier(0);
+      ws_use<MODE, false>(st[s], (t + s) * RS + q, n0, arow, acc, vs, ms);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // drain: fewer than 2 SS - 1 full stages left
+#pragma unroll
+  for (int s = 0; s < 2 * SS - 2; ++s) {
+    if (t + s >= T) break;
+    if (t + s + SS - 1 < T) ws_load<MODE, false>(st[(s + SS - 1) % SS], src, (t + s + SS - 1) * RS + q);
+    ws_use<MODE, false>(st[s % SS], (t + s) * RS + q, n0, arow, acc, vs, ms);
+  }
+  if (T * RS < n0) {
+    const int64_t j0 = T * RS + q;
+    ws_load<MODE, true>(st[0], src, j0);
+    ws_use<MODE, true>(st[0], j0, n0, arow, acc, vs, ms);
+  }
+}
 
-// One cell tile of the one-pass predict. FUSED (inside k_inc_stream): L21 is
-// read from A once sync[1] is signalled, L22 / z2 (with ldx) once sync[2] is.
+// (max, first argmax) of var over one wave's 32 cells (slot = the wave's cell
+// group) into tred; the last group of the launch to arrive reduces all of them.
+// Write-through partials, a drain and a relaxed counter: no fence (a release
+// fence writes the whole L2 back).
+__device__ void var_argmax_group(const GPDesc& d, double bv, int64_t bi, int64_t slot, int64_t nslots) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  unsigned* cnt = reinterpret_cast<unsigned*>(d.tred);   // tred = [counter | (max, argmax) per group]
+  double* part = d.tred + 1;
+  unsigned old = 0;
+  if (lane == 0) {
+    __hip_atomic_store(part + 2 * slot, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 2 * slot + 1, (double)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  old = __shfl(old, 0);
+  if (old != (unsigned)(nslots - 1)) return;
+  bv = -__builtin_inf();
+  bi = INT64_MAX;
+  for (int64_t t = lane; t < nslots; t += 64)
+    argmax_pair(bv, bi, __hip_atomic_load(part + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                (int64_t)__hip_atomic_load(part + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  if (lane == 0) {
+    if (d.vmax) *d.vmax = bv;
+    if (d.vargmax) *d.vargmax = bi;
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Value of register `v` of lane `src` (all lanes take part).
+__device__ __forceinline__ double lane_get(double v, int src) { return __shfl(v, src); }
+
+// One 128-cell workgroup of the one-pass predict. FUSED (inside k_inc_stream): the
+// compact rows are read once sync[1] is signalled, L22 / z2 (L2-bypassing) once
+// sync[2] is; each wave polls for itself.
 template <bool FUSED>
-__device__ void vstream_tile(const GPDesc& d, int64_t tile, double* sm) {
+__device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
   const int64_t M = d.M;
-  const int64_t c0 = tile * PBM;
   const int64_t n0 = d.n0, N = d.N, ld = d.ld;
   const int k = (int)(N - n0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
-  double* __restrict__ Vt = d.V + tile * d.vld * PBM;
-  const double* __restrict__ A = d.A;
-  const double* __restrict__ z = d.zv;
-  double(*red)[KINC * PBM] = reinterpret_cast<double(*)[KINC * PBM]>(sm);   // per-wave partial L21 V_old
-  double(*sred)[NT / 64][PBM] = reinterpret_cast<double(*)[NT / 64][PBM]>(sm + (NT / 64) * KINC * PBM);
-  double* L22 = sm + (NT / 64) * KINC * PBM + 2 * (NT / 64) * PBM;         // L22 (row-major) | z2
-  double* Xn = L22 + KINC * KINC + KINC;                                     // new rows' (x, y)
-  double* Gc = Xn + 2 * KINC;                                                // cells' (x, y)
-  // the epilogue's inputs are loaded ahead of the stream: a workgroup that
-  // finishes its rows must not then sit out a memory round trip at full load
-  if (k > 0) {
-    if (tid < 2 * KINC) Xn[tid] = (tid / 2 < k) ? row_pt(d, n0 + tid / 2)[tid & 1] : 0.0;
-    if (tid >= NT - 2 * PBM) {
-      const int e = tid - (NT - 2 * PBM);
-      const int64_t cc = c0 + (e >> 1) < M ? c0 + (e >> 1) : M - 1;
-      Gc[e] = d.grid[2 * cc + (e & 1)];
+  const int64_t vt = 2 * wgt + (w >> 1);   // V tile of this wave
+  const int cw = WS_CELLS * (w & 1);        // first cell of this wave inside it
+  const int64_t cg = vt * PBM + cw;         // first grid cell of this wave
+  const bool live = vt * PBM < M;           // a ragged last workgroup may hold an empty V tile
+  double* __restrict__ Vt = d.V + vt * d.vld * PBM;
+  const Hyp& h = d.hp;
+  double* L22 = sm;                          // L22 (row-major) | z2
+  double* Xn = sm + KINC * KINC + KINC;      // new rows' (x, y)
+  double* Gc = Xn + 2 * KINC;                // the workgroup's cells' (x, y)
+  const int64_t c0 = cg + 2 * r;             // this lane's cells c0, c0 + 1
+  d4 acc[2];
+  acc[0] = d4{0.0, 0.0, 0.0, 0.0};
+  acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+  double vs[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, ms[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  const bool mma = k > 0;
+  const bool zrow = mma && k < KINC && d.l21c_ok;
+  for (int e = tid; !FUSED && mma && e < KINC * KINC + KINC; e += NT) {
+    // L22 | z2 (written by an earlier launch): the record of the append that
+    // wrote the compact rows, else A / zv
+    double v = 0.0;
+    if (e < KINC * KINC) {
+      const int ra = e / KINC, cb = e % KINC;
+      if (ra < k && cb <= ra) v = d.l21c_ok ? d.l22r[e] : d.A[(n0 + cb) * ld + n0 + ra];
+    } else if (e - KINC * KINC < k) {
+      v = d.l21c_ok ? d.l22r[e] : d.zv[n0 + e - KINC * KINC];
     }
-    if (!FUSED) {
-      if (tid < KINC * KINC) {
-        const int ra = tid / KINC, cb = tid % KINC;
-        L22[tid] = (ra < k && cb <= ra) ? A[(n0 + cb) * ld + n0 + ra] : 0.0;
-      }
-      if (tid < KINC) L22[KINC * KINC + tid] = tid < k ? z[n0 + tid] : 0.0;
+    L22[e] = v;
+  }
+  if (mma) {
+    // the psi_new inputs through LDS (one 16-byte load per thread: the producers'
+    // round trips at the start of the launch run beside this traffic)
+    if (tid < WS_WG) {
+      const int64_t cc = wgt * WS_WG + tid < M ? wgt * WS_WG + tid : M - 1;
+      reinterpret_cast<dv2*>(Gc)[tid] = *reinterpret_cast<const GLOBAL dv2*>(gp(d.grid) + 2 * cc);
+    } else if (tid < WS_WG + KINC) {
+      const int a = tid - WS_WG;
+      const double* p = row_pt(d, n0 + (a < k ? a : 0));
+      Xn[2 * a] = p[0];
+      Xn[2 * a + 1] = p[1];
     }
+    __syncthreads();
   }
-  if (FUSED && tile == 0) FSTAMP(33);
-  if (FUSED && k > 0) wait_flag(d, d.sync + 1, d.epoch);
-  if (FUSED && tile == 0) FSTAMP(34);
-  d4 acc[4];
+  if (live && mma) {
+    {
+      // T = psi_new^T - L21 V_old: the accumulators start at -psi_new (MFMA output
+      // row q + 4v of lane (r, q), cells c0 + x), so the epilogue has no exps left
+      const int e0 = (int)(c0 - wgt * WS_WG);
+      const double g0x = Gc[2 * e0], g0y = Gc[2 * e0 + 1], g1x = Gc[2 * e0 + 2], g1y = Gc[2 * e0 + 3];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) acc[nt] = d4{0.0, 0.0, 0.0, 0.0};
-  double vs[4] = {0.0, 0.0, 0.0, 0.0}, ms[4] = {0.0, 0.0, 0.0, 0.0};
-  // rounds of 64 rows: wave w streams rows 16w.. (four 4-row MFMA steps, 8 KB);
-  // full rounds without guards, then one guarded tail round
-  if (k > 0) vs_rounds<true>(Vt, A, z, ld, n0, k, w, r, q, acc, vs, ms);
-  else vs_rounds<false>(Vt, A, z, ld, n0, k, w, r, q, acc, vs, ms);
-  if (k > 0) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) red[w][(q + 4 * v) * PBM + vs_cell(nt, r)] = acc[nt][v];
-  }
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    vs[nt] += __shfl_xor(vs[nt], 16);
-    vs[nt] += __shfl_xor(vs[nt], 32);
-    ms[nt] += __shfl_xor(ms[nt], 16);
-    ms[nt] += __shfl_xor(ms[nt], 32);
-  }
-  if (q == 0) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      sred[0][w][vs_cell(nt, r)] = vs[nt];
-      sred[1][w][vs_cell(nt, r)] = ms[nt];
-    }
-  }
-  if (FUSED && tile == 0) FSTAMP(35);
-  if (FUSED && k > 0) {
-    wait_flag(d, d.sync + 2, d.epoch);
-    if (tid < KINC * KINC) {
-      const int ra = tid / KINC, cb = tid % KINC;
-      L22[tid] = (ra < k && cb <= ra) ? ldx<true>(&A[(n0 + cb) * ld + n0 + ra]) : 0.0;
-    }
-    if (tid < KINC) L22[KINC * KINC + tid] = tid < k ? ldx<true>(&z[n0 + tid]) : 0.0;
-  }
-  if (FUSED && tile == 0) FSTAMP(36);
-  __syncthreads();
-  if (tid < PBM) {
-    const int e = tid;
-    const int64_t c = c0 + e;
-    double vsum = (sred[0][0][e] + sred[0][1][e]) + (sred[0][2][e] + sred[0][3][e]);
-    double msum = (sred[1][0][e] + sred[1][1][e]) + (sred[1][2][e] + sred[1][3][e]);
-    const Hyp& h = d.hp;
-    if (k > 0) {
-      const double gx = Gc[2 * e], gy = Gc[2 * e + 1];
-      const double cLx = div_(gx, h.lL), cLy = div_(gy, h.lL);
-      const double cHx = div_(gx, h.lH), cHy = div_(gy, h.lH);
-      double vn[KINC];
-#pragma unroll
-      for (int a = 0; a < KINC; ++a) {
-        vn[a] = 0.0;
+      for (int v = 0; v < 4; ++v) {
+        const int a = q + 4 * v;
+#ifdef MFGP_DIAG_NOEPI   // diagnostic build: no psi_new seeds (timing only)
+        if (false) {
+#else
         if (a < k) {
-          const int64_t g = n0 + a;
+#endif
           const double tx = Xn[2 * a], ty = Xn[2 * a + 1];
-          const double tLx = div_(tx, h.lL), tLy = div_(ty, h.lL);
-          double psi;
-          if (h.kind == 0) {
-            psi = se_scaled(cLx, cLy, tLx, tLy, h.sL);
-          } else if (g < d.NL) {
-            psi = h.rho * se_scaled(cLx, cLy, tLx, tLy, h.sL);
-          } else {
-#pragma clang fp contract(off)
-            psi = h.rho2 * se_scaled(cLx, cLy, tLx, tLy, h.sL) +
-                  se_scaled(cHx, cHy, div_(tx, h.lH), div_(ty, h.lH), h.sH);
-          }
-          const int ei = a * PBM + e;
-          double t = psi - ((red[0][ei] + red[1][ei]) + (red[2][ei] + red[3][ei]));
-#pragma unroll
-          for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
-          vn[a] = t / L22[a * KINC + a];
-          vsum += vn[a] * vn[a];
-          msum += vn[a] * L22[KINC * KINC + a];
-          gp(Vt)[(n0 + a) * PBM + e] = vn[a];
+          acc[0][v] = -psi_new(h, d.NL, n0 + a, g0x, g0y, tx, ty);
+          acc[1][v] = -psi_new(h, d.NL, n0 + a, g1x, g1y, tx, ty);
         }
       }
     }
-    const double vc = h.kss - vsum;
-    if (c < M) {
-      d.mu[c] = msum + h.meanH;
-      d.var[c] = vc;
-    }
-    if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M, tile);
   }
-  if (FUSED) FSTAMP(37);   // latest tile end
+  if (FUSED && mma) wait_flag(d, d.sync + 1, d.epoch);   // the compact rows of this append (all waves)
+  WsPrefetch pf{(FUSED && mma) ? d.sync + 2 : nullptr, d.epoch, d.l22r, 0u, 0.0, 0.0, false};
+  if (FUSED) WTRACE(1);
+  if (live) {
+    const GLOBAL dv2* vb = reinterpret_cast<const GLOBAL dv2*>(gp(Vt)) + (cw >> 1) + r;
+    if (zrow) {
+      const WsSrc<2> src{vb, gp(d.l21c) + r, KINC, nullptr, n0};
+      ws_stream<2>(src, q, true, acc, vs, ms, pf);
+    } else if (mma) {
+      const WsSrc<1> src{vb, gp(d.A) + n0 + (r < k ? r : 0), ld, gp(d.zv), n0};
+      ws_stream<1>(src, q, r < k, acc, vs, ms, pf);
+    } else {
+      const WsSrc<0> src{vb, nullptr, 0, gp(d.zv), n0};
+      ws_stream<0>(src, q, false, acc, vs, ms, pf);
+    }
+  }
+  // colsums over the lanes' row residues q (and, for k = 0, the four row classes)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if (e >= 2 && mma) break;
+    vs[e] += __shfl_xor(vs[e], 16);
+    vs[e] += __shfl_xor(vs[e], 32);
+    ms[e] += __shfl_xor(ms[e], 16);
+    ms[e] += __shfl_xor(ms[e], 32);
+  }
+  if (!mma) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      vs[x] = (vs[x] + vs[2 + x]) + (vs[4 + x] + vs[6 + x]);
+      ms[x] = (ms[x] + ms[2 + x]) + (ms[4 + x] + ms[6 + x]);
+    }
+  }
+  if (FUSED) WTRACE(2);
+  // L22 / z2 (sync[2]): from the stream's prefetch if every wave had it, else now
+  const bool pre = (FUSED && mma) ? __syncthreads_and(pf.have) != 0 : false;
+  if (pre) {
+    for (int e = tid, i = 0; e < KINC * KINC + KINC; e += NT, ++i) {
+      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+      L22[e] = use ? (i == 0 ? pf.r0 : pf.r1) : 0.0;
+    }
+  }
+  if (FUSED && mma && !pre) {
+    // the workgroup's waves end their streams together
+    if (tid == 0) {
+      int it = 0;
+      while (__hip_atomic_load(d.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != d.epoch) {
+        __builtin_amdgcn_s_sleep(MFGP_SPIN_SLEEP);
+        if (++it == (1 << 22)) {
+          atomicMin(d.status, SYNC_FAIL);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    // plain loads: no line of the record is read in this launch before sync[2]
+    // (an L2 miss for the first workgroup of an XCD, hits for the others)
+    for (int e = tid; e < KINC * KINC + KINC; e += NT) {
+      const double v = d.l22r[e];
+      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+      L22[e] = use ? v : 0.0;
+    }
+  }
+  __syncthreads();
+  if (FUSED) WTRACE(3);
+  // epilogue: lane (r, x) with x = q < 2 finishes cell c0 + x. Row a of T for that
+  // cell sits in acc[x][a / 4] of lane (r, a % 4).
+  const int x = q & 1;
+  const int64_t c = c0 + x;
+  double vsum = x ? vs[1] : vs[0];
+  double msum = x ? ms[1] : ms[0];
+  if (mma) {
+    if (zrow) {
+      const double m0 = lane_get(acc[0][k / 4], r + 16 * (k % 4));
+      const double m1 = lane_get(acc[1][k / 4], r + 16 * (k % 4));
+      msum += x ? m1 : m0;
+    }
+    double vn[KINC];
+#pragma unroll
+    for (int a = 0; a < KINC; ++a) {
+      vn[a] = 0.0;
+      if (a < k) {
+        const double t0 = lane_get(acc[0][a / 4], r + 16 * (a % 4));
+        const double t1 = lane_get(acc[1][a / 4], r + 16 * (a % 4));
+        double t = -(x ? t1 : t0);   // psi_new - L21 V_old
+#pragma unroll
+        for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+        vn[a] = t / L22[a * KINC + a];
+        vsum += vn[a] * vn[a];
+        msum += vn[a] * L22[KINC * KINC + a];
+      }
+    }
+#ifdef MFGP_DIAG_NOSTORE   // diagnostic build: no V_new stores (timing only)
+    if (false) {
+#else
+    if (live && q < 2 && c < M) {
+#endif
+#pragma unroll
+      for (int a = 0; a < KINC; ++a)
+        if (a < k) {
+#ifdef MFGP_WS_NTSTORE
+          __builtin_nontemporal_store(vn[a], gp(Vt) + (n0 + a) * PBM + cw + 2 * r + x);
+#else
+          gp(Vt)[(n0 + a) * PBM + cw + 2 * r + x] = vn[a];
+#endif
+        }
+    }
+  }
+  const double vc = h.kss - vsum;
+  const bool valid = live && q < 2 && c < M;
+  if (valid) {
+    d.mu[c] = msum + h.meanH;
+    d.var[c] = vc;
+  }
+  if ((d.vmax || d.vargmax) && cg < M)
+    var_argmax_group(d, valid ? vc : -__builtin_inf(), valid ? c : INT64_MAX, cg / WS_CELLS,
+                     (M + WS_CELLS - 1) / WS_CELLS);
+  if (FUSED) WTRACE(4);
 }
 
-__global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_vstream(
+    const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
-  if ((int64_t)blockIdx.x * PBM >= d.M) return;
+  if ((int64_t)blockIdx.x * WS_WG >= d.M) return;
   if (d.gate && *d.gate == 0) return;
   __shared__ double sm[VS_LDS];
-  vstream_tile<false>(d, blockIdx.x, sm);
+  vstream_wg<false>(d, blockIdx.x, sm);
 }
 
 // ---------------------------------------------------------------------------
@@ -1497,29 +1763,35 @@ __global__ __launch_bounds__(NT) void k_vstream(const GPDesc* __restrict__ descs
 //               solves L21, then sync[2] once L22 / z2 are stored) and resets
 //               sync[0] for the next launch.
 // With d.tiles the same launch also runs the one-pass predict: roles >= nprod
-// stream the cell tiles (vstream_tile<true>), waiting for sync[1] before the
-// first L21 load and for sync[2] before the L22 solve of the epilogue. x = GP,
+// stream the 128-cell workgroups (vstream_wg<true>), waiting for sync[1] before
+// the first L21 load and for sync[2] before the L22 solve of the epilogue. x = GP,
 // so the linear dispatch order is every GP's producer 0, then producer 1, ...,
-// then the cell tiles round-robin over the GPs: producers are dispatched before
-// any tile that waits for them and are therefore resident (no deadlock); the
-// waits are bounded anyway (wait_flag). The flags hold the launch's epoch (host
-// counter, never 0), so they need no reset. Without tiles nothing waits.
+// then the cell workgroups round-robin over the GPs: producers are dispatched
+// before any workgroup that waits for them and are therefore resident (no
+// deadlock); the waits are bounded anyway. The flags hold the launch's epoch
+// (host counter, never 0), so they need no reset. Without tiles nothing waits.
+// Five workgroups per CU (26.5 KB of LDS, <= 102 VGPRs): at the headline size
+// (8 GPs: 128 producers + 1024 cell workgroups) every workgroup is resident.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_inc_stream(const GPDesc* __restrict__ descs) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream(
+    const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.x];
   const int k = (int)(d.N - d.n0);
   if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
   if (d.gate && *d.gate == 0) return;
-  __shared__ double sm[VS_LDS];
+  static_assert(VS_LDS <= FIN_LDS, "one LDS image serves every role");
+  __shared__ double sm[FIN_LDS];
+  WTRACE(0);
   const int64_t np = d.nprod, role = blockIdx.y;
   if (role >= np) {
-    const int64_t tile = role - np;
-    if (d.tiles && tile * PBM < d.M) vstream_tile<true>(d, tile, sm);
+    const int64_t wgt = role - np;
+    if (d.tiles && wgt * WS_WG < d.M) vstream_wg<true>(d, wgt, sm);
     return;
   }
   __shared__ int cell[KINC];
   __shared__ unsigned last;
   if (role == 0) FSTAMP(30);
+  __builtin_amdgcn_s_setprio(3);   // producers and the finish before the cell streams
   const bool gathered = inc_produce(d, role, FCH, cell, reinterpret_cast<double(*)[ISZ]>(sm));
   FSTAMP(40);   // latest producer done storing (before the drain)
   drain_stores();
@@ -1534,7 +1806,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   }
   FSTAMP(31);   // latest producer arrival
   __syncthreads();
-  if (last) inc_finish<true>(d, sm, FCH);   // the hand-off accesses: tiles may stream concurrently
+  WTRACE(1);
+  if (last) inc_finish<true>(d, sm, FCH);
+  if (last) WTRACE(2);   // the hand-off accesses: tiles may stream concurrently
+  WTRACE(4);
 }
 
 // One iteration of compute_sample_points (simulator.py:344-370) on the device:

@@ -2,19 +2,20 @@
 from a -DMFGP_STAMPS build named by argv[1] (default build_diag/libmfgp_stamps.so)."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MFGP_LIB"] = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build_diag", "libmfgp_stamps.so")
+os.environ["MFGP_LIB"] = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build", "libmfgp_stamps.so")
+BACK_TO_BACK = "--b2b" in sys.argv   # launches back to back (stamps: max over launches = the last one)
 sys.path.insert(0, ROOT)
 import numpy as np
 import torch
 from mfgp_coverage_amd import _lib, synthetic
 
-B, G, NL, NH, k, T = 8, 128, 1024, 1024, 8, 6
+B, G, NL, NH, k, T = 8, 128, 1024, 1024, 8, (24 if BACK_TO_BACK else 6)
 NH0 = NH - k
 M = G * G
 hyp = synthetic.HYP["australia8_mf"]
 wls = [synthetic.Workload(G, NL, NH0, k, T, seed=s) for s in range(B)]
 dev = torch.device("cuda", 0)
-st = torch.zeros(64, dtype=torch.int64, device=dev)
+st = torch.zeros(64 + 8 * 8 * (16 + 256) + 64, dtype=torch.int64, device=dev)   # + per-WG traces
 L = _lib.lib()
 L.mfgp_debug_set_stamps.argtypes = [ctypes.c_void_p]
 assert L.mfgp_debug_set_stamps(ctypes.c_void_p(st.data_ptr())) == 0
@@ -33,12 +34,18 @@ vmax = torch.empty(T, B, dtype=torch.float64, device=dev)
 for s in range(T):
     for m in models:
         m.truncate(NH0)
-    torch.cuda.synchronize()
-    st.zero_()
-    torch.cuda.synchronize()
+    if not BACK_TO_BACK or s == 0:
+        torch.cuda.synchronize()
+        st.zero_()
+        torch.cuda.synchronize()
     _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
-                              vmax_ptr=vmax[s].data_ptr())
-    torch.cuda.synchronize()
+                              vmax_ptr=vmax[s].data_ptr(), asynchronous=BACK_TO_BACK)
+    if not BACK_TO_BACK:
+        torch.cuda.synchronize()
+try:
+    ctx.synchronize()
+except Exception as e:   # diagnostic builds that compute garbage on purpose
+    print("(synchronize:", type(e).__name__, ")")
 v = st.cpu().numpy()
 t0 = v[30]
 names = {30: "producer 0 start", 38: "producers: cells found", 39: "producers: gathered", 40: "producers: partials stored",
