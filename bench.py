@@ -89,6 +89,23 @@ def pmc_traffic(kernel="k_predict"):
     return None, None
 
 
+def pmc_mfma(kernel):
+    """MFMA utilisation of `kernel` from the newest committed rocprofv3 summary
+    (profiles/<round>_mfma_util.csv: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per
+    XCD x 1024 SIMDs), with the shader clock it implies)."""
+    import glob
+    import csv
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_mfma_util.csv")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Name"]:
+                return {"mfma_util": float(row["mfma_util"]), "clock_ghz": float(row["clock_ghz"]),
+                        "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def cpu_baseline(wl, hyp, s, NL, NH0, k, reps=3):
     """Time the oracle on one seed's update (same inputs as step s)."""
     from oracle import gp_oracle as O
@@ -302,6 +319,7 @@ def main():
                     "bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / PEAK_F64_TFLOPS, "traffic": ftraffic,
                     "kernel": "k_predict", "flops_per_launch": flops, "avg_launch_ms": avg_ms,
+                    "pmc": pmc_mfma("k_predict") if default_cfg else None,
                 },
                 "host_enqueue_ms_per_step": full["host_ms"],
                 "breakdown_ms_per_step": full["breakdown"],

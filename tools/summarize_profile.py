@@ -4,7 +4,10 @@ usage: python tools/summarize_profile.py gpurun_out/prof_r01 r01
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, names shortened) and
 profiles/<tag>_hbm_traffic.csv (per-kernel mean FETCH_SIZE / WRITE_SIZE per
 dispatch in KB as reported, plus bytes with the gfx950 FETCH_SIZE x2 correction
-of MI355X_MICROARCH.md section HBM).
+of MI355X_MICROARCH.md section HBM), and profiles/<tag>_mfma_util.csv (per-kernel
+MfmaUtil = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD x 1024 SIMDs), the
+rocprofv3 derived-counter formula; the CSV's GRBM_GUI_ACTIVE is the sum over the 8
+XCDs, so it is divided by 8, and the clock it implies).
 """
 import os
 import re
@@ -42,6 +45,21 @@ def main(d, tag):
             t["write_bytes"] = t["WRITE_SIZE"] * 1024
         t.to_csv(f"profiles/{tag}_hbm_traffic.csv", index=False)
         print(t.to_string())
+    p = os.path.join(d, "mfma", "bench_counter_collection.csv")
+    if os.path.exists(p):
+        c = pd.read_csv(p)
+        c["Name"] = c["Kernel_Name"].map(short)
+        g = c.groupby(["Name", "Dispatch_Id", "Counter_Name"]).Counter_Value.sum().unstack().reset_index()
+        tr = pd.read_csv(os.path.join(d, "mfma", "bench_kernel_trace.csv"))
+        tr["dur_ns"] = tr.End_Timestamp - tr.Start_Timestamp
+        g = g.merge(tr[["Dispatch_Id", "dur_ns"]], on="Dispatch_Id")
+        g["grbm_per_xcd"] = g.GRBM_GUI_ACTIVE / 8
+        g["mfma_util"] = g.SQ_VALU_MFMA_BUSY_CYCLES / (g.grbm_per_xcd * 1024)
+        g["clock_ghz"] = g.grbm_per_xcd / g.dur_ns
+        m = g.groupby("Name")[["mfma_util", "clock_ghz", "SQ_VALU_MFMA_BUSY_CYCLES", "grbm_per_xcd", "dur_ns"]].median()
+        m = m.reset_index()
+        m.to_csv(f"profiles/{tag}_mfma_util.csv", index=False)
+        print(m.to_string())
     print(s.head(8).to_string())
 
 
