@@ -898,20 +898,24 @@ __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, boo
 // wave). Lane (r, q) holds L21[r][j], j = 4s + q, eight 4-row steps in flight per
 // wave. With `cell`, L21[r][.] is gathered from the V column of the grid cell and
 // written to row n0 + r of A; otherwise it is read from there.
-template <int NW, bool XW = false>
+template <int NW, bool XW, bool FROMV>
 __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo, int64_t j_hi,
                                   double (*red)[ISZ]) {
+  // descriptor fields in registers: the write-through stores below would make the
+  // compiler reload them (and drain every load) before each store
   const int64_t n0 = d.n0, ld = d.ld;
   const int k = (int)(d.N - n0);
+  double* const A = d.A;
+  double* const l21c = d.l21c;
+  const double* const zv = d.zv;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
   d4 sacc = {0.0, 0.0, 0.0, 0.0}, uacc = {0.0, 0.0, 0.0, 0.0};
   constexpr int IU = 8;
-  const bool from_v = cell != nullptr;
-  const int cr = (from_v && r < k) ? cell[r] : 0;
-  const double* src = from_v ? d.V + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : d.A + n0 + (r < k ? r : 0);
-  const int64_t sstride = from_v ? PBM : ld;
+  const int cr = (FROMV && r < k) ? cell[r] : 0;
+  const double* src = FROMV ? d.V + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : A + n0 + (r < k ? r : 0);
+  const int64_t sstride = FROMV ? PBM : ld;
   const int64_t s_lo = j_lo >> 2, s_hi = (j_hi + 3) >> 2;   // j_lo is a multiple of 4
   for (int64_t s0 = s_lo + w; s0 < s_hi; s0 += NW * IU) {
     double a[IU], zz[IU];
@@ -921,21 +925,22 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
       const bool ok = j < j_hi;
       const int64_t jj = ok ? j : j_lo;
 #ifndef MFGP_DIAG_NOGATHER   // diagnostic build: no V-column loads (timing only)
-      a[u] = from_v ? gp(src)[jj * sstride] : ldx<XW>(src + jj * sstride);
+      a[u] = FROMV ? gp(src)[jj * sstride] : ldx<XW>(src + jj * sstride);
 #else
-      a[u] = from_v ? 1.0 : ldx<XW>(src + jj * sstride);
+      a[u] = FROMV ? 1.0 : ldx<XW>(src + jj * sstride);
 #endif
-      zz[u] = gp(d.zv)[jj];
-      a[u] = (ok && r < k) ? a[u] : 0.0;
-      zz[u] = ok ? zz[u] : 0.0;
+      zz[u] = gp(zv)[jj];
     }
 #pragma unroll
     for (int u = 0; u < IU; ++u) {
       const int64_t j = 4 * (s0 + NW * u) + q;
-      if (from_v && r < k && j < j_hi) stx<XW>(&d.A[j * ld + n0 + r], a[u]);
+      const bool ok = j < j_hi;
+      a[u] = (ok && r < k) ? a[u] : 0.0;
+      zz[u] = ok ? zz[u] : 0.0;
+      if (FROMV && r < k && ok) stx<XW>(&A[j * ld + n0 + r], a[u]);
       // compact rows for the cell tiles: L21 | z1 at row k | zeros
 #ifndef MFGP_DIAG_NOPSTORE   // diagnostic build: no compact-row stores (timing only)
-      if (j < j_hi) stx<XW>(&d.l21c[j * KINC + r], r < k ? a[u] : (r == k ? zz[u] : 0.0));
+      if (ok) stx<XW>(&l21c[j * KINC + r], r < k ? a[u] : (r == k ? zz[u] : 0.0));
 #endif
       sacc = mfma(a[u], a[u], sacc);
       uacc = mfma(a[u], zz[u], uacc);
@@ -1007,7 +1012,7 @@ __device__ int lattice_cell(const GPDesc& d, double px, double py) {
 // [chunk * ch, +ch) and store the chunk's partials. Returns false when L21 is not
 // a set of V columns (off the grid / no resident V): the finish solves for it.
 // All NTHR threads take part; `cell` and `red` are in LDS.
-__device__ __noinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell, double (*red)[ISZ]) {
+__device__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell, double (*red)[ISZ]) {
   constexpr int NTHR = NT;
   constexpr bool XW = true;
   const int64_t n0 = d.n0, N = d.N;
@@ -1060,7 +1065,7 @@ __device__ __noinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t
   if (!use_v || j_lo >= n0) return use_v;   // off the grid: the finish solves
   inc_init_blocks<XW>(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
   __syncthreads();
-  inc_schur_partial<NTHR / 64, XW>(d, cell, j_lo, j_hi, red);
+  inc_schur_partial<NTHR / 64, XW, true>(d, cell, j_lo, j_hi, red);
   __syncthreads();
   if (XW) FSTAMP(39);   // latest producer past its gather
   double* __restrict__ part = d.iscr + ISC0 + chunk * ISZ;
@@ -1088,7 +1093,7 @@ constexpr int LBW = 16;   // Linv_OO columns staged per pass (63 rows x 16 = 100
 // this step solved it) and `sync[2]` once L22 / z2 are, with the hand-off
 // accesses of ldx / stx.
 template <bool FUSED>
-__device__ __noinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch) {
+__device__ void inc_finish(const GPDesc& d, double* sm, int64_t ch) {
   const int64_t n0 = d.n0, N = d.N, ld = d.ld, NL = d.NL;
   const int k = (int)(N - n0);
   const Hyp& h = d.hf;
@@ -1170,7 +1175,7 @@ __device__ __noinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch)
       if (FUSED) drain_stores();
       __syncthreads();   // W_I visible to every wave; Ts free
     }
-    inc_schur_partial<NT / 64, FUSED>(d, nullptr, 0, n0, red);
+    inc_schur_partial<NT / 64, FUSED, false>(d, nullptr, 0, n0, red);
     if (FUSED) drain_stores();   // the compact rows, before sync[1]
     __syncthreads();
     for (int e = tid; e < ISZ; e += NT) ssum[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);

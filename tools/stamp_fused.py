@@ -4,6 +4,7 @@ import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["MFGP_LIB"] = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build", "libmfgp_stamps.so")
 BACK_TO_BACK = "--b2b" in sys.argv   # launches back to back (stamps: max over launches = the last one)
+UNFUSED = "--unfused" in sys.argv     # the append alone (producers + finish), then k_vstream
 sys.path.insert(0, ROOT)
 import numpy as np
 import torch
@@ -22,6 +23,8 @@ assert L.mfgp_debug_set_stamps(ctypes.c_void_p(st.data_ptr())) == 0
 Xnew = torch.from_numpy(np.ascontiguousarray(np.stack([w.Xnew for w in wls], 1).reshape(T, B * k, 2))).to(dev)
 ynew = torch.from_numpy(np.ascontiguousarray(np.stack([w.ynew for w in wls], 1).reshape(T, B * k))).to(dev)
 ctx = _lib.context()
+if UNFUSED:
+    ctx.set_fused(False)
 models = []
 for wl in wls:
     m = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
