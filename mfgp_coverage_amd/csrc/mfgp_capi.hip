@@ -77,6 +77,7 @@ struct mfgp_ctx {
   // refactor and recompute V from scratch, as the reference does
   bool incremental = true;
   bool fused = true;          // bordered append + one-pass predict in one launch (k_inc_stream)
+  int ncu = 256;              // compute units (hipDeviceProp multiProcessorCount)
 };
 
 struct mfgp_model {
@@ -359,6 +360,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.nprod = 0;
   d.tiles = 0;
   d.l21c_ok = 0;
+  d.rsplit = 1;
   d.ld = m->ld;
   d.N = m->NL + m->NH;
   d.NL = m->NL;
@@ -411,7 +413,7 @@ int enqueue_inc_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
 
 int enqueue_vstream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_ct = 0;
-  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_wg(hd[i].M));
+  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_wg(hd[i].M, hd[i].rsplit));
   if (max_ct == 0) return MFGP_OK;
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
@@ -459,12 +461,22 @@ int ensure_sync(mfgp_model* m) {
 // Bordered appends and their one-pass predicts in one k_inc_stream launch.
 int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_blocks = 0;
-  for (int i = 0; i < count; ++i) max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_wg(hd[i].M));
+  for (int i = 0; i < count; ++i) max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_wg(hd[i].M, hd[i].rsplit));
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
   HIP_TRY(launch_inc_stream(dd, count, max_blocks, c->stream));
   return ev_end(c, ev);
+}
+
+// Row splits of the one-pass predict for a launch over these descriptors: 128-cell
+// workgroups while they fill the chip (~4 per CU), else 64 or 32 cells with the
+// rows split 2 or 4 ways (the drop-in simulator predicts one GP at a time).
+void set_rsplit(const mfgp_ctx* c, GPDesc* hd, int count) {
+  int64_t w1 = 0;
+  for (int i = 0; i < count; ++i) w1 += ntiles_wg(hd[i].M);
+  const int R = (w1 >= 3 * c->ncu) ? 1 : (2 * w1 >= 3 * c->ncu ? 2 : 4);
+  for (int i = 0; i < count; ++i) hd[i].rsplit = R;
 }
 
 bool hyp_same(const mfgp_model* m) {
@@ -615,6 +627,11 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   mfgp_ctx* c = new mfgp_ctx();
   c->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+      c->ncu = ncu;
+  }
   c->stream = c->own;
   HIP_TRY(hipHostMalloc(&c->h_ring, sizeof(GPDesc) * RING * MAXB, hipHostMallocDefault));
   HIP_TRY(hipMalloc(&c->d_ring, sizeof(GPDesc) * RING * MAXB));
@@ -936,6 +953,7 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   hd[0].var = hd[0].mu + m->M;
   const bool vst = can_vstream(m);
   set_vstream_rows(hd[0], m);
+  set_rsplit(c, hd, 1);
   const GPDesc* dd = nullptr;
   if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
   if ((rc = vst ? enqueue_vstream(c, dd, hd, 1) : enqueue_predict(c, dd, hd, 1))) return rc;
@@ -1103,6 +1121,10 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.tiles = 1;
       }
     }
+    if (nv > 0) {
+      set_rsplit(c, hd + nb, nv);
+      for (int i = 0; fuse && i < ninc; ++i) hd[i].rsplit = hd[nb].rsplit;
+    }
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
     if (do_factor) {
@@ -1198,14 +1220,16 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
       pd.gate = gate;
       t->v_n = t->NL + t->NH;
     }
+    set_rsplit(c, hd + 1, 1);
+    for (int64_t i = 0; i < 2 * C; ++i) hd[i].rsplit = hd[1].rsplit;
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, (int)(2 * C), &dd))) return fail(rc);
     for (int64_t it = 0; it < C; ++it) {
       const bool ok = hipSuccess == launch_choi_select(dd + 2 * it, threshold, pts, max_points, c->stream) &&
-                      (c->fused ? hipSuccess == launch_inc_stream(dd + 2 * it, 1, hd[2 * it].nprod + ntiles_wg(M),
+                      (c->fused ? hipSuccess == launch_inc_stream(dd + 2 * it, 1, hd[2 * it].nprod + ntiles_wg(M, hd[2 * it].rsplit),
                                                                    c->stream)
                                 : (hipSuccess == launch_inc_factor(dd + 2 * it, 1, hd[2 * it].nprod, c->stream) &&
-                                   hipSuccess == launch_vstream(dd + 2 * it + 1, 1, ntiles_wg(M), c->stream)));
+                                   hipSuccess == launch_vstream(dd + 2 * it + 1, 1, ntiles_wg(M, hd[2 * it + 1].rsplit), c->stream)));
       if (!ok) return fail(set_err(MFGP_ERR_DEVICE, "sample_points: launch failed"));
     }
     if ((rc = release_slot(c, slot))) return fail(rc);

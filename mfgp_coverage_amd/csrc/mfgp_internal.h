@@ -83,6 +83,7 @@ struct GPDesc {
   int nprod;           // k_inc_stream: producer workgroups ahead of the cell tiles
   int tiles;           // k_inc_stream: 1 = the launch also streams the cell tiles (one-pass predict)
   int l21c_ok;         // one-pass predict: l21c holds the rows [n0, N) bordered onto V's n0 rows
+  int rsplit;          // one-pass predict: row splits per cell group (1, 2, 4; 128 / rsplit cells per workgroup)
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -90,8 +91,11 @@ struct GPDesc {
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
 inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
 inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1) / PBM; }
-// one-pass predict workgroups: 128 cells (two V tiles), 32 per wave
-inline __host__ __device__ int64_t ntiles_wg(int64_t M) { return (M + 2 * PBM - 1) / (2 * PBM); }
+// one-pass predict workgroups: 128 / rsplit cells (32 per wave and row split)
+inline __host__ __device__ int64_t ntiles_wg(int64_t M, int rsplit = 1) {
+  const int64_t c = 2 * PBM / rsplit;
+  return (M + c - 1) / c;
+}
 inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1) / PRB; }
 
 // Launchers (mfgp_kernels.hip). `d` points to `count` descriptors in device memory.

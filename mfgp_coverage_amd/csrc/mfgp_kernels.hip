@@ -1334,8 +1334,9 @@ __device__ void inc_finish(const GPDesc& d, double* sm, int64_t ch) {
 // ---------------------------------------------------------------------------
 constexpr int WS_CELLS = 32;            // cells per wave
 constexpr int WS_WG = 4 * WS_CELLS;     // cells per workgroup (two V tiles; ntiles_wg)
-// LDS of a cell workgroup (doubles): L22 (row-major) | z2 | new rows' (x, y) | cells' (x, y)
-constexpr int VS_LDS = KINC * KINC + KINC + 2 * KINC + 2 * WS_WG;
+// LDS of a cell workgroup (doubles): L22 (row-major) | z2 | new rows' (x, y) |
+// cells' (x, y) | the row splits' partials (R = 4: 3 slots of 12 x 64)
+constexpr int VS_LDS = KINC * KINC + KINC + 2 * KINC + 2 * WS_WG + 3 * 12 * 64;
 static_assert(WS_WG == 2 * PBM, "a cell workgroup is two V tiles");
 #ifndef MFGP_WS_U
 #define MFGP_WS_U 2
@@ -1382,7 +1383,8 @@ struct WsSrc {
   const GLOBAL double* ab;    // A operand, row 0 (MODE >= 1)
   int64_t astride;
   const GLOBAL double* zb;    // z, row 0 (MODE <= 1)
-  int64_t n0;
+  int64_t n0;                 // end of this wave's row range
+  int64_t j_lo;               // start of it (a multiple of 8)
 };
 
 // Rows j0 + 4u (u < WS_U) of this lane; GUARD clamps rows >= n0 to row 0.
@@ -1472,15 +1474,16 @@ __device__ __forceinline__ void ws_prefetch(WsPrefetch& pf, int64_t t, int64_t T
   }
 }
 
-// The whole row range [0, n0) of this lane's cells: full stages pipelined, the
+// The row range [j_lo, n0) of this lane's cells: full stages pipelined, the
 // ragged last stage guarded.
 template <int MODE>
-__device__ __forceinline__ void ws_stream(const WsSrc<MODE>& src, int q, bool arow, d4* acc, double* vs,
+__device__ __forceinline__ void ws_stream(const WsSrc<MODE>& src, int q0, bool arow, d4* acc, double* vs,
                                           double* ms, WsPrefetch& pf) {
   constexpr int64_t RS = 4 * ws_u<MODE>();   // rows per stage
   constexpr int SS = ws_s<MODE>();           // stages in the ring
   const int64_t n0 = src.n0;
-  const int64_t T = n0 / RS;         // full stages
+  const int64_t q = src.j_lo + q0;           // this lane's first row
+  const int64_t T = (n0 - src.j_lo) / RS;    // full stages
   WsStage<MODE> st[SS];
 #pragma unroll
   for (int s = 0; s < SS - 1; ++s)
@@ -1514,7 +1517,7 @@ __device__ __forceinline__ void ws_stream(const WsSrc<MODE>& src, int q, bool ar
     if (t + s + SS - 1 < T) ws_load<MODE, false>(st[(s + SS - 1) % SS], src, (t + s + SS - 1) * RS + q);
     ws_use<MODE, false>(st[s % SS], (t + s) * RS + q, n0, arow, acc, vs, ms);
   }
-  if (T * RS < n0) {
+  if (src.j_lo + T * RS < n0) {
     const int64_t j0 = T * RS + q;
     ws_load<MODE, true>(st[0], src, j0);
     ws_use<MODE, true>(st[0], j0, n0, arow, acc, vs, ms);
@@ -1557,9 +1560,12 @@ __device__ void var_argmax_group(const GPDesc& d, double bv, int64_t bi, int64_t
 // Value of register `v` of lane `src` (all lanes take part).
 __device__ __forceinline__ double lane_get(double v, int src) { return __shfl(v, src); }
 
-// One 128-cell workgroup of the one-pass predict. FUSED (inside k_inc_stream): the
-// compact rows are read once sync[1] is signalled, L22 / z2 (L2-bypassing) once
-// sync[2] is; each wave polls for itself.
+// One workgroup of the one-pass predict: 128 / R cells, R = d.rsplit row splits.
+// Wave w owns cell group w % (4 / R) (32 cells) over row split w / (4 / R); with
+// R > 1 (small batches, so that the chip still holds ~4 workgroups per CU) the
+// splits' partial sums meet in LDS, added in split order. FUSED (inside
+// k_inc_stream): the compact rows are read once sync[1] is signalled, L22 / z2
+// once sync[2] is.
 template <bool FUSED>
 __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
   const int64_t M = d.M;
@@ -1568,10 +1574,14 @@ __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
-  const int64_t vt = 2 * wgt + (w >> 1);   // V tile of this wave
-  const int cw = WS_CELLS * (w & 1);        // first cell of this wave inside it
-  const int64_t cg = vt * PBM + cw;         // first grid cell of this wave
-  const bool live = vt * PBM < M;           // a ragged last workgroup may hold an empty V tile
+  const int R = d.rsplit;                   // 1, 2 or 4 (uniform)
+  const int ncg = 4 / R;                    // cell groups per workgroup
+  const int cpw = WS_CELLS * ncg;           // cells per workgroup
+  const int si = w / ncg;                   // this wave's row split
+  const int64_t cg = wgt * cpw + WS_CELLS * (w % ncg);   // first grid cell of this wave
+  const int64_t vt = cg / PBM;              // its V tile
+  const int cw = (int)(cg % PBM);           // and first cell inside it
+  const bool live = cg < M;                 // a ragged last workgroup may hold empty groups
   double* __restrict__ Vt = d.V + vt * d.vld * PBM;
   const Hyp& h = d.hp;
   double* L22 = sm;                          // L22 (row-major) | z2
@@ -1599,22 +1609,22 @@ __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
   if (mma) {
     // the psi_new inputs through LDS (one 16-byte load per thread: the producers'
     // round trips at the start of the launch run beside this traffic)
-    if (tid < WS_WG) {
-      const int64_t cc = wgt * WS_WG + tid < M ? wgt * WS_WG + tid : M - 1;
+    if (tid < cpw) {
+      const int64_t cc = wgt * cpw + tid < M ? wgt * cpw + tid : M - 1;
       reinterpret_cast<dv2*>(Gc)[tid] = *reinterpret_cast<const GLOBAL dv2*>(gp(d.grid) + 2 * cc);
-    } else if (tid < WS_WG + KINC) {
-      const int a = tid - WS_WG;
+    } else if (tid >= NT - KINC) {
+      const int a = tid - (NT - KINC);
       const double* p = row_pt(d, n0 + (a < k ? a : 0));
       Xn[2 * a] = p[0];
       Xn[2 * a + 1] = p[1];
     }
     __syncthreads();
   }
-  if (live && mma) {
+  if (live && mma && si == 0) {
     {
       // T = psi_new^T - L21 V_old: the accumulators start at -psi_new (MFMA output
       // row q + 4v of lane (r, q), cells c0 + x), so the epilogue has no exps left
-      const int e0 = (int)(c0 - wgt * WS_WG);
+      const int e0 = (int)(c0 - wgt * cpw);
       const double g0x = Gc[2 * e0], g0y = Gc[2 * e0 + 1], g1x = Gc[2 * e0 + 2], g1y = Gc[2 * e0 + 3];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -1634,17 +1644,60 @@ __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
   if (FUSED && mma) wait_flag(d, d.sync + 1, d.epoch);   // the compact rows of this append (all waves)
   WsPrefetch pf{(FUSED && mma) ? d.sync + 2 : nullptr, d.epoch, d.l22r, 0u, 0.0, 0.0, false};
   if (FUSED) WTRACE(1);
-  if (live) {
+  // this wave's rows: split si of [0, n0) at multiples of 8 rows; a re-predict
+  // (k = 0) streams all rows in split 0 (the exact summation order of k_predict)
+  int64_t j_lo = 0, j_hi = n0;
+  if (R > 1) {
+    if (!mma) {
+      j_hi = si == 0 ? n0 : 0;
+    } else {
+      j_lo = (si * n0 / R) & ~(int64_t)7;
+      j_hi = si == R - 1 ? n0 : ((si + 1) * n0 / R) & ~(int64_t)7;
+    }
+  }
+  if (live && j_hi > j_lo) {
     const GLOBAL dv2* vb = reinterpret_cast<const GLOBAL dv2*>(gp(Vt)) + (cw >> 1) + r;
     if (zrow) {
-      const WsSrc<2> src{vb, gp(d.l21c) + r, KINC, nullptr, n0};
+      const WsSrc<2> src{vb, gp(d.l21c) + r, KINC, nullptr, j_hi, j_lo};
       ws_stream<2>(src, q, true, acc, vs, ms, pf);
     } else if (mma) {
-      const WsSrc<1> src{vb, gp(d.A) + n0 + (r < k ? r : 0), ld, gp(d.zv), n0};
+      const WsSrc<1> src{vb, gp(d.A) + n0 + (r < k ? r : 0), ld, gp(d.zv), j_hi, j_lo};
       ws_stream<1>(src, q, r < k, acc, vs, ms, pf);
     } else {
-      const WsSrc<0> src{vb, nullptr, 0, gp(d.zv), n0};
+      const WsSrc<0> src{vb, nullptr, 0, gp(d.zv), j_hi, j_lo};
       ws_stream<0>(src, q, false, acc, vs, ms, pf);
+    }
+  }
+  if (R > 1 && mma) {
+    // the row splits' partials meet in LDS (lane-for-lane, before the lane
+    // reductions), added to split 0's in split order
+    double* part = Gc + 2 * WS_WG;   // [(R - 1) * ncg slots][12][64]
+    if (si > 0) {
+      double* pp = part + ((si - 1) * ncg + w % ncg) * 12 * 64 + lane;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        pp[v * 64] = acc[0][v];
+        pp[(4 + v) * 64] = acc[1][v];
+      }
+      pp[8 * 64] = vs[0];
+      pp[9 * 64] = vs[1];
+      pp[10 * 64] = ms[0];
+      pp[11 * 64] = ms[1];
+    }
+    __syncthreads();
+    if (si == 0) {
+      for (int sj = 1; sj < R; ++sj) {
+        const double* pp = part + ((sj - 1) * ncg + w % ncg) * 12 * 64 + lane;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          acc[0][v] += pp[v * 64];
+          acc[1][v] += pp[(4 + v) * 64];
+        }
+        vs[0] += pp[8 * 64];
+        vs[1] += pp[9 * 64];
+        ms[0] += pp[10 * 64];
+        ms[1] += pp[11 * 64];
+      }
     }
   }
   // colsums over the lanes' row residues q (and, for k = 0, the four row classes)
@@ -1725,7 +1778,7 @@ __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
 #ifdef MFGP_DIAG_NOSTORE   // diagnostic build: no V_new stores (timing only)
     if (false) {
 #else
-    if (live && q < 2 && c < M) {
+    if (live && si == 0 && q < 2 && c < M) {
 #endif
 #pragma unroll
       for (int a = 0; a < KINC; ++a)
@@ -1739,12 +1792,12 @@ __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
     }
   }
   const double vc = h.kss - vsum;
-  const bool valid = live && q < 2 && c < M;
+  const bool valid = live && si == 0 && q < 2 && c < M;
   if (valid) {
     d.mu[c] = msum + h.meanH;
     d.var[c] = vc;
   }
-  if ((d.vmax || d.vargmax) && cg < M)
+  if ((d.vmax || d.vargmax) && cg < M && si == 0)
     var_argmax_group(d, valid ? vc : -__builtin_inf(), valid ? c : INT64_MAX, cg / WS_CELLS,
                      (M + WS_CELLS - 1) / WS_CELLS);
   if (FUSED) WTRACE(4);
@@ -1753,7 +1806,7 @@ __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_vstream(
     const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
-  if ((int64_t)blockIdx.x * WS_WG >= d.M) return;
+  if ((int64_t)blockIdx.x * (WS_WG / d.rsplit) >= d.M) return;
   if (d.gate && *d.gate == 0) return;
   __shared__ double sm[VS_LDS];
   vstream_wg<false>(d, blockIdx.x, sm);
@@ -1790,7 +1843,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
   const int64_t np = d.nprod, role = blockIdx.y;
   if (role >= np) {
     const int64_t wgt = role - np;
-    if (d.tiles && wgt * WS_WG < d.M) vstream_wg<true>(d, wgt, sm);
+    if (d.tiles && wgt * (WS_WG / d.rsplit) < d.M) vstream_wg<true>(d, wgt, sm);
     return;
   }
   __shared__ int cell[KINC];
