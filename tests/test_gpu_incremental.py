@@ -405,3 +405,41 @@ def test_batched_ragged_fused_append_predict(full_ctx, split_ctx, fused):
         np.testing.assert_allclose(inc[i].factor(), full[i].factor(), rtol=1e-6, atol=1e-9)
         st = inc[i].stats()
         assert st["inc_factor"] == steps and st["vstream"] == steps - 1, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [2, 4, 8])
+def test_headline_batch_row_splits_vs_full(full_ctx, B):
+    """Batches of B headline-size MF GPs in one fused launch. On MI355X (256 CUs) the
+    one-pass predict then runs with 4 / 2 / 1 row splits per cell group (32 / 64 / 128
+    cells per workgroup, partials meeting in LDS): each must equal the full recompute
+    (size-independent property), including the fused np.amax / np.argmax."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    G, NL, NH0, k = 128, 1024, 1016, 8
+    ctx = _lib.context()
+    cases = [_points(G, NL + NH0 + k, seed=300 + b, ongrid=True) for b in range(B)]
+    inc = [_model(ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0] for Xs, X, y in cases]
+    full = [_model(full_ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0] for Xs, X, y in cases]
+    for mdl in inc:
+        mdl.predict()                      # V resident: the appends below are bordered steps
+    M = G * G
+    lo = NL + NH0
+    Xn = np.ascontiguousarray(np.vstack([X[lo:lo + k] for _, X, _ in cases]))
+    yn = np.ascontiguousarray(np.concatenate([y[lo:lo + k] for _, _, y in cases]))
+    Xd, yd = torch.from_numpy(Xn).cuda(), torch.from_numpy(yn).cuda()
+    outs = []
+    for models in (inc, full):
+        mu_d = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        var_d = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        vmax = torch.full((B,), -1.0, dtype=torch.float64, device="cuda")
+        varg = torch.full((B,), -1, dtype=torch.int64, device="cuda")
+        _lib.batch_append_predict(models, Xd.data_ptr(), yd.data_ptr(), [k] * B, mu_d.data_ptr(),
+                                  var_d.data_ptr(), vmax_ptr=vmax.data_ptr(), vargmax_ptr=varg.data_ptr())
+        outs.append((mu_d.cpu().numpy().reshape(B, M), var_d.cpu().numpy().reshape(B, M),
+                     vmax.cpu().numpy(), varg.cpu().numpy()))
+    (mu, var, vm, va), (mu_f, var_f, vm_f, va_f) = outs
+    for b in range(B):
+        assert _err(mu[b], var[b], mu_f[b], var_f[b], HYP_MF) < 1e-8
+        assert vm[b] == np.amax(var[b]) and va[b] == int(np.argmax(var[b]))
+    assert all(m.stats()["vstream"] >= 1 and m.stats()["inc_factor"] >= 1 for m in inc)
