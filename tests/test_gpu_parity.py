@@ -279,3 +279,34 @@ def test_headline_size_vs_oracle(gp):
     _check(mu, cov, mu_r, var_r, hyp)
     var = np.diag(cov)
     assert np.all(var > -1e-12) and np.all(var <= O.prior_variance(hyp) * (1 + 1e-12))
+
+
+def test_config5_size_vs_oracle(gp):
+    """BASELINE configs[4] sizes for one GP: 256x256 grid (M = 65536), N = 4096 lofi + 4096 hifi,
+    australia9 MF hyp, at fp64 (the fp32 mode is not built). The full
+    factor + predict, then an 8-row bordered append (the incremental path), each against the
+    diag oracle on 4096 sampled cells plus the new samples' cells and the device's argmax
+    cell, at the parity tolerance."""
+    from mfgp_coverage_amd.synthetic import HYP, Workload
+    hyp = HYP["australia9_mf"]
+    w = Workload(256, 4096, 4088, 8, 1, seed=11)
+    m = gp.MFGP(w.XL, w.yL.reshape(-1, 1), w.XH, w.yH.reshape(-1, 1), 1, 1)
+    m.hyp = hyp
+    m.updt_info(m.X_L, m.y_L, m.X_H, m.y_H)
+    M = w.xs.shape[0]
+    rng = np.random.default_rng(5)
+    Xn, yn = w.Xnew[0], w.ynew[0].reshape(-1, 1)
+    new_cells = np.array([int(np.argmin(np.abs(w.xs - p).sum(1))) for p in Xn])
+    for step in range(2):
+        mu, cov = m.predict(w.xs)
+        var = np.diag(cov)
+        XH = m.X_H
+        pick = np.unique(np.concatenate([rng.choice(M, 4096, replace=False), new_cells,
+                                         [int(np.argmax(var))]]))
+        mu_r, var_r = O.mf_diag(w.XL, w.yL, XH, m.y_H, hyp, w.xs[pick])
+        e = O.parity_errors(mu[pick, 0], var[pick], mu_r, var_r, O.prior_variance(hyp))
+        assert max(e) < TOL, (step, e)
+        if step == 0:
+            m.updt_hifi(Xn, yn)
+    st = m._dev().stats()
+    assert st["inc_factor"] >= 1 and st["vstream"] >= 1, st
