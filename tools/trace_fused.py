@@ -11,14 +11,15 @@ import numpy as np
 import torch
 from mfgp_coverage_amd import _lib, synthetic
 
-B, G, NL, NH, k = 8, 128, 1024, 1024, 8
+B = int(os.environ.get("TRACE_B", "8"))
+G, NL, NH, k = 128, 1024, 1024, 8
 T = 24 if B2B else 6
 NH0 = NH - k
 M = G * G
 hyp = synthetic.HYP["australia8_mf"]
 wls = [synthetic.Workload(G, NL, NH0, k, T, seed=s) for s in range(B)]
 dev = torch.device("cuda", 0)
-NWG = B * (16 + 256)
+NWG = B * (16 + 1024)   # room for the row-split launches of small batches
 st = torch.zeros(64 + 8 * NWG + 64, dtype=torch.int64, device=dev)
 L = _lib.lib()
 L.mfgp_debug_set_stamps.argtypes = [ctypes.c_void_p]
@@ -53,7 +54,7 @@ tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)   # us
 nprod = 16
 role = np.arange(NWG) // B
 prod, tiles = tr[role < nprod], tr[role >= nprod]
-tag = os.path.basename(sys.argv[1]).replace("libmfgp_", "").replace(".so", "") + ("_b2b" if B2B else "")
+tag = os.path.basename(sys.argv[1]).replace("libmfgp_", "").replace(".so", "") + ("_b2b" if B2B else "") + f"_B{B}"
 np.savez(os.path.join(ROOT, "gpurun_out", f"trace_{tag}.npz"), tr=tr, hw=hw)
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100))
 print(f"[{tag}] percentiles 0/10/50/90/100 (us from the first WG start)")
