@@ -230,6 +230,8 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   HIP_TRY(hipMalloc(&y, sizeof(double) * cap));
   HIP_TRY(hipMalloc(&zv, sizeof(double) * cap));
   HIP_TRY(hipMalloc(&isc, sizeof(double) * inc_scratch_doubles(cap)));
+  // producer ready flags start below every epoch (epochs are never 0)
+  HIP_TRY(hipMemsetAsync(isc + inc_pflag_offset(cap), 0, sizeof(unsigned) * inc_pflag_count(cap), c->stream));
   HIP_TRY(hipMalloc(&A, sizeof(double) * ld * ld));
   HIP_TRY(hipMalloc(&Li, sizeof(double) * (ld / NB) * TILE));
   const int64_t n = m->NL + m->NH;
@@ -345,6 +347,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.iscr = m->iscr;
   d.l21c = m->iscr ? m->iscr + inc_l21c_offset(m->cap) : nullptr;
   d.l22r = m->iscr ? m->iscr + inc_l22r_offset(m->cap) : nullptr;
+  d.pflag = m->iscr ? reinterpret_cast<unsigned*>(m->iscr + inc_pflag_offset(m->cap)) : nullptr;
   d.mu = nullptr;
   d.var = nullptr;
   d.vmax = nullptr;

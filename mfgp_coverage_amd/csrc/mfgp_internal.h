@@ -23,7 +23,11 @@ constexpr int64_t inc_l21c_offset(int64_t cap) {
 }
 // then (128-byte aligned) the L22 record: L22 row-major [KINC][KINC] | z2 [KINC]
 constexpr int64_t inc_l22r_offset(int64_t cap) { return (inc_l21c_offset(cap) + cap * KINC + 15) / 16 * 16; }
-constexpr int64_t inc_scratch_doubles(int64_t cap) { return inc_l22r_offset(cap) + KINC * KINC + KINC; }
+// then the producers' ready flags (k_inc_stream): one unsigned per FUSED_CHUNK-row
+// chunk, holding the epoch of the launch whose compact rows of that chunk are stored
+constexpr int64_t inc_pflag_offset(int64_t cap) { return inc_l22r_offset(cap) + KINC * KINC + KINC; }
+constexpr int64_t inc_pflag_count(int64_t cap) { return (cap + FUSED_CHUNK - 1) / FUSED_CHUNK; }
+constexpr int64_t inc_scratch_doubles(int64_t cap) { return inc_pflag_offset(cap) + (inc_pflag_count(cap) + 1) / 2; }
 // k_inc_stream producers for a factor current for n0 rows (at least one: the finish)
 inline int64_t fused_producers(int64_t n0) { return n0 > 0 ? (n0 + FUSED_CHUNK - 1) / FUSED_CHUNK : 1; }
 
@@ -79,6 +83,7 @@ struct GPDesc {
   int64_t ablk;        // k_inc_factor: 64-row blocks of A / Linv already initialised
   GridLattice lat;     // lattice structure of `grid` (nx == 0: none)
   unsigned* sync;      // k_inc_stream hand-off: {producer arrivals, L21 ready, L22 / z2 ready}
+  unsigned* pflag;     // k_inc_stream: per producer chunk, the epoch once its compact rows are stored (in iscr)
   unsigned epoch;      // k_inc_stream: value of this launch's ready flags (never 0)
   int nprod;           // k_inc_stream: producer workgroups ahead of the cell tiles
   int tiles;           // k_inc_stream: 1 = the launch also streams the cell tiles (one-pass predict)

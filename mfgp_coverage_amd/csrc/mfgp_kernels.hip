@@ -862,6 +862,30 @@ __device__ void wait_flag(const GPDesc& d, const unsigned* f, unsigned v) {
   __syncthreads();
 }
 
+// Wait (wave 0; the workgroup joins at the barrier) until the compact rows of
+// this append are stored: every producer chunk's flag holds this launch's epoch,
+// or sync[1] does (raised by the last producer to arrive, or by the finish when
+// it solved L21 itself). Bounded like wait_flag.
+__device__ void wait_l21(const GPDesc& d) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int it = 0;
+    while (true) {
+      bool mine = true;
+      for (int c = lane; c < d.nprod; c += 64)
+        mine = mine && __hip_atomic_load(d.pflag + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d.epoch;
+      const bool any = __hip_atomic_load(d.sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d.epoch;
+      if (any || __ballot(!mine) == 0) break;
+      __builtin_amdgcn_s_sleep(MFGP_SPIN_SLEEP);
+      if (++it == (1 << 22)) {
+        if (lane == 0) atomicMin(d.status, SYNC_FAIL);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // Coordinates / observation of training row `row`: rows landing in this launch
 // ([N - k_new, N), device source) are read from the source itself.
 __device__ __forceinline__ const double* row_pt(const GPDesc& d, int64_t row) {
@@ -876,8 +900,10 @@ __device__ __forceinline__ double row_obs(const GPDesc& d, int64_t row) {
 // Identity padding for the 64-row blocks [ablk, nbf) entered for the first time,
 // columns [c_lo, c_hi) (the full predict reads whole blocks: padding rows must
 // stay finite), and, with `linv`, their Linv blocks.
+// Rows [skip_lo, skip_hi) are left out (the caller stores them itself).
 template <bool XW = false>
-__device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, bool linv) {
+__device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, bool linv, int64_t skip_lo = 0,
+                                int64_t skip_hi = 0) {
   const int64_t nbf = nblocks_factor(d.N);
   const int tid = threadIdx.x, nthr = blockDim.x;
   for (int64_t bb = d.ablk; bb < nbf; ++bb) {
@@ -886,7 +912,7 @@ __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, boo
       for (int64_t e = tid; e < (c1 - c_lo) * NB; e += nthr) {
         const int64_t col = c_lo + (e >> 6);
         const int64_t row = bb * NB + (e & 63);
-        stx<XW>(&d.A[col * d.ld + row], (col == row) ? 1.0 : 0.0);
+        if (row < skip_lo || row >= skip_hi) stx<XW>(&d.A[col * d.ld + row], (col == row) ? 1.0 : 0.0);
       }
     }
     if (linv)
@@ -1007,12 +1033,89 @@ __device__ int lattice_cell(const GPDesc& d, double px, double py) {
   return hit;
 }
 
+// End of a gathering producer chunk: its compact rows (and L21 rows in A) are
+// drained and announced in pflag[chunk] (the cell workgroups wait for these),
+// then the chunk's partials (red, summed over the waves) are stored for the finish.
+__device__ __forceinline__ bool inc_chunk_done(const GPDesc& d, int64_t chunk, double (*red)[ISZ]) {
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) publish(d.pflag + chunk, d.epoch);
+  FSTAMP(39);   // latest producer past its gather
+  double* __restrict__ part = d.iscr + ISC0 + chunk * ISZ;
+  for (int e = threadIdx.x; e < ISZ; e += NT) {
+    double acc = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) acc += red[w][e];
+    stx<true>(part + e, acc);
+  }
+  return true;
+}
+
+// Fast path of a producer chunk (at most FUSED_CHUNK rows) on a lattice grid: each
+// wave estimates the new points' cells itself (lane r < k: point r, the rounded
+// axis estimate), gathers its rows of L21 from those V columns and checks the
+// estimates against the grid coordinates in the same round trip. Every wave
+// checks the same points, so the verdict is uniform; on a miss nothing has been
+// stored and the caller takes the general path. Otherwise as inc_schur_partial
+// (FROMV): L21 rows into A and the compact rows, partials into red, and the
+// chunk's identity padding of newly entered blocks (rows [n0, N) excepted: they
+// are the L21 stores, so no barrier orders the two).
+__device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, int64_t j_hi, double (*red)[ISZ]) {
+  constexpr int NW = NT / 64, IU = 8;
+  static_assert(4 * NW * IU >= FUSED_CHUNK, "one round of loads covers a chunk");
+  const int64_t n0 = d.n0, ld = d.ld, N = d.N;
+  const int k = (int)(N - n0);
+  double* const A = d.A;
+  double* const l21c = d.l21c;
+  const double* const zv = d.zv;
+  const GridLattice L = d.lat;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  const double* p = row_pt(d, n0 + (r < k ? r : 0));
+  const double px = p[0], py = p[1];
+  const int ix = (int)rint(fmin(fmax((px - L.x0) * L.xinv, 0.0), (double)(L.nx - 1)));
+  const int iy = (int)rint(fmin(fmax((py - L.y0) * L.yinv, 0.0), (double)(L.ny - 1)));
+  const int64_t cr = (px == px && py == py) ? ix * L.sx + iy * L.sy : 0;
+  const dv2 g = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid))[cr];
+  const double* src = d.V + (cr / PBM) * d.vld * PBM + (cr % PBM);
+  double a[IU], zz[IU];
+#pragma unroll
+  for (int u = 0; u < IU; ++u) {
+    const int64_t j = j_lo + 4 * (w + NW * u) + q;
+    const int64_t jj = j < j_hi ? j : j_lo;
+    a[u] = gp(src)[jj * PBM];
+    zz[u] = gp(zv)[jj];
+  }
+  const bool miss = r < k && !(g.x == px && g.y == py);
+  if (__ballot(miss) != 0) return false;
+  inc_init_blocks<true>(d, j_lo, j_hi, false, n0, N);
+  d4 sacc = {0.0, 0.0, 0.0, 0.0}, uacc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int u = 0; u < IU; ++u) {
+    const int64_t j = j_lo + 4 * (w + NW * u) + q;
+    const bool ok = j < j_hi;
+    a[u] = (ok && r < k) ? a[u] : 0.0;
+    zz[u] = ok ? zz[u] : 0.0;
+    if (r < k && ok) stx<true>(&A[j * ld + n0 + r], a[u]);
+    if (ok) stx<true>(&l21c[j * KINC + r], r < k ? a[u] : (r == k ? zz[u] : 0.0));
+    sacc = mfma(a[u], a[u], sacc);
+    uacc = mfma(a[u], zz[u], uacc);
+  }
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    red[w][(q + 4 * v) * KINC + r] = sacc[v];
+    if (r == 0) red[w][KINC * KINC + q + 4 * v] = uacc[v];
+  }
+  return true;
+}
+
 // One producer chunk: land device-resident new rows (chunk 0), find the new
 // points' grid cells, gather their V columns into rows n0.. of A for rows
 // [chunk * ch, +ch) and store the chunk's partials. Returns false when L21 is not
 // a set of V columns (off the grid / no resident V): the finish solves for it.
 // All NTHR threads take part; `cell` and `red` are in LDS.
-__device__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell, double (*red)[ISZ]) {
+__device__ __forceinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell, double (*red)[ISZ]) {
   constexpr int NTHR = NT;
   constexpr bool XW = true;
   const int64_t n0 = d.n0, N = d.N;
@@ -1033,6 +1136,14 @@ __device__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cel
   }
   const int64_t j_lo = chunk * ch;
   const int64_t j_hi = j_lo + ch < n0 ? j_lo + ch : n0;
+#ifndef MFGP_NO_FASTGATHER
+  if (d.lat.nx > 0 && j_lo < n0 && ch <= FUSED_CHUNK && inc_gather_fast(d, j_lo, j_hi, red)) {
+#else
+  if (false) {
+#endif
+    if (chunk == 0 && tid == 0) stx<XW>(d.iscr, 1.0);
+    return inc_chunk_done(d, chunk, red);
+  }
   if (tid < KINC) cell[tid] = INT_MAX;
   __syncthreads();
   // lattice grids: a few probes per point; otherwise (or for a point off the
@@ -1066,16 +1177,7 @@ __device__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cel
   inc_init_blocks<XW>(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
   __syncthreads();
   inc_schur_partial<NTHR / 64, XW, true>(d, cell, j_lo, j_hi, red);
-  __syncthreads();
-  if (XW) FSTAMP(39);   // latest producer past its gather
-  double* __restrict__ part = d.iscr + ISC0 + chunk * ISZ;
-  for (int e = tid; e < ISZ; e += NTHR) {
-    double acc = 0.0;
-#pragma unroll
-    for (int w = 0; w < NTHR / 64; ++w) acc += red[w][e];
-    stx<XW>(part + e, acc);
-  }
-  return true;
+  return inc_chunk_done(d, chunk, red);
 }
 
 // LDS of the finish step (doubles; 256 threads):
@@ -1093,7 +1195,7 @@ constexpr int LBW = 16;   // Linv_OO columns staged per pass (63 rows x 16 = 100
 // this step solved it) and `sync[2]` once L22 / z2 are, with the hand-off
 // accesses of ldx / stx.
 template <bool FUSED>
-__device__ void inc_finish(const GPDesc& d, double* sm, int64_t ch) {
+__device__ __forceinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch) {
   const int64_t n0 = d.n0, N = d.N, ld = d.ld, NL = d.NL;
   const int k = (int)(N - n0);
   const Hyp& h = d.hf;
@@ -1567,7 +1669,7 @@ __device__ __forceinline__ double lane_get(double v, int src) { return __shfl(v,
 // k_inc_stream): the compact rows are read once sync[1] is signalled, L22 / z2
 // once sync[2] is.
 template <bool FUSED>
-__device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
+__device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
   const int64_t M = d.M;
   const int64_t n0 = d.n0, N = d.N, ld = d.ld;
   const int k = (int)(N - n0);
@@ -1641,7 +1743,11 @@ __device__ void vstream_wg(const GPDesc& d, int64_t wgt, double* sm) {
       }
     }
   }
-  if (FUSED && mma) wait_flag(d, d.sync + 1, d.epoch);   // the compact rows of this append (all waves)
+#ifndef MFGP_OLDWAIT
+  if (FUSED && mma) wait_l21(d);   // the compact rows of this append (all waves)
+#else
+  if (FUSED && mma) wait_flag(d, d.sync + 1, d.epoch);
+#endif
   WsPrefetch pf{(FUSED && mma) ? d.sync + 2 : nullptr, d.epoch, d.l22r, 0u, 0.0, 0.0, false};
   if (FUSED) WTRACE(1);
   // this wave's rows: split si of [0, n0) at multiples of 8 rows; a re-predict
