@@ -1136,11 +1136,7 @@ __device__ __forceinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int6
   }
   const int64_t j_lo = chunk * ch;
   const int64_t j_hi = j_lo + ch < n0 ? j_lo + ch : n0;
-#ifndef MFGP_NO_FASTGATHER
   if (d.lat.nx > 0 && j_lo < n0 && ch <= FUSED_CHUNK && inc_gather_fast(d, j_lo, j_hi, red)) {
-#else
-  if (false) {
-#endif
     if (chunk == 0 && tid == 0) stx<XW>(d.iscr, 1.0);
     return inc_chunk_done(d, chunk, red);
   }
@@ -1743,11 +1739,7 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
       }
     }
   }
-#ifndef MFGP_OLDWAIT
   if (FUSED && mma) wait_l21(d);   // the compact rows of this append (all waves)
-#else
-  if (FUSED && mma) wait_flag(d, d.sync + 1, d.epoch);
-#endif
   WsPrefetch pf{(FUSED && mma) ? d.sync + 2 : nullptr, d.epoch, d.l22r, 0u, 0.0, 0.0, false};
   if (FUSED) WTRACE(1);
   // this wave's rows: split si of [0, n0) at multiples of 8 rows; a re-predict
