@@ -281,7 +281,7 @@ def test_headline_size_vs_oracle(gp):
     assert np.all(var > -1e-12) and np.all(var <= O.prior_variance(hyp) * (1 + 1e-12))
 
 
-def test_config5_size_vs_oracle(gp):
+def test_configs4_size_vs_oracle(gp):
     """BASELINE configs[4] sizes for one GP: 256x256 grid (M = 65536), N = 4096 lofi + 4096 hifi,
     australia9 MF hyp, at fp64 (the fp32 mode is not built). The full
     factor + predict, then an 8-row bordered append (the incremental path), each against the
