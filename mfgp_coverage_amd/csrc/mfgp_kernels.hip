@@ -131,10 +131,12 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // Broadcast lane k of each 16-lane DPP row to the whole row (row_newbcast:k, gfx90a+).
 // The DPP control must be an immediate: the switch folds away once the callers'
 // fully unrolled loops make k a constant.
+// (Every lane reads a valid lane of its row, so no `old` operand is needed: with
+// bound_ctrl the compiler drops the zero-initialising moves of update_dpp.)
 template <int K>
 __device__ __forceinline__ double bcast16_(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + K, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + K, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + K, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + K, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double bcast16(double v, int k) {
