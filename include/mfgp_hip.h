@@ -64,6 +64,13 @@ int mfgp_ctx_set_incremental(mfgp_ctx* ctx, int enable);
  * 0 = two launches (k_inc_stream for the append alone, then k_vstream). Same
  * numbers either way. */
 int mfgp_ctx_set_fused(mfgp_ctx* ctx, int enable);
+/* Deferred appends (default 0): mfgp_append of rows that a bordered append can
+ * take only stages them; the next call that needs the factor runs the append --
+ * mfgp_predict as one launch with the one-pass predict (the single-model form of
+ * the batched path). A non-positive-definite append is then reported by that
+ * call instead of by mfgp_append (the reference raises in updt / updt_hifi,
+ * gp:254 / gp:529). */
+int mfgp_ctx_set_deferred_appends(mfgp_ctx* ctx, int enable);
 /* Kernel timing with HIP events on the launch stream: enable = 1 times every
  * predict-kernel launch (fused predict or one-pass incremental predict) and
  * every factor stage; 2 times the predict launches only (each event pair is a

@@ -5,7 +5,7 @@ of MSU-dcypherlab/mfgp-coverage.
 the reference's ``from gaussian_process import MFGP, SFGP`` (simulator.py:25).
 The compute path is libmfgp_hip.so (HIP for gfx950, C ABI in include/mfgp_hip.h).
 """
-from ._lib import context, set_device  # noqa: F401
+from ._lib import context, set_deferred_appends, set_device  # noqa: F401
 from .gaussian_process import MFGP, SFGP, DiagCov  # noqa: F401
 
-__all__ = ["SFGP", "MFGP", "DiagCov", "context", "set_device"]
+__all__ = ["SFGP", "MFGP", "DiagCov", "context", "set_device", "set_deferred_appends"]

@@ -31,6 +31,7 @@ SIGNATURES = {
     "mfgp_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "mfgp_ctx_set_incremental": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mfgp_ctx_set_deferred_appends": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_timing_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "mfgp_batch_append_predict_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -151,6 +152,12 @@ class Context:
         """Bordered append + one-pass predict of a batch in one launch (default on)."""
         check(lib().mfgp_ctx_set_fused(self.handle, 1 if on else 0))
 
+    def set_deferred_appends(self, on=True):
+        """Stage appends and run them with the next predict, in one launch (default off:
+        an append factors at once, so a non-PD step raises in updt / updt_hifi as in
+        the reference; deferred, it raises in the predict that runs it)."""
+        check(lib().mfgp_ctx_set_deferred_appends(self.handle, 1 if on else 0))
+
     def enable_timing(self, on=True, predict_only=False):
         """HIP-event timing of the predict launches (and, unless predict_only, the factor stages)."""
         check(lib().mfgp_ctx_enable_timing(self.handle, (2 if predict_only else 1) if on else 0))
@@ -179,6 +186,13 @@ def set_device(device):
     """Device used by models created afterwards in this process (one process per GPU)."""
     global _default_device
     _default_device = int(device)
+
+
+def set_deferred_appends(on=True, device=None):
+    """Deferred appends on the calling thread's context (see Context.set_deferred_appends):
+    updt / updt_hifi stage their rows and the next predict runs the bordered append and
+    the one-pass predict as one launch."""
+    context(device).set_deferred_appends(on)
 
 
 def context(device=None):

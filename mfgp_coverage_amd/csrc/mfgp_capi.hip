@@ -77,6 +77,12 @@ struct mfgp_ctx {
   // refactor and recompute V from scratch, as the reference does
   bool incremental = true;
   bool fused = true;          // bordered append + one-pass predict in one launch (k_inc_stream)
+  bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
+  // pinned host staging: predict outputs bound for pageable memory, status words
+  double* h_out = nullptr;
+  size_t h_out_bytes = 0;
+  int* h_status = nullptr;
+  size_t h_status_n = 0;
   int ncu = 256;              // compute units (hipDeviceProp multiProcessorCount)
 };
 
@@ -200,6 +206,29 @@ int drain_timing(mfgp_ctx* c) {
     c->pool.push_back(p.b);
   }
   c->pending.clear();
+  return MFGP_OK;
+}
+
+int ensure_h_out(mfgp_ctx* c, size_t bytes) {
+  if (bytes <= c->h_out_bytes) return MFGP_OK;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->h_out) HIP_TRY(hipHostFree(c->h_out));
+  c->h_out = nullptr;
+  c->h_out_bytes = 0;
+  HIP_TRY(hipHostMalloc(&c->h_out, bytes, hipHostMallocDefault));
+  c->h_out_bytes = bytes;
+  return MFGP_OK;
+}
+
+int ensure_h_status(mfgp_ctx* c, size_t n) {
+  if (n <= c->h_status_n) return MFGP_OK;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->h_status) HIP_TRY(hipHostFree(c->h_status));
+  c->h_status = nullptr;
+  c->h_status_n = 0;
+  const size_t want = std::max<size_t>(n, 64);
+  HIP_TRY(hipHostMalloc(&c->h_status, sizeof(int) * want, hipHostMallocDefault));
+  c->h_status_n = want;
   return MFGP_OK;
 }
 
@@ -448,10 +477,38 @@ int status_error(int st) {
 }
 
 int read_status(mfgp_model* m) {
-  int st = INT_MAX;
-  HIP_TRY(hipMemcpy(&st, m->status, sizeof(int), hipMemcpyDeviceToHost));
+  mfgp_ctx* c = m->ctx;
+  int rc = ensure_h_status(c, 1);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->h_status, m->status, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const int st = c->h_status[0];
   if (st != INT_MAX) return status_error(st);
   return MFGP_OK;
+}
+
+bool is_device_ptr(const void* p);
+
+// mu / var ([M] each, contiguous at src on the device) into the caller's buffers:
+// device buffers by device copies, host buffers through the pinned staging buffer
+// (one DMA; the host copies happen in finish_out after the stream is synchronized).
+int start_out(mfgp_ctx* c, double* mu, double* var, const double* src, int64_t M, bool& staged) {
+  staged = !(is_device_ptr(mu) && is_device_ptr(var));
+  if (!staged) {
+    HIP_TRY(hipMemcpyAsync(mu, src, sizeof(double) * M, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(var, src + M, sizeof(double) * M, hipMemcpyDeviceToDevice, c->stream));
+    return MFGP_OK;
+  }
+  int rc = ensure_h_out(c, sizeof(double) * 2 * (size_t)M);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->h_out, src, sizeof(double) * 2 * (size_t)M, hipMemcpyDeviceToHost, c->stream));
+  return MFGP_OK;
+}
+
+void finish_out(const mfgp_ctx* c, double* mu, double* var, int64_t M, bool staged) {
+  if (!staged) return;
+  std::memcpy(mu, c->h_out, sizeof(double) * M);
+  std::memcpy(var, c->h_out + M, sizeof(double) * M);
 }
 
 int ensure_sync(mfgp_model* m) {
@@ -655,6 +712,8 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
   for (int i = 0; i < RING; ++i) (void)hipEventDestroy(c->ring_ev[i]);
   if (c->ws) (void)hipFree(c->ws);
   if (c->d_ring) (void)hipFree(c->d_ring);
+  if (c->h_out) (void)hipHostFree(c->h_out);
+  if (c->h_status) (void)hipHostFree(c->h_status);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -671,11 +730,14 @@ void* mfgp_ctx_get_stream(mfgp_ctx* c) { return c ? (void*)c->stream : nullptr; 
 
 int mfgp_ctx_synchronize(mfgp_ctx* c) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  int rc = ensure_h_status(c, c->async_status.size());
+  if (rc) return rc;
+  // the status words come back through pinned memory with the stream's last copies
+  for (size_t i = 0; i < c->async_status.size(); ++i)
+    HIP_TRY(hipMemcpyAsync(c->h_status + i, c->async_status[i], sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  int rc = MFGP_OK;
-  for (int* s : c->async_status) {
-    int st = INT_MAX;
-    HIP_TRY(hipMemcpy(&st, s, sizeof(int), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < c->async_status.size(); ++i) {
+    const int st = c->h_status[i];
     if (st != INT_MAX && rc == MFGP_OK) rc = status_error(st);
   }
   c->async_status.clear();
@@ -693,6 +755,13 @@ int mfgp_ctx_set_fused(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->fused = enable != 0;
+  return MFGP_OK;
+}
+
+int mfgp_ctx_set_deferred_appends(mfgp_ctx* c, int enable) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->deferred = enable != 0;
   return MFGP_OK;
 }
 
@@ -921,6 +990,7 @@ int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
   if ((rc = copy_rows(m, n, X, y, k))) return rc;
   m->NH += k;
   if (!m->ctx->incremental) m->factored = false;   // reference behaviour: refactor from scratch
+  if (m->ctx->deferred && can_inc_factor(m)) return MFGP_OK;   // the next factor user runs the append
   return update_factor(m);
 }
 
@@ -938,11 +1008,30 @@ int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
   return MFGP_OK;
 }
 
+static int batch_run(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
+                     double* mu, double* var, double* vmax, int64_t* vargmax, int flags, bool do_factor,
+                     bool do_predict);
+
 int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   int rc = check_model(m);
   if (rc) return rc;
   mfgp_ctx* c = m->ctx;
   if (m->M > 0 && (!mu || !var)) return set_err(MFGP_ERR_ARG, "null output");
+  if (m->M > 0 && !factor_current(m) && can_inc_factor(m)) {
+    // a staged (deferred) append: the bordered append and the one-pass predict
+    // as one launch when V is resident (the batched path for one model)
+    const size_t ob2 = sizeof(double) * 2 * (size_t)m->M;
+    if ((rc = ensure_ws(c, ob2))) return rc;
+    double* mu_d = c->ws;
+    double* var_d = mu_d + m->M;
+    rc = batch_run(&m, 1, nullptr, nullptr, nullptr, mu_d, var_d, nullptr, nullptr, MFGP_ASYNC, true, true);
+    bool staged = false;
+    if (rc == MFGP_OK) rc = start_out(c, mu, var, mu_d, m->M, staged);
+    if (rc == MFGP_OK) rc = mfgp_ctx_synchronize(c);
+    if (rc == MFGP_OK) finish_out(c, mu, var, m->M, staged);
+    if (rc != MFGP_OK) m->factored = false;   // a failed step leaves no usable factor
+    return rc;
+  }
   if ((rc = update_factor(m))) return rc;
   if (m->M == 0) return MFGP_OK;
   if ((rc = ensure_v(m))) return rc;
@@ -962,10 +1051,11 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   if ((rc = vst ? enqueue_vstream(c, dd, hd, 1) : enqueue_predict(c, dd, hd, 1))) return rc;
   (vst ? m->n_vstream : m->n_full_predict) += 1;
   m->v_n = m->NL + m->NH;
-  HIP_TRY(hipMemcpyAsync(mu, hd[0].mu, sizeof(double) * m->M, hipMemcpyDefault, c->stream));
-  HIP_TRY(hipMemcpyAsync(var, hd[0].var, sizeof(double) * m->M, hipMemcpyDefault, c->stream));
+  bool staged = false;
+  if ((rc = start_out(c, mu, var, hd[0].mu, m->M, staged))) return rc;
   if ((rc = release_slot(c, slot))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
+  finish_out(c, mu, var, m->M, staged);
   return MFGP_OK;
 }
 

@@ -443,3 +443,45 @@ def test_headline_batch_row_splits_vs_full(full_ctx, B):
         assert _err(mu[b], var[b], mu_f[b], var_f[b], HYP_MF) < 1e-8
         assert vm[b] == np.amax(var[b]) and va[b] == int(np.argmax(var[b]))
     assert all(m.stats()["vstream"] >= 1 and m.stats()["inc_factor"] >= 1 for m in inc)
+
+
+@pytest.mark.parametrize("kind", ["sf", "mf"])
+def test_deferred_appends_vs_oracle(kind):
+    """Deferred appends (mfgp_ctx_set_deferred_appends): appends stage their rows and the
+    predict runs the bordered append and the one-pass predict as one launch. Sequences of
+    single and repeated appends (staged rows up to KINC, then beyond it: a full refactor),
+    each predict against the oracle."""
+    from mfgp_coverage_amd import _lib
+    ctx = _lib.Context(0)
+    ctx.set_deferred_appends(True)
+    Xs, X, y = _points(40, 400, seed=11, ongrid=True)
+    NL = 0 if kind == "sf" else 150
+    n = NL + 120
+    m, hyp = _model(ctx, kind, X[:n], y[:n], NL, Xs)
+    m.predict()
+    for ks in ([8], [1], [4, 4], [16], [0], [8, 8], [5, 9, 3], [2]):
+        for kk in ks:
+            m.append(X[n:n + kk], y[n:n + kk])
+            n += kk
+        mu, var = m.predict()
+        mu_r, var_r = _ref(kind, X[:n], y[:n], NL, Xs, hyp)
+        assert _err(mu, var, mu_r, var_r, hyp) < TOL, (ks, _err(mu, var, mu_r, var_r, hyp))
+    st = m.stats()
+    assert st["inc_factor"] >= 6 and st["full_factor"] >= 2, st   # [5, 9, 3] exceeds KINC: refactor
+
+
+def test_deferred_append_not_pd_raises_at_predict():
+    """Deferred, the non-PD bordered step of test_incremental_not_pd_raises is reported by
+    the predict that runs it (the eager default reports it from the append)."""
+    from mfgp_coverage_amd import _lib
+    ctx = _lib.Context(0)
+    ctx.set_deferred_appends(True)
+    Xs, X, y = _points(24, 30, seed=2, ongrid=True)
+    hyp = np.array([0.0, 0.0, -1.0, 0.0, -3.0, -1.0, -1.0, 2.0, -20.0])
+    m = _lib.Model(ctx, _lib.MF, hyp, -1.0)
+    m.set_grid(Xs)
+    m.set_data(X[:20], y[:20], np.empty((0, 2)), np.empty(0))
+    m.predict()
+    m.append(X[20:21], y[20:21])
+    with pytest.raises(np.linalg.LinAlgError):
+        m.predict()
