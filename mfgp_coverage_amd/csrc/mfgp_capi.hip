@@ -79,10 +79,12 @@ struct mfgp_ctx {
   bool fused = true;          // bordered append + one-pass predict in one launch (k_inc_stream)
   bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
   // pinned host staging: predict outputs bound for pageable memory, status words
-  double* h_out = nullptr;
+  double* h_out = nullptr;       // mapped: the kernels write host-bound outputs here
+  double* h_out_dev = nullptr;   // its device address
   size_t h_out_bytes = 0;
   int* h_status = nullptr;
   size_t h_status_n = 0;
+
   int ncu = 256;              // compute units (hipDeviceProp multiProcessorCount)
 };
 
@@ -214,8 +216,12 @@ int ensure_h_out(mfgp_ctx* c, size_t bytes) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->h_out) HIP_TRY(hipHostFree(c->h_out));
   c->h_out = nullptr;
+  c->h_out_dev = nullptr;
   c->h_out_bytes = 0;
-  HIP_TRY(hipHostMalloc(&c->h_out, bytes, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc(&c->h_out, bytes, hipHostMallocMapped));
+  void* dev = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&dev, c->h_out, 0));
+  c->h_out_dev = static_cast<double*>(dev);
   c->h_out_bytes = bytes;
   return MFGP_OK;
 }
@@ -489,19 +495,21 @@ int read_status(mfgp_model* m) {
 
 bool is_device_ptr(const void* p);
 
-// mu / var ([M] each, contiguous at src on the device) into the caller's buffers:
-// device buffers by device copies, host buffers through the pinned staging buffer
-// (one DMA; the host copies happen in finish_out after the stream is synchronized).
-int start_out(mfgp_ctx* c, double* mu, double* var, const double* src, int64_t M, bool& staged) {
+// Where the predict kernels write mu / var ([M] each): the caller's buffers when
+// both are device memory, else the mapped pinned staging buffer (the kernels'
+// epilogues store over the bus while the stream runs; finish_out copies it into
+// the caller's host buffers once the stream is synchronized).
+int out_targets(mfgp_ctx* c, double* mu, double* var, int64_t M, double*& kmu, double*& kvar, bool& staged) {
   staged = !(is_device_ptr(mu) && is_device_ptr(var));
   if (!staged) {
-    HIP_TRY(hipMemcpyAsync(mu, src, sizeof(double) * M, hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(var, src + M, sizeof(double) * M, hipMemcpyDeviceToDevice, c->stream));
+    kmu = mu;
+    kvar = var;
     return MFGP_OK;
   }
   int rc = ensure_h_out(c, sizeof(double) * 2 * (size_t)M);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(c->h_out, src, sizeof(double) * 2 * (size_t)M, hipMemcpyDeviceToHost, c->stream));
+  kmu = c->h_out_dev;
+  kvar = c->h_out_dev + M;
   return MFGP_OK;
 }
 
@@ -1020,13 +1028,10 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   if (m->M > 0 && !factor_current(m) && can_inc_factor(m)) {
     // a staged (deferred) append: the bordered append and the one-pass predict
     // as one launch when V is resident (the batched path for one model)
-    const size_t ob2 = sizeof(double) * 2 * (size_t)m->M;
-    if ((rc = ensure_ws(c, ob2))) return rc;
-    double* mu_d = c->ws;
-    double* var_d = mu_d + m->M;
-    rc = batch_run(&m, 1, nullptr, nullptr, nullptr, mu_d, var_d, nullptr, nullptr, MFGP_ASYNC, true, true);
+    double *kmu = nullptr, *kvar = nullptr;
     bool staged = false;
-    if (rc == MFGP_OK) rc = start_out(c, mu, var, mu_d, m->M, staged);
+    if ((rc = out_targets(c, mu, var, m->M, kmu, kvar, staged))) return rc;
+    rc = batch_run(&m, 1, nullptr, nullptr, nullptr, kmu, kvar, nullptr, nullptr, MFGP_ASYNC, true, true);
     if (rc == MFGP_OK) rc = mfgp_ctx_synchronize(c);
     if (rc == MFGP_OK) finish_out(c, mu, var, m->M, staged);
     if (rc != MFGP_OK) m->factored = false;   // a failed step leaves no usable factor
@@ -1035,14 +1040,15 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   if ((rc = update_factor(m))) return rc;
   if (m->M == 0) return MFGP_OK;
   if ((rc = ensure_v(m))) return rc;
-  const size_t ob = sizeof(double) * 2 * (size_t)m->M;
-  if ((rc = ensure_ws(c, ob))) return rc;
+  double *kmu = nullptr, *kvar = nullptr;
+  bool staged = false;
+  if ((rc = out_targets(c, mu, var, m->M, kmu, kvar, staged))) return rc;
   int slot;
   GPDesc* hd = acquire_slot(c, slot, rc);
   if (!hd) return rc;
   fill_desc(hd[0], m);
-  hd[0].mu = c->ws;
-  hd[0].var = hd[0].mu + m->M;
+  hd[0].mu = kmu;
+  hd[0].var = kvar;
   const bool vst = can_vstream(m);
   set_vstream_rows(hd[0], m);
   set_rsplit(c, hd, 1);
@@ -1051,8 +1057,6 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   if ((rc = vst ? enqueue_vstream(c, dd, hd, 1) : enqueue_predict(c, dd, hd, 1))) return rc;
   (vst ? m->n_vstream : m->n_full_predict) += 1;
   m->v_n = m->NL + m->NH;
-  bool staged = false;
-  if ((rc = start_out(c, mu, var, hd[0].mu, m->M, staged))) return rc;
   if ((rc = release_slot(c, slot))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   finish_out(c, mu, var, m->M, staged);
