@@ -78,10 +78,7 @@ struct mfgp_ctx {
   bool incremental = true;
   bool fused = true;          // bordered append + one-pass predict in one launch (k_inc_stream)
   bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
-  // pinned host staging: predict outputs bound for pageable memory, status words
-  double* h_out = nullptr;       // mapped: the kernels write host-bound outputs here
-  double* h_out_dev = nullptr;   // its device address
-  size_t h_out_bytes = 0;
+  // pinned host staging of the status words
   int* h_status = nullptr;
   size_t h_status_n = 0;
 
@@ -123,6 +120,15 @@ struct mfgp_model {
   // the compact bordered rows in iscr (inc_l21c_offset) hold rows [l21c_n0, l21c_N)
   // bordered onto l21c_n0 factor rows (-1: none)
   int64_t l21c_n0 = -1, l21c_N = -1;
+  // speculative predict: an (eager) append that follows the pattern append ->
+  // predict runs the bordered append and the one-pass predict as one launch and
+  // keeps mu | var in `spec_out` (mapped pinned, [2][M]) for the predict that
+  // follows; any change to the model drops them
+  double* spec_out = nullptr;
+  double* spec_out_dev = nullptr;
+  int64_t spec_cap = 0;
+  bool spec_valid = false;
+  bool pred_since_append = false;   // a predict came after the last append
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0;
 };
@@ -208,21 +214,6 @@ int drain_timing(mfgp_ctx* c) {
     c->pool.push_back(p.b);
   }
   c->pending.clear();
-  return MFGP_OK;
-}
-
-int ensure_h_out(mfgp_ctx* c, size_t bytes) {
-  if (bytes <= c->h_out_bytes) return MFGP_OK;
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  if (c->h_out) HIP_TRY(hipHostFree(c->h_out));
-  c->h_out = nullptr;
-  c->h_out_dev = nullptr;
-  c->h_out_bytes = 0;
-  HIP_TRY(hipHostMalloc(&c->h_out, bytes, hipHostMallocMapped));
-  void* dev = nullptr;
-  HIP_TRY(hipHostGetDevicePointer(&dev, c->h_out, 0));
-  c->h_out_dev = static_cast<double*>(dev);
-  c->h_out_bytes = bytes;
   return MFGP_OK;
 }
 
@@ -495,28 +486,47 @@ int read_status(mfgp_model* m) {
 
 bool is_device_ptr(const void* p);
 
-// Where the predict kernels write mu / var ([M] each): the caller's buffers when
-// both are device memory, else the mapped pinned staging buffer (the kernels'
-// epilogues store over the bus while the stream runs; finish_out copies it into
-// the caller's host buffers once the stream is synchronized).
-int out_targets(mfgp_ctx* c, double* mu, double* var, int64_t M, double*& kmu, double*& kvar, bool& staged) {
-  staged = !(is_device_ptr(mu) && is_device_ptr(var));
-  if (!staged) {
+// The model's mapped pinned result buffer [2][M] (spec_out): host-bound predict
+// outputs are written there by the kernels over the bus and kept, so that the
+// predicts of an unchanged model return them (the same bits, no launch).
+int ensure_spec_out(mfgp_model* m) {
+  if (m->spec_cap >= m->M) return MFGP_OK;
+  mfgp_ctx* c = m->ctx;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (m->spec_out) HIP_TRY(hipHostFree(m->spec_out));
+  m->spec_out = nullptr;
+  m->spec_out_dev = nullptr;
+  m->spec_cap = 0;
+  m->spec_valid = false;
+  HIP_TRY(hipHostMalloc(&m->spec_out, sizeof(double) * 2 * (size_t)m->M, hipHostMallocMapped));
+  void* dev = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&dev, m->spec_out, 0));
+  m->spec_out_dev = static_cast<double*>(dev);
+  m->spec_cap = m->M;
+  return MFGP_OK;
+}
+
+// Where the predict kernels write mu / var: the caller's buffers when both are
+// device memory, else the model's result buffer (model_out_done copies it out).
+int model_out(mfgp_model* m, double* mu, double* var, double*& kmu, double*& kvar, bool& host) {
+  host = !(is_device_ptr(mu) && is_device_ptr(var));
+  if (!host) {
     kmu = mu;
     kvar = var;
     return MFGP_OK;
   }
-  int rc = ensure_h_out(c, sizeof(double) * 2 * (size_t)M);
+  int rc = ensure_spec_out(m);
   if (rc) return rc;
-  kmu = c->h_out_dev;
-  kvar = c->h_out_dev + M;
+  kmu = m->spec_out_dev;
+  kvar = m->spec_out_dev + m->M;
   return MFGP_OK;
 }
 
-void finish_out(const mfgp_ctx* c, double* mu, double* var, int64_t M, bool staged) {
-  if (!staged) return;
-  std::memcpy(mu, c->h_out, sizeof(double) * M);
-  std::memcpy(var, c->h_out + M, sizeof(double) * M);
+void model_out_done(mfgp_model* m, double* mu, double* var, bool host) {
+  if (!host) return;
+  std::memcpy(mu, m->spec_out, sizeof(double) * m->M);
+  std::memcpy(var, m->spec_out + m->M, sizeof(double) * m->M);
+  m->spec_valid = true;
 }
 
 int ensure_sync(mfgp_model* m) {
@@ -720,7 +730,6 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
   for (int i = 0; i < RING; ++i) (void)hipEventDestroy(c->ring_ev[i]);
   if (c->ws) (void)hipFree(c->ws);
   if (c->d_ring) (void)hipFree(c->d_ring);
-  if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->h_status) (void)hipHostFree(c->h_status);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -835,6 +844,7 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
 void mfgp_model_destroy(mfgp_model* m) {
   if (!m) return;
   if (m->ctx) (void)hipStreamSynchronize(m->ctx->stream);
+  if (m->spec_out) (void)hipHostFree(m->spec_out);
   if (m->X) (void)hipFree(m->X);
   if (m->y) (void)hipFree(m->y);
   if (m->A) (void)hipFree(m->A);
@@ -902,6 +912,7 @@ int mfgp_model_set_hyp(mfgp_model* m, const double* hyp, int nhyp, double jitter
   if (rc) return rc;
   if (!hyp || nhyp != m->nhyp)
     return set_err(MFGP_ERR_ARG, "Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)");
+  if (jitter != m->jitter || std::memcmp(hyp, m->hyp, sizeof(double) * nhyp) != 0) m->spec_valid = false;
   std::memcpy(m->hyp, hyp, sizeof(double) * nhyp);
   m->jitter = jitter;
   return MFGP_OK;
@@ -955,6 +966,7 @@ int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
   if (M < 0 || (M > 0 && !xs)) return set_err(MFGP_ERR_ARG, "bad grid");
   mfgp_ctx* c = m->ctx;
   m->v_n = 0;   // V columns belong to the previous grid
+  m->spec_valid = false;
   if (M > m->Mcap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (m->grid) HIP_TRY(hipFree(m->grid));
@@ -980,6 +992,7 @@ int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL,
   if (rc) return rc;
   if (NL < 0 || NH < 0) return set_err(MFGP_ERR_ARG, "negative sizes");
   if (m->kind == MFGP_SF && NL != 0) return set_err(MFGP_ERR_ARG, "SF model takes its data in the H slots");
+  m->spec_valid = false;
   if ((rc = ensure_cap(m, NL + NH))) return rc;
   m->NL = NL;
   m->NH = NH;
@@ -989,22 +1002,31 @@ int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL,
   return factor_one(m);
 }
 
+int spec_append_predict(mfgp_model* m);
+
 int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
   int rc = check_model(m);
   if (rc) return rc;
   if (k < 0) return set_err(MFGP_ERR_ARG, "negative k");
+  m->spec_valid = false;
+  const bool spec = m->pred_since_append;   // the last append was followed by a predict
+  m->pred_since_append = false;
   const int64_t n = m->NL + m->NH;
   if ((rc = ensure_cap(m, n + k))) return rc;
   if ((rc = copy_rows(m, n, X, y, k))) return rc;
   m->NH += k;
   if (!m->ctx->incremental) m->factored = false;   // reference behaviour: refactor from scratch
   if (m->ctx->deferred && can_inc_factor(m)) return MFGP_OK;   // the next factor user runs the append
+  if (spec && m->ctx->fused && k > 0 && m->M > 0 && can_inc_factor(m) && m->V && m->v_n == m->factor_N &&
+      m->vtiles >= ntiles_grid(m->M))
+    return spec_append_predict(m);
   return update_factor(m);
 }
 
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
   int rc = check_model(m);
   if (rc) return rc;
+  if (n_keep_hifi != m->NH) m->spec_valid = false;
   if (n_keep_hifi < 0 || n_keep_hifi > m->NH) return set_err(MFGP_ERR_ARG, "bad truncate size");
   if (n_keep_hifi != m->NH) {
     m->NH = n_keep_hifi;
@@ -1020,20 +1042,51 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
                      double* mu, double* var, double* vmax, int64_t* vargmax, int flags, bool do_factor,
                      bool do_predict);
 
+// The speculative form of an eager append (mfgp_append): the bordered append and
+// the one-pass predict as one launch, synchronised (a non-PD step is reported
+// here, as by update_factor), with mu | var kept for the next predict.
+int spec_append_predict(mfgp_model* m) {
+  mfgp_ctx* c = m->ctx;
+  int rc = ensure_spec_out(m);
+  if (rc) return rc;
+  rc = batch_run(&m, 1, nullptr, nullptr, nullptr, m->spec_out_dev, m->spec_out_dev + m->M, nullptr, nullptr,
+                     MFGP_ASYNC, true, true);
+  if (rc == MFGP_OK) rc = mfgp_ctx_synchronize(c);
+  if (rc != MFGP_OK) {
+    m->factored = false;   // a failed step leaves no usable factor
+    return rc;
+  }
+  m->spec_valid = true;
+  return MFGP_OK;
+}
+
 int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   int rc = check_model(m);
   if (rc) return rc;
   mfgp_ctx* c = m->ctx;
   if (m->M > 0 && (!mu || !var)) return set_err(MFGP_ERR_ARG, "null output");
+  m->pred_since_append = true;
+  if (m->spec_valid && factor_current(m)) {   // kept from the last predict or the append (spec_append_predict)
+    const size_t b = sizeof(double) * (size_t)m->M;
+    if (is_device_ptr(mu) && is_device_ptr(var)) {
+      HIP_TRY(hipMemcpyAsync(mu, m->spec_out_dev, b, hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(var, m->spec_out_dev + m->M, b, hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+    } else {
+      std::memcpy(mu, m->spec_out, b);
+      std::memcpy(var, m->spec_out + m->M, b);
+    }
+    return MFGP_OK;
+  }
   if (m->M > 0 && !factor_current(m) && can_inc_factor(m)) {
     // a staged (deferred) append: the bordered append and the one-pass predict
     // as one launch when V is resident (the batched path for one model)
     double *kmu = nullptr, *kvar = nullptr;
-    bool staged = false;
-    if ((rc = out_targets(c, mu, var, m->M, kmu, kvar, staged))) return rc;
+    bool host = false;
+    if ((rc = model_out(m, mu, var, kmu, kvar, host))) return rc;
     rc = batch_run(&m, 1, nullptr, nullptr, nullptr, kmu, kvar, nullptr, nullptr, MFGP_ASYNC, true, true);
     if (rc == MFGP_OK) rc = mfgp_ctx_synchronize(c);
-    if (rc == MFGP_OK) finish_out(c, mu, var, m->M, staged);
+    if (rc == MFGP_OK) model_out_done(m, mu, var, host);
     if (rc != MFGP_OK) m->factored = false;   // a failed step leaves no usable factor
     return rc;
   }
@@ -1041,8 +1094,8 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   if (m->M == 0) return MFGP_OK;
   if ((rc = ensure_v(m))) return rc;
   double *kmu = nullptr, *kvar = nullptr;
-  bool staged = false;
-  if ((rc = out_targets(c, mu, var, m->M, kmu, kvar, staged))) return rc;
+  bool host = false;
+  if ((rc = model_out(m, mu, var, kmu, kvar, host))) return rc;
   int slot;
   GPDesc* hd = acquire_slot(c, slot, rc);
   if (!hd) return rc;
@@ -1059,7 +1112,7 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   m->v_n = m->NL + m->NH;
   if ((rc = release_slot(c, slot))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
-  finish_out(c, mu, var, m->M, staged);
+  model_out_done(m, mu, var, host);
   return MFGP_OK;
 }
 
@@ -1101,6 +1154,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
   int rc = MFGP_OK;
   for (int i = 0; i < count; ++i) {
     if ((rc = check_model(models[i]))) return rc;
+    models[i]->spec_valid = false;
     if (models[i]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
     if (k && k[i] < 0) return set_err(MFGP_ERR_ARG, "negative k");
     if (!do_factor && !factor_current(models[i]))

@@ -176,7 +176,9 @@ def test_clone_keeps_resident_state(gp_mod):
         j = int(np.argmax(v))
         tmp.updt_hifi(Xs[j:j + 1], mu0[j:j + 1])
     st = tmp._dev().stats()
-    assert st["inc_factor"] == 4 and st["full_predict"] == 0 and st["vstream"] == 4
+    # each append follows a predict, so it runs the one-pass predict with it (the
+    # speculative form of an eager append, kept for the next predict): 1 + 4 streams
+    assert st["inc_factor"] == 4 and st["full_predict"] == 0 and st["vstream"] == 5
     mu1, cov1 = m.predict(Xs)
     np.testing.assert_array_equal(mu1, mu0)
     np.testing.assert_array_equal(np.diag(cov1), np.diag(cov0))
@@ -485,3 +487,60 @@ def test_deferred_append_not_pd_raises_at_predict():
     m.append(X[20:21], y[20:21])
     with pytest.raises(np.linalg.LinAlgError):
         m.predict()
+
+
+def test_speculative_predict_after_append():
+    """An eager append that follows a predict runs the bordered append and the one-pass
+    predict in one launch and keeps the result for the next predict. Every change to
+    the model in between (more rows, hyperparameters, grid) must drop it; repeated
+    predicts return the same bits; a non-PD append still raises at the append."""
+    from mfgp_coverage_amd import _lib
+    Xs, X, y = _points(36, 400, seed=13, ongrid=True)
+    NL, n = 150, 270
+    m, hyp = _model(_lib.context(), "mf", X[:n], y[:n], NL, Xs)
+    m.predict()
+    for step, kk in enumerate((8, 3, 8, 1)):
+        m.append(X[n:n + kk], y[n:n + kk])
+        n += kk
+        if step == 2:                      # a second append before the predict: the first's result is stale
+            m.append(X[n:n + 2], y[n:n + 2])
+            n += 2
+        mu, var = m.predict()
+        mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs, hyp)
+        assert _err(mu, var, mu_r, var_r, hyp) < TOL, step
+        mu2, var2 = m.predict()
+        np.testing.assert_array_equal(mu2, mu)
+        np.testing.assert_array_equal(var2, var)
+    # a hyperparameter change after the append: the kept result is not used
+    m.append(X[n:n + 4], y[n:n + 4])
+    n += 4
+    hyp2 = hyp.copy()
+    hyp2[2] += 0.1
+    m.set_hyp(hyp2, 1e-8)
+    mu, var = m.predict()
+    mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs, hyp2)
+    assert _err(mu, var, mu_r, var_r, hyp2) < TOL
+    # a grid change after the append
+    m.set_hyp(hyp, 1e-8)
+    m.predict()
+    m.append(X[n:n + 4], y[n:n + 4])
+    n += 4
+    Xs2 = Xs[::3].copy()
+    m.set_grid(Xs2)
+    mu, var = m.predict()
+    mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs2, hyp)
+    assert _err(mu, var, mu_r, var_r, hyp) < TOL
+
+
+def test_speculative_append_not_pd_raises_at_append():
+    from mfgp_coverage_amd import _lib
+    Xs, X, y = _points(24, 30, seed=2, ongrid=True)
+    hyp = np.array([0.0, 0.0, -1.0, 0.0, -3.0, -1.0, -1.0, 2.0, -20.0])
+    m = _lib.Model(_lib.context(), _lib.MF, hyp, -1.0)
+    m.set_grid(Xs)
+    m.set_data(X[:20], y[:20], np.empty((0, 2)), np.empty(0))
+    m.predict()
+    m.append(X[20:20], y[20:20])           # k = 0
+    m.predict()
+    with pytest.raises(np.linalg.LinAlgError):
+        m.append(X[20:21], y[20:21])       # speculative form (after a predict): raises here
