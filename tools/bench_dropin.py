@@ -26,4 +26,7 @@ for s in range(T):
     v = np.diag(cov); vm = np.amax(cov)
     t3 = time.perf_counter()
     ts["updt_hifi"].append(t1 - t0); ts["predict"].append(t2 - t1); ts["np.diag+amax"].append(t3 - t2)
-print("deferred" if DEFERRED else "eager", {k: round(1e6 * float(np.median(v[10:])), 1) for k, v in ts.items()}, "us (median)")
+import json
+res = {"mode": "deferred" if DEFERRED else "eager", "grid": 128, "N_L": 1024, "N_H": 1024, "agents": 8,
+       "steps_timed": T - 10, "us_median": {k: round(1e6 * float(np.median(v[10:])), 1) for k, v in ts.items()}}
+print(json.dumps(res))
