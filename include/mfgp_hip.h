@@ -106,12 +106,17 @@ int mfgp_set_grid(mfgp_model* m, const double* xstar, int64_t M);
 int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL,
                   const double* XH, const double* yH, int64_t NH);
 
-/* updt (gp:257-268) / updt_hifi (gp:531-542): append k >= 0 rows and refactor. */
+/* updt (gp:257-268) / updt_hifi (gp:531-542): append k >= 0 rows and refactor.
+ * When the previous append was followed by a predict (the simulator's step), the
+ * append also runs the one-pass predict in the same launch and keeps the result
+ * for the next mfgp_predict; a non-PD step is still reported here. */
 int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k);
 
 /* predict (gp:121-148 / gp:401-438): posterior mean and the diagonal of the
  * posterior covariance at every grid cell (the only part the callers use,
- * simulator.py:301, 341, 672, 685, 842, 855, 1014). mu, var: [M]. */
+ * simulator.py:301, 341, 672, 685, 842, 855, 1014). mu, var: [M], host or
+ * device memory. Results for host buffers are kept with the model: predicts of
+ * an unchanged model return them again (the same bits, no launch). */
 int mfgp_predict(mfgp_model* m, double* mu, double* var);
 
 /* Sizes and state readers (the Python mirror's .X/.L attributes). */
