@@ -1182,7 +1182,7 @@ __device__ __forceinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int6
 //   phase 1 (partials / L21 solve, L22):  red [0,1088) ssum [1088,1360) K22s [1360,1616) Ts [1616,2640)
 //   phase 2 (new Linv rows):              Ln [0,1024) Ps [1024,2048) Lb [2048,3056)
 //   both:                                 L22s [3056,3312)
-// (26.5 KB: five workgroups of k_inc_stream fit a CU)
+// (26.5 KB: LDS would fit five workgroups of k_inc_stream per CU; its 128 VGPRs allow four)
 constexpr int FIN_LDS = 3312;
 constexpr int LBW = 16;   // Linv_OO columns staged per pass (63 rows x 16 = 1008 doubles)
 
@@ -1928,8 +1928,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
 // before any workgroup that waits for them and are therefore resident (no
 // deadlock); the waits are bounded anyway. The flags hold the launch's epoch
 // (host counter, never 0), so they need no reset. Without tiles nothing waits.
-// Five workgroups per CU (26.5 KB of LDS, <= 102 VGPRs): at the headline size
-// (8 GPs: 128 producers + 1024 cell workgroups) every workgroup is resident.
+// Four workgroups per CU (128 VGPRs; 26.5 KB of LDS): at the headline size
+// (8 GPs: 128 producers + 1024 cell workgroups) 1024 are resident at once and
+// the last 128 cell workgroups take the producers' slots as they finish (9-15 us).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream(
     const GPDesc* __restrict__ descs) {
