@@ -289,7 +289,9 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{a.hyp} MFGP seed ensemble"
-                            f"{' (BASELINE configs[3])' if default_cfg else ''}: {B} seeds/GPU, "
+                            f"{' (BASELINE configs[3])' if default_cfg else ''}"
+                            f"{' (BASELINE configs[4] sizes, computed in fp64)' if (G, NL, NH, B) == (256, 4096, 4096, 32) else ''}"
+                            f": {B} seeds/GPU, "
                             f"{G}x{G} grid (M={M}), N_L={NL} lofi + N_H={NH} hifi ({NH0} + {k} new agent "
                             f"samples appended per update), factor update + mean/var at every cell, fp64",
                 "update": ("incremental, one launch per step (k_inc_stream): bordered-Cholesky append + one "
