@@ -209,13 +209,17 @@ def context(device=None):
 class Model:
     """Owning handle of one device-resident GP (mfgp_model)."""
 
-    def __init__(self, ctx, kind, hyp, jitter, handle=None):
+    def __init__(self, ctx, kind, hyp, jitter, handle=None, dtype=F64):
+        """dtype: F64 (default; everything in fp64, the reference's precision) or F32
+        (the resident V = L^-1 psi^T -- the only O(M N) state -- stored and streamed in
+        fp32; factor, solves and reductions stay fp64; BASELINE configs[4])."""
         self.ctx = ctx
         self.kind = kind
+        self.dtype = dtype
         if handle is None:
             hyp = np.ascontiguousarray(hyp, dtype=np.float64)
             h = ctypes.c_void_p()
-            check(lib().mfgp_model_create(ctx.handle, kind, F64, ptr(hyp), int(hyp.shape[0]),
+            check(lib().mfgp_model_create(ctx.handle, kind, int(dtype), ptr(hyp), int(hyp.shape[0]),
                                           float(jitter), ctypes.byref(h)))
             handle = h
         self.handle = handle
@@ -229,7 +233,7 @@ class Model:
     def clone(self):
         h = ctypes.c_void_p()
         check(lib().mfgp_clone(self.handle, ctypes.byref(h)))
-        return Model(self.ctx, self.kind, None, None, handle=h)
+        return Model(self.ctx, self.kind, None, None, handle=h, dtype=self.dtype)
 
     def set_hyp(self, hyp, jitter):
         hyp = np.ascontiguousarray(hyp, dtype=np.float64).reshape(-1)

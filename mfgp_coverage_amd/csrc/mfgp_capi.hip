@@ -43,6 +43,8 @@ int set_err(int code, const char* fmt, ...) {
 
 constexpr int RING = 64;       // descriptor upload slots
 constexpr int MAXB = 256;      // GPs per launch
+constexpr int64_t MAX_FULL_CAP = 16319;   // largest training capacity the full predict serves (ld <= 16383)
+constexpr size_t F32_SCRATCH = size_t(16) << 30;   // bytes of fp64 V scratch for MFGP_F32 full predicts
 
 struct EvPair {
   hipEvent_t a, b;
@@ -71,8 +73,14 @@ struct mfgp_ctx {
   std::vector<hipEvent_t> pool;
   double t_predict = 0.0, t_factor = 0.0;
   int64_t n_predict = 0, n_factor = 0;
-  // deferred status words of ASYNC batches
-  std::vector<int*> async_status;
+  // deferred status words of ASYNC batches, with the model each belongs to (a
+  // failed factor is dropped from its model at mfgp_ctx_synchronize)
+  std::vector<std::pair<mfgp_model*, int*>> async_status;
+  // fp64 scratch in which the full predicts of MFGP_F32 models compute V
+  // (k_predict re-reads its own rows), then rounded into their fp32 V
+  double* vscr = nullptr;
+  size_t vscr_bytes = 0;
+  int f32_group = 1;          // full predicts per k_predict launch that share vscr
   // incremental append / predict (bordered Cholesky + resident V); off = always
   // refactor and recompute V from scratch, as the reference does
   bool incremental = true;
@@ -88,6 +96,7 @@ struct mfgp_ctx {
 struct mfgp_model {
   mfgp_ctx* ctx = nullptr;
   int kind = MFGP_SF;
+  int dtype = MFGP_F64;     // precision of the resident V (MFGP_F32: fp32 storage and stream)
   int nhyp = 4;
   double hyp[9] = {0};
   double jitter = 1e-8;
@@ -111,8 +120,9 @@ struct mfgp_model {
   int64_t M = 0, Mcap = 0;
   double* grid = nullptr;
   GridLattice lat{};        // lattice structure of the grid (nx == 0: none)
-  // resident V = L^-1 psi^T [vtiles][vld][PBM]; rows [0, v_n) valid for the current factor and grid
-  double* V = nullptr;
+  // resident V = L^-1 psi^T [vtiles][vld][PBM] (double, or float for MFGP_F32);
+  // rows [0, v_n) valid for the current factor and grid
+  void* V = nullptr;
   int64_t vld = 0, vtiles = 0, v_n = 0;
   double* tred = nullptr;     // [vtiles][2] per-tile (max, argmax) of var, then the tiles' arrival counter
   unsigned* sync = nullptr;   // k_inc_stream hand-off words {arrivals, L21 ready, L22 ready} (zeroed)
@@ -248,6 +258,9 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   if (need <= m->cap && m->A) return MFGP_OK;
   mfgp_ctx* c = m->ctx;
   int64_t cap = std::max<int64_t>({need, m->cap + m->cap / 2, 63});
+  // the full predict (k_predict) addresses A through a 32-bit buffer descriptor:
+  // ld <= 16383, i.e. a capacity of at most MAX_FULL_CAP rows; 1.5x growth stops there
+  if (cap > MAX_FULL_CAP && need <= MAX_FULL_CAP) cap = MAX_FULL_CAP;
   int64_t ld = round_up(cap + 1, NB);
   cap = ld - 1;
   double *X = nullptr, *y = nullptr, *A = nullptr, *Li = nullptr, *zv = nullptr, *isc = nullptr;
@@ -297,17 +310,20 @@ int ensure_cap(mfgp_model* m, int64_t need) {
 }
 
 // Resident V for the current capacity and grid (contents kept when it fits).
+size_t v_elem(const mfgp_model* m) { return m->dtype == MFGP_F32 ? sizeof(float) : sizeof(double); }
+
 int ensure_v(mfgp_model* m) {
   const int64_t vld = round_up(m->cap, PRB);
   const int64_t tiles = ntiles_grid(m->M);
   if (m->V && m->vld == vld && m->vtiles >= tiles) return MFGP_OK;
   hipStream_t s = m->ctx->stream;
-  double* V = nullptr;
-  HIP_TRY(hipMalloc(&V, sizeof(double) * (size_t)tiles * vld * PBM));
+  const size_t es = v_elem(m);
+  void* V = nullptr;
+  HIP_TRY(hipMalloc(&V, es * (size_t)tiles * vld * PBM));
   if (m->V && m->v_n > 0 && m->vtiles >= tiles && m->vld >= m->v_n) {
     // capacity grew: move the valid rows of every tile to the new row stride
-    HIP_TRY(hipMemcpy2DAsync(V, sizeof(double) * vld * PBM, m->V, sizeof(double) * m->vld * PBM,
-                             sizeof(double) * m->v_n * PBM, tiles, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpy2DAsync(V, es * vld * PBM, m->V, es * m->vld * PBM, es * m->v_n * PBM, tiles,
+                             hipMemcpyDeviceToDevice, s));
   } else {
     m->v_n = 0;
   }
@@ -368,7 +384,9 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.Linv = m->Linv;
   d.grid = m->grid;
   d.lat = m->lat;
-  d.V = m->V;
+  d.V = m->dtype == MFGP_F64 ? static_cast<double*>(m->V) : nullptr;
+  d.Vf = m->dtype == MFGP_F32 ? static_cast<float*>(m->V) : nullptr;
+  d.vf32 = m->dtype == MFGP_F32 ? 1 : 0;
   d.zv = m->zv;
   d.iscr = m->iscr;
   d.l21c = m->iscr ? m->iscr + inc_l21c_offset(m->cap) : nullptr;
@@ -436,19 +454,46 @@ int enqueue_inc_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
   EvPair ev{};
   int rc = ev_begin(c, ev, 1);
   if (rc) return rc;
-  HIP_TRY(launch_inc_factor(dd, count, max_np, c->stream));
+  HIP_TRY(launch_inc_factor(dd, count, max_np, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
 int enqueue_vstream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_ct = 0;
-  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_wg(hd[i].M, hd[i].rsplit));
+  for (int i = 0; i < count; ++i) max_ct = std::max(max_ct, ntiles_wg(hd[i].M, hd[i].rsplit, hd[i].vf32));
   if (max_ct == 0) return MFGP_OK;
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
-  HIP_TRY(launch_vstream(dd, count, max_ct, c->stream));
+  HIP_TRY(launch_vstream(dd, count, max_ct, hd[0].vf32, c->stream));
   return ev_end(c, ev);
+}
+
+// fp64 V bytes of a full predict of descriptor d (k_predict's image of V).
+size_t v64_bytes(const GPDesc& d) { return sizeof(double) * (size_t)ntiles_grid(d.M) * d.vld * PBM; }
+
+// MFGP_F32 full predicts compute V in fp64 scratch (k_predict's left-looking
+// solve re-reads its own rows) and round it into the resident fp32 V
+// (k_vnarrow): point the descriptors at slots of the context's scratch, as many
+// GPs per launch as F32_SCRATCH holds (at least one). Call before the upload.
+int assign_predict_scratch(mfgp_ctx* c, GPDesc* hd, int count) {
+  if (count <= 0 || !hd[0].vf32) return MFGP_OK;
+  size_t per = 0;
+  for (int i = 0; i < count; ++i) per = std::max(per, v64_bytes(hd[i]));
+  per = (per + 255) / 256 * 256;
+  if (per == 0) return MFGP_OK;
+  const int g = (int)std::max<size_t>(1, std::min<size_t>((size_t)count, F32_SCRATCH / per));
+  if (per * g > c->vscr_bytes) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->vscr) HIP_TRY(hipFree(c->vscr));
+    c->vscr = nullptr;
+    c->vscr_bytes = 0;
+    HIP_TRY(hipMalloc(&c->vscr, per * g));
+    c->vscr_bytes = per * g;
+  }
+  c->f32_group = g;
+  for (int i = 0; i < count; ++i) hd[i].V = c->vscr + (per / sizeof(double)) * (i % g);
+  return MFGP_OK;
 }
 
 int enqueue_predict(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
@@ -456,14 +501,26 @@ int enqueue_predict(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   for (int i = 0; i < count; ++i) {
     max_ct = std::max(max_ct, ntiles_grid(hd[i].M));
     // k_predict addresses A through a 32-bit buffer descriptor: 8 * ld^2 < 2^31
-    if (hd[i].ld > 16383)
-      return set_err(MFGP_ERR_ARG, "fused predict supports N <= 16382 training rows (got %lld)", (long long)hd[i].N);
+    if (hd[i].ld > MAX_FULL_CAP + 64)
+      return set_err(MFGP_ERR_ARG,
+                     "the full predict supports a training capacity of at most %lld rows (this model's is %lld, N = %lld)",
+                     (long long)MAX_FULL_CAP, (long long)(hd[i].ld - 1), (long long)hd[i].N);
   }
   if (max_ct == 0) return MFGP_OK;
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
-  HIP_TRY(launch_predict(dd, count, max_ct, c->stream));
+  if (!hd[0].vf32) {
+    HIP_TRY(launch_predict(dd, count, max_ct, c->stream));
+  } else {
+    // groups sharing the scratch run one after the other (stream order)
+    const int g = c->f32_group;
+    for (int g0 = 0; g0 < count; g0 += g) {
+      const int gn = std::min(g, count - g0);
+      HIP_TRY(launch_predict(dd + g0, gn, max_ct, c->stream));
+      HIP_TRY(launch_vnarrow(dd + g0, gn, max_ct, c->stream));
+    }
+  }
   return ev_end(c, ev);
 }
 
@@ -539,11 +596,12 @@ int ensure_sync(mfgp_model* m) {
 // Bordered appends and their one-pass predicts in one k_inc_stream launch.
 int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_blocks = 0;
-  for (int i = 0; i < count; ++i) max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_wg(hd[i].M, hd[i].rsplit));
+  for (int i = 0; i < count; ++i)
+    max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_wg(hd[i].M, hd[i].rsplit, hd[i].vf32));
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
-  HIP_TRY(launch_inc_stream(dd, count, max_blocks, c->stream));
+  HIP_TRY(launch_inc_stream(dd, count, max_blocks, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
@@ -551,6 +609,10 @@ int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
 // workgroups while they fill the chip (~4 per CU), else 64 or 32 cells with the
 // rows split 2 or 4 ways (the drop-in simulator predicts one GP at a time).
 void set_rsplit(const mfgp_ctx* c, GPDesc* hd, int count) {
+  if (count > 0 && hd[0].vf32) {   // the fp32 stream has no row splits
+    for (int i = 0; i < count; ++i) hd[i].rsplit = 1;
+    return;
+  }
   int64_t w1 = 0;
   for (int i = 0; i < count; ++i) w1 += ntiles_wg(hd[i].M);
   const int R = (w1 >= 3 * c->ncu) ? 1 : (2 * w1 >= 3 * c->ncu ? 2 : 4);
@@ -693,7 +755,7 @@ int mfgp_debug_set_stamps(void* p) {
   return MFGP_OK;
 }
 #endif
-const char* mfgp_version(void) { return "mfgp_hip 0.2 gfx950 f64"; }
+const char* mfgp_version(void) { return "mfgp_hip 0.3 gfx950 f64 f32v"; }
 
 int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (!out) return set_err(MFGP_ERR_ARG, "null out");
@@ -729,6 +791,7 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
   for (auto e : c->pool) (void)hipEventDestroy(e);
   for (int i = 0; i < RING; ++i) (void)hipEventDestroy(c->ring_ev[i]);
   if (c->ws) (void)hipFree(c->ws);
+  if (c->vscr) (void)hipFree(c->vscr);
   if (c->d_ring) (void)hipFree(c->d_ring);
   if (c->h_status) (void)hipHostFree(c->h_status);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
@@ -751,11 +814,20 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
   if (rc) return rc;
   // the status words come back through pinned memory with the stream's last copies
   for (size_t i = 0; i < c->async_status.size(); ++i)
-    HIP_TRY(hipMemcpyAsync(c->h_status + i, c->async_status[i], sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_status + i, c->async_status[i].second, sizeof(int), hipMemcpyDeviceToHost,
+                           c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (size_t i = 0; i < c->async_status.size(); ++i) {
     const int st = c->h_status[i];
-    if (st != INT_MAX && rc == MFGP_OK) rc = status_error(st);
+    if (st == INT_MAX) continue;
+    // a failed factor leaves its model without one: the next use refactors (and
+    // raises again), instead of serving the failed factor and its V
+    mfgp_model* m = c->async_status[i].first;
+    m->factored = false;
+    m->v_n = 0;
+    m->l21c_N = -1;
+    m->spec_valid = false;
+    if (rc == MFGP_OK) rc = status_error(st);
   }
   c->async_status.clear();
   return rc;
@@ -820,7 +892,7 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
   if (!c || !out) return set_err(MFGP_ERR_ARG, "null ctx/out");
   *out = nullptr;
   if (kind != MFGP_SF && kind != MFGP_MF) return set_err(MFGP_ERR_ARG, "kind must be MFGP_SF or MFGP_MF");
-  if (dtype != MFGP_F64) return set_err(MFGP_ERR_ARG, "only MFGP_F64 is implemented");
+  if (dtype != MFGP_F64 && dtype != MFGP_F32) return set_err(MFGP_ERR_ARG, "dtype must be MFGP_F64 or MFGP_F32");
   const int want = kind == MFGP_SF ? 4 : 9;
   if (!hyp || nhyp != want)
     return set_err(MFGP_ERR_ARG, "Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)");
@@ -828,6 +900,7 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
   mfgp_model* m = new mfgp_model();
   m->ctx = c;
   m->kind = kind;
+  m->dtype = dtype;
   m->nhyp = nhyp;
   std::memcpy(m->hyp, hyp, sizeof(double) * nhyp);
   m->jitter = jitter;
@@ -843,7 +916,13 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
 
 void mfgp_model_destroy(mfgp_model* m) {
   if (!m) return;
-  if (m->ctx) (void)hipStreamSynchronize(m->ctx->stream);
+  if (m->ctx) {
+    (void)hipStreamSynchronize(m->ctx->stream);
+    // an ASYNC batch's status word of this model dies with it (the work is done)
+    auto& as = m->ctx->async_status;
+    as.erase(std::remove_if(as.begin(), as.end(), [m](const std::pair<mfgp_model*, int*>& e) { return e.first == m; }),
+             as.end());
+  }
   if (m->spec_out) (void)hipHostFree(m->spec_out);
   if (m->X) (void)hipFree(m->X);
   if (m->y) (void)hipFree(m->y);
@@ -865,7 +944,7 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
   if (!out) return set_err(MFGP_ERR_ARG, "null out");
   mfgp_ctx* c = src->ctx;
   mfgp_model* m = nullptr;
-  if ((rc = mfgp_model_create(c, src->kind, MFGP_F64, src->hyp, src->nhyp, src->jitter, &m))) return rc;
+  if ((rc = mfgp_model_create(c, src->kind, src->dtype, src->hyp, src->nhyp, src->jitter, &m))) return rc;
   if ((rc = ensure_cap(m, src->cap))) {
     mfgp_model_destroy(m);
     return rc;
@@ -897,7 +976,7 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
     // resident V (the Choi planner clones a model and keeps appending to the copy, sim:339)
     if (m->factored && src->V && src->v_n > 0 && src->vld == round_up(m->cap, PRB)) {
       if ((rc = ensure_v(m))) return rc;
-      HIP_TRY(hipMemcpyAsync(m->V, src->V, sizeof(double) * (size_t)src->vtiles * src->vld * PBM,
+      HIP_TRY(hipMemcpyAsync(m->V, src->V, v_elem(src) * (size_t)src->vtiles * src->vld * PBM,
                              hipMemcpyDeviceToDevice, c->stream));
       m->v_n = src->v_n;
     }
@@ -1105,6 +1184,7 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   const bool vst = can_vstream(m);
   set_vstream_rows(hd[0], m);
   set_rsplit(c, hd, 1);
+  if (!vst && (rc = assign_predict_scratch(c, hd, 1))) return rc;
   const GPDesc* dd = nullptr;
   if ((rc = upload_slot(c, slot, 1, &dd))) return rc;
   if ((rc = vst ? enqueue_vstream(c, dd, hd, 1) : enqueue_predict(c, dd, hd, 1))) return rc;
@@ -1156,6 +1236,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     if ((rc = check_model(models[i]))) return rc;
     models[i]->spec_valid = false;
     if (models[i]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
+    if (models[i]->dtype != models[0]->dtype)
+      return set_err(MFGP_ERR_ARG, "batch models must share one dtype (MFGP_F64 or MFGP_F32)");
     if (k && k[i] < 0) return set_err(MFGP_ERR_ARG, "negative k");
     if (!do_factor && !factor_current(models[i]))
       return set_err(MFGP_ERR_ARG, "model %d has no current factor (call mfgp_batch_append_factor first)", i);
@@ -1227,7 +1309,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; i < ninc + nfull; ++i) {   // host bookkeeping of the factors enqueued below
         if (i < ninc) mark_inc_factor(order[i]);
         else mark_full_factor(order[i]);
-        c->async_status.push_back(order[i]->status);
+        c->async_status.emplace_back(order[i], order[i]->status);
       }
     }
     // predict descriptors (state after the factor step), ordered
@@ -1276,6 +1358,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       set_rsplit(c, hd + nb, nv);
       for (int i = 0; fuse && i < ninc; ++i) hd[i].rsplit = hd[nb].rsplit;
     }
+    if (np > nv && (rc = assign_predict_scratch(c, hd + nb + nv, np - nv))) return rc;
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
     if (do_factor) {
@@ -1375,12 +1458,15 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
     for (int64_t i = 0; i < 2 * C; ++i) hd[i].rsplit = hd[1].rsplit;
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, (int)(2 * C), &dd))) return fail(rc);
+    const int vf = t->dtype == MFGP_F32 ? 1 : 0;
     for (int64_t it = 0; it < C; ++it) {
       const bool ok = hipSuccess == launch_choi_select(dd + 2 * it, threshold, pts, max_points, c->stream) &&
-                      (c->fused ? hipSuccess == launch_inc_stream(dd + 2 * it, 1, hd[2 * it].nprod + ntiles_wg(M, hd[2 * it].rsplit),
-                                                                   c->stream)
-                                : (hipSuccess == launch_inc_factor(dd + 2 * it, 1, hd[2 * it].nprod, c->stream) &&
-                                   hipSuccess == launch_vstream(dd + 2 * it + 1, 1, ntiles_wg(M, hd[2 * it + 1].rsplit), c->stream)));
+                      (c->fused ? hipSuccess == launch_inc_stream(dd + 2 * it, 1,
+                                                                   hd[2 * it].nprod + ntiles_wg(M, hd[2 * it].rsplit, vf),
+                                                                   vf, c->stream)
+                                : (hipSuccess == launch_inc_factor(dd + 2 * it, 1, hd[2 * it].nprod, vf, c->stream) &&
+                                   hipSuccess == launch_vstream(dd + 2 * it + 1, 1, ntiles_wg(M, hd[2 * it + 1].rsplit, vf),
+                                                                vf, c->stream)));
       if (!ok) return fail(set_err(MFGP_ERR_DEVICE, "sample_points: launch failed"));
     }
     if ((rc = release_slot(c, slot))) return fail(rc);

@@ -12,6 +12,7 @@ namespace mfgp {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 // Generic -> global address space, so loads/stores through descriptor pointers
 // are emitted as global_* (vmcnt only) instead of flat_* (vmcnt + lgkmcnt).
@@ -29,6 +30,12 @@ __device__ __forceinline__ int swz(int k, int i) { return k * NB + (i ^ ((k & 1)
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+// exact f32 (v_mfma_f32_16x16x4_f32 = an fmaf chain). A/B lane maps as the f64
+// form; C/D: lane (r, g) register v holds row 4g + v, column r (the f64 form:
+// row g + 4v).
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // Per-wave 32x32 accumulator = 2x2 MFMA tiles of 16x16.

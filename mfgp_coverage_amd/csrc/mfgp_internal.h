@@ -61,7 +61,9 @@ struct GPDesc {
   double* A;           // [ld,ld] column-major; lower triangle = L after the factor
   double* Linv;        // [nb][NB*NB] column-major inverses of the diagonal blocks of L
   const double* grid;  // [M,2]
-  double* V;           // resident V = L^-1 psi^T: [ceil(M/PBM)][vld][PBM] (tile, row, cell)
+  double* V;           // resident V = L^-1 psi^T: [ceil(M/PBM)][vld][PBM] (tile, row, cell); for an
+                       // MFGP_F32 model: the fp64 scratch a full predict computes V in (k_predict)
+  float* Vf;           // MFGP_F32 model: the resident V stored in fp32, same layout (null for F64)
   double* zv;          // [N] z = L^-1 (y - m)
   double* iscr;        // incremental append scratch: [0] = rows gathered from V, then per-chunk partial sums
   double* l21c;        // compact bordered rows [cap][KINC] inside iscr (inc_l21c_offset)
@@ -89,6 +91,7 @@ struct GPDesc {
   int tiles;           // k_inc_stream: 1 = the launch also streams the cell tiles (one-pass predict)
   int l21c_ok;         // one-pass predict: l21c holds the rows [n0, N) bordered onto V's n0 rows
   int rsplit;          // one-pass predict: row splits per cell group (1, 2, 4; 128 / rsplit cells per workgroup)
+  int vf32;            // 1 = the resident V is Vf (fp32; the one-pass predict streams 256 cells per workgroup)
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -96,9 +99,10 @@ struct GPDesc {
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
 inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
 inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1) / PBM; }
-// one-pass predict workgroups: 128 / rsplit cells (32 per wave and row split)
-inline __host__ __device__ int64_t ntiles_wg(int64_t M, int rsplit = 1) {
-  const int64_t c = 2 * PBM / rsplit;
+// one-pass predict workgroups: 128 / rsplit cells (32 per wave and row split); an
+// fp32 V: 256 cells (64 per wave, no row splits)
+inline __host__ __device__ int64_t ntiles_wg(int64_t M, int rsplit = 1, int vf32 = 0) {
+  const int64_t c = vf32 ? 4 * PBM : 2 * PBM / rsplit;
   return (M + c - 1) / c;
 }
 inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1) / PRB; }
@@ -115,10 +119,14 @@ hipError_t set_stamps(long long* p);
 #endif
 hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream_t s);
 // bordered append (k_inc_stream without cell tiles); max_nprod = max over GPs of nprod
-hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, hipStream_t s);
+// vf32: the batch's models store V in fp32 (GPDesc::Vf); a batch is of one V precision
+hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, int vf32, hipStream_t s);
 // bordered append + one-pass predict in one launch; max_blocks = max over GPs of nprod + cell tiles
-hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, hipStream_t s);
-hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
+hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int vf32, hipStream_t s);
+hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s);
+// MFGP_F32 full predict: round the fp64 V that k_predict wrote into d.V (rows [0, N)
+// of every tile) into the resident fp32 V (d.Vf)
+hipError_t launch_vnarrow(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);
 hipError_t launch_cell_reduce(const double* grid, int64_t M, const double* verts, const int* vstart, int ncells,
                               const double* seeds, const double* w, const double* f, const double* var,
                               double* part, double* out, int64_t* argmax, hipStream_t s);

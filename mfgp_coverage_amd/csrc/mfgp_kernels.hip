@@ -922,11 +922,37 @@ __device__ void inc_init_blocks(const GPDesc& d, int64_t c_lo, int64_t c_hi, boo
   }
 }
 
+// The compact bordered row j, entry r, for the cell workgroups' MFMA A operand:
+// fp64 V: L21[r][j] for r < k, z1[j] at r = k, zeros; fp32 V (VT = float, the
+// rows stored as floats over the same area): L21[r][j] for r < k, z1[j] at
+// r = ZROW (the f32 stream sums the mean out of that fixed row), zeros.
+constexpr int ZROW = KINC - 1;
+template <bool XW, class VT>
+__device__ __forceinline__ void store_l21c(double* l21c, int64_t j, int r, int k, double a, double z) {
+  if constexpr (sizeof(VT) == 8) {
+    stx<XW>(&l21c[j * KINC + r], r < k ? a : (r == k ? z : 0.0));
+  } else {
+    float* p = reinterpret_cast<float*>(l21c) + j * KINC + r;
+    const float v = (float)(r < k ? a : (r == ZROW ? z : 0.0));
+    if constexpr (XW) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+  }
+}
+
+// The resident V of this GP in the precision VT (fp64 d.V, fp32 d.Vf).
+template <class VT>
+__device__ __forceinline__ const VT* vres_ptr(const GPDesc& d) {
+  if constexpr (sizeof(VT) == 8) return d.V;
+  else return d.Vf;
+}
+
 // Partial L21 L21^T and L21 z1 over rows [j_lo, j_hi) into red[w][ISZ] (one slot per
 // wave). Lane (r, q) holds L21[r][j], j = 4s + q, eight 4-row steps in flight per
 // wave. With `cell`, L21[r][.] is gathered from the V column of the grid cell and
-// written to row n0 + r of A; otherwise it is read from there.
-template <int NW, bool XW, bool FROMV>
+// written to row n0 + r of A; otherwise it is read from there. VT: the precision
+// of the resident V (an fp32 V's entries are widened: L21 is then the factor of K
+// perturbed by their rounding, |dL21| <= 2^-24 |L21|).
+template <int NW, bool XW, bool FROMV, class VT>
 __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo, int64_t j_hi,
                                   double (*red)[ISZ]) {
   // descriptor fields in registers: the write-through stores below would make the
@@ -942,7 +968,8 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
   d4 sacc = {0.0, 0.0, 0.0, 0.0}, uacc = {0.0, 0.0, 0.0, 0.0};
   constexpr int IU = 8;
   const int cr = (FROMV && r < k) ? cell[r] : 0;
-  const double* src = FROMV ? d.V + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : A + n0 + (r < k ? r : 0);
+  const VT* vsrc = FROMV ? vres_ptr<VT>(d) + (int64_t)(cr / PBM) * d.vld * PBM + (cr % PBM) : nullptr;
+  const double* src = A + n0 + (r < k ? r : 0);
   const int64_t sstride = FROMV ? PBM : ld;
   const int64_t s_lo = j_lo >> 2, s_hi = (j_hi + 3) >> 2;   // j_lo is a multiple of 4
   for (int64_t s0 = s_lo + w; s0 < s_hi; s0 += NW * IU) {
@@ -953,7 +980,7 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
       const bool ok = j < j_hi;
       const int64_t jj = ok ? j : j_lo;
 #ifndef MFGP_DIAG_NOGATHER   // diagnostic build: no V-column loads (timing only)
-      a[u] = FROMV ? gp(src)[jj * sstride] : ldx<XW>(src + jj * sstride);
+      a[u] = FROMV ? (double)gp(vsrc)[jj * sstride] : ldx<XW>(src + jj * sstride);
 #else
       a[u] = FROMV ? 1.0 : ldx<XW>(src + jj * sstride);
 #endif
@@ -966,9 +993,9 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
       a[u] = (ok && r < k) ? a[u] : 0.0;
       zz[u] = ok ? zz[u] : 0.0;
       if (FROMV && r < k && ok) stx<XW>(&A[j * ld + n0 + r], a[u]);
-      // compact rows for the cell tiles: L21 | z1 at row k | zeros
+      // compact rows for the cell tiles: L21 | z1 | zeros
 #ifndef MFGP_DIAG_NOPSTORE   // diagnostic build: no compact-row stores (timing only)
-      if (ok) stx<XW>(&l21c[j * KINC + r], r < k ? a[u] : (r == k ? zz[u] : 0.0));
+      if (ok) store_l21c<XW, VT>(l21c, j, r, k, a[u], zz[u]);
 #endif
       sacc = mfma(a[u], a[u], sacc);
       uacc = mfma(a[u], zz[u], uacc);
@@ -1062,6 +1089,7 @@ __device__ __forceinline__ bool inc_chunk_done(const GPDesc& d, int64_t chunk, d
 // (FROMV): L21 rows into A and the compact rows, partials into red, and the
 // chunk's identity padding of newly entered blocks (rows [n0, N) excepted: they
 // are the L21 stores, so no barrier orders the two).
+template <class VT>
 __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, int64_t j_hi, double (*red)[ISZ]) {
   constexpr int NW = NT / 64, IU = 8;
   static_assert(4 * NW * IU >= FUSED_CHUNK, "one round of loads covers a chunk");
@@ -1080,13 +1108,13 @@ __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, i
   const int iy = (int)rint(fmin(fmax((py - L.y0) * L.yinv, 0.0), (double)(L.ny - 1)));
   const int64_t cr = (px == px && py == py) ? ix * L.sx + iy * L.sy : 0;
   const dv2 g = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid))[cr];
-  const double* src = d.V + (cr / PBM) * d.vld * PBM + (cr % PBM);
+  const VT* src = vres_ptr<VT>(d) + (cr / PBM) * d.vld * PBM + (cr % PBM);
   double a[IU], zz[IU];
 #pragma unroll
   for (int u = 0; u < IU; ++u) {
     const int64_t j = j_lo + 4 * (w + NW * u) + q;
     const int64_t jj = j < j_hi ? j : j_lo;
-    a[u] = gp(src)[jj * PBM];
+    a[u] = (double)gp(src)[jj * PBM];
     zz[u] = gp(zv)[jj];
   }
   const bool miss = r < k && !(g.x == px && g.y == py);
@@ -1100,7 +1128,7 @@ __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, i
     a[u] = (ok && r < k) ? a[u] : 0.0;
     zz[u] = ok ? zz[u] : 0.0;
     if (r < k && ok) stx<true>(&A[j * ld + n0 + r], a[u]);
-    if (ok) stx<true>(&l21c[j * KINC + r], r < k ? a[u] : (r == k ? zz[u] : 0.0));
+    if (ok) store_l21c<true, VT>(l21c, j, r, k, a[u], zz[u]);
     sacc = mfma(a[u], a[u], sacc);
     uacc = mfma(a[u], zz[u], uacc);
   }
@@ -1117,6 +1145,7 @@ __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, i
 // [chunk * ch, +ch) and store the chunk's partials. Returns false when L21 is not
 // a set of V columns (off the grid / no resident V): the finish solves for it.
 // All NTHR threads take part; `cell` and `red` are in LDS.
+template <class VT>
 __device__ __forceinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell, double (*red)[ISZ]) {
   constexpr int NTHR = NT;
   constexpr bool XW = true;
@@ -1131,14 +1160,14 @@ __device__ __forceinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int6
       else const_cast<double*>(d.y)[at + e - 2 * kn] = d.srcY[e - 2 * kn];
     }
   }
-  const bool try_v = n0 > 0 && d.vres >= n0 && d.V != nullptr && d.M > 0;
+  const bool try_v = n0 > 0 && d.vres >= n0 && vres_ptr<VT>(d) != nullptr && d.M > 0;
   if (!try_v) {
     if (chunk == 0 && tid == 0) stx<XW>(d.iscr, 0.0);
     return false;
   }
   const int64_t j_lo = chunk * ch;
   const int64_t j_hi = j_lo + ch < n0 ? j_lo + ch : n0;
-  if (d.lat.nx > 0 && j_lo < n0 && ch <= FUSED_CHUNK && inc_gather_fast(d, j_lo, j_hi, red)) {
+  if (d.lat.nx > 0 && j_lo < n0 && ch <= FUSED_CHUNK && inc_gather_fast<VT>(d, j_lo, j_hi, red)) {
     if (chunk == 0 && tid == 0) stx<XW>(d.iscr, 1.0);
     return inc_chunk_done(d, chunk, red);
   }
@@ -1174,7 +1203,7 @@ __device__ __forceinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int6
   if (!use_v || j_lo >= n0) return use_v;   // off the grid: the finish solves
   inc_init_blocks<XW>(d, j_lo, j_hi, false);   // this chunk's columns of newly entered blocks
   __syncthreads();
-  inc_schur_partial<NTHR / 64, XW, true>(d, cell, j_lo, j_hi, red);
+  inc_schur_partial<NTHR / 64, XW, true, VT>(d, cell, j_lo, j_hi, red);
   return inc_chunk_done(d, chunk, red);
 }
 
@@ -1192,7 +1221,7 @@ constexpr int LBW = 16;   // Linv_OO columns staged per pass (63 rows x 16 = 100
 // inverses. FUSED (inside k_inc_stream): signals `sync[1]` once L21 is in A (when
 // this step solved it) and `sync[2]` once L22 / z2 are, with the hand-off
 // accesses of ldx / stx.
-template <bool FUSED>
+template <bool FUSED, class VT>
 __device__ __forceinline__ void inc_finish(const GPDesc& d, double* sm, int64_t ch) {
   const int64_t n0 = d.n0, N = d.N, ld = d.ld, NL = d.NL;
   const int k = (int)(N - n0);
@@ -1275,7 +1304,7 @@ __device__ __forceinline__ void inc_finish(const GPDesc& d, double* sm, int64_t 
       if (FUSED) drain_stores();
       __syncthreads();   // W_I visible to every wave; Ts free
     }
-    inc_schur_partial<NT / 64, FUSED, false>(d, nullptr, 0, n0, red);
+    inc_schur_partial<NT / 64, FUSED, false, VT>(d, nullptr, 0, n0, red);
     if (FUSED) drain_stores();   // the compact rows, before sync[1]
     __syncthreads();
     for (int e = tid; e < ISZ; e += NT) ssum[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
@@ -1903,13 +1932,320 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
   if (FUSED) WTRACE(4);
 }
 
+// ---------------------------------------------------------------------------
+// One-pass predict over an fp32 V (MFGP_F32 models, BASELINE configs[4]): the
+// same algorithm as vstream_wg, with V stored in fp32 -- half the bytes of the
+// HBM-bound stream. Everything but V stays fp64: the factor, z, L21 (widened
+// from the V gather), L22, the epilogue's solve for V_new, and both reductions
+// (var = k** - colsum(V o V) and mu = m + V^T z accumulate in f64).
+// Lane (r, q) of a wave: cells 4r .. 4r + 3 of the wave's 64 (one 64-cell V
+// tile; one 16-byte load per row), rows 4s + q of row step s. T = psi_new^T -
+// L21 V_old on the exact f32 MFMA (v_mfma_f32_16x16x4_f32), one per cell slot
+// x: A = the compact rows (fp32: L21 rows 0..k-1, z1 in row ZROW), B = the
+// slot's V entries; output lane (r, g) register v = row 4g + v, cell 4r + x.
+// Row ZROW (lanes g = 3, register 3) is V_old^T z1: it is added into f64 and
+// cleared once per pass of the stage ring, so no f32 sum runs over more than 32
+// rows. T itself accumulates in f32 over all n0 rows (its error is divided by
+// L22 >= sqrt(noise_H) in V_new). No row splits: 256 cells per workgroup.
+// ---------------------------------------------------------------------------
+constexpr int WF_CELLS = 64;            // cells per wave (one V tile)
+constexpr int WF_WG = 4 * WF_CELLS;     // cells per workgroup (ntiles_wg(M, 1, 1))
+constexpr int WF_LDS = KINC * KINC + KINC + 2 * KINC + 2 * WF_WG;
+static_assert(WF_LDS <= FIN_LDS, "one LDS image serves every role");
+static_assert(WF_WG == NT, "one thread per cell of the workgroup stages the psi inputs");
+#ifndef MFGP_WF_S
+#define MFGP_WF_S 4
+#endif
+
+// MODE as ws_*: 0 = k = 0 (VALU mean over z), 1 = A operand from A (widened
+// to f32 per load; VALU mean), 2 = compact rows (mean from row ZROW).
+template <int MODE>
+constexpr int wf_u() { return 2; }
+template <int MODE>
+constexpr int wf_s() { return MODE == 2 ? MFGP_WF_S : 3; }
+
+template <int MODE>
+struct WfStage {
+  f4 v[wf_u<MODE>()];
+  float a[wf_u<MODE>()];
+  double z[wf_u<MODE>()];
+};
+
+struct WfSrc {
+  const GLOBAL f4* vb;        // this lane's cells, row 0
+  const GLOBAL float* af;     // MODE 2: compact rows, this lane's entry of row 0
+  const GLOBAL double* ad;    // MODE 1: A, row n0 + r of column 0
+  int64_t astride;
+  const GLOBAL double* zb;    // z, row 0 (MODE <= 1)
+  int64_t n0;
+};
+
+template <int MODE, bool GUARD>
+__device__ __forceinline__ void wf_load(WfStage<MODE>& s, const WfSrc& src, int64_t j0) {
+#pragma unroll
+  for (int u = 0; u < wf_u<MODE>(); ++u) {
+    const int64_t j = j0 + 4 * u;
+    const int64_t jj = (!GUARD || j < src.n0) ? j : 0;
+    s.v[u] = __builtin_nontemporal_load(src.vb + jj * (PBM / 4));
+    if (MODE == 2) s.a[u] = src.af[jj * KINC];
+    if (MODE == 1) s.a[u] = (float)src.ad[jj * src.astride];
+    if (MODE <= 1) s.z[u] = src.zb[jj];
+  }
+}
+
+template <int MODE, bool GUARD>
+__device__ __forceinline__ void wf_use(WfStage<MODE>& s, int64_t j0, int64_t n0, bool arow, f4* acc, double* vs,
+                                       double* ms) {
+#pragma unroll
+  for (int u = 0; u < wf_u<MODE>(); ++u) {
+    if (GUARD && j0 + 4 * u >= n0) {
+      s.v[u] = f4{0.f, 0.f, 0.f, 0.f};
+      s.a[u] = 0.f;
+      s.z[u] = 0.0;
+    }
+    double vx[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      vx[x] = (double)s.v[u][x];
+      vs[x] = __builtin_fma(vx[x], vx[x], vs[x]);
+      if (MODE <= 1) ms[x] = __builtin_fma(vx[x], s.z[u], ms[x]);
+    }
+    if (MODE >= 1) {
+      const float a = (MODE == 1 && !arow) ? 0.f : s.a[u];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) acc[x] = mfma(a, s.v[u][x], acc[x]);
+    }
+  }
+}
+
+// Row ZROW of the accumulators (lanes g = 3, register 3) into the f64 mean sums.
+__device__ __forceinline__ void wf_flush_zrow(f4* acc, double* ms, bool zl) {
+  static_assert(ZROW == 15, "row 15 = lane group 3, register 3");
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const float t = acc[x][3];
+    ms[x] += zl ? (double)t : 0.0;
+    acc[x][3] = zl ? 0.f : t;
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void wf_stream(const WfSrc& src, int q0, bool arow, f4* acc, double* vs, double* ms,
+                                          WsPrefetch& pf) {
+  constexpr int64_t RS = 4 * wf_u<MODE>();
+  constexpr int SS = wf_s<MODE>();
+  const int64_t n0 = src.n0;
+  const int64_t q = q0;
+  const int64_t T = n0 / RS;
+  const bool zl = q0 == 3;
+  WfStage<MODE> st[SS];
+#pragma unroll
+  for (int s = 0; s < SS - 1; ++s)
+    if (s < T) wf_load<MODE, false>(st[s], src, s * RS + q);
+  int64_t t = 0;
+  for (; t + 2 * SS - 1 <= T; t += SS) {
+#ifndef MFGP_WS_NOPRIO
+    // as ws_stream: priority falls as a wave advances
+    if (t >= (2 * T) / 3) __builtin_amdgcn_s_setprio(0);
+    else if (t >= T / 3) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(2);
+#endif
+#pragma unroll
+    for (int s = 0; s < SS; ++s) ws_prefetch(pf, t + s, T);
+#pragma unroll
+    for (int s = 0; s < SS; ++s) {
+      wf_load<MODE, false>(st[(s + SS - 1) % SS], src, (t + s + SS - 1) * RS + q);
+      __builtin_amdgcn_sched_barrier(0);
+      wf_use<MODE, false>(st[s], (t + s) * RS + q, n0, arow, acc, vs, ms);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (MODE == 2) wf_flush_zrow(acc, ms, zl);
+  }
+#pragma unroll
+  for (int s = 0; s < 2 * SS - 2; ++s) {
+    if (t + s >= T) break;
+    if (t + s + SS - 1 < T) wf_load<MODE, false>(st[(s + SS - 1) % SS], src, (t + s + SS - 1) * RS + q);
+    wf_use<MODE, false>(st[s % SS], (t + s) * RS + q, n0, arow, acc, vs, ms);
+  }
+  if (T * RS < n0) {
+    const int64_t j0 = T * RS + q;
+    wf_load<MODE, true>(st[0], src, j0);
+    wf_use<MODE, true>(st[0], j0, n0, arow, acc, vs, ms);
+  }
+  if (MODE == 2) wf_flush_zrow(acc, ms, zl);
+}
+
+// Pick element x of a per-slot quadruple (x uniform per lane).
+__device__ __forceinline__ double pick4(double a0, double a1, double a2, double a3, int x) {
+  return x == 0 ? a0 : (x == 1 ? a1 : (x == 2 ? a2 : a3));
+}
+
+// One workgroup of the fp32 one-pass predict: 256 cells, wave w owns cells
+// [wgt * 256 + 64 w, +64) over all n0 rows. FUSED as vstream_wg.
+template <bool FUSED>
+__device__ __forceinline__ void vstream_wg_f32(const GPDesc& d, int64_t wgt, double* sm) {
+  const int64_t M = d.M;
+  const int64_t n0 = d.n0, N = d.N, ld = d.ld;
+  const int k = (int)(N - n0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t cg = wgt * WF_WG + WF_CELLS * w;   // first grid cell of this wave = its V tile's
+  const bool live = cg < M;
+  float* __restrict__ Vt = d.Vf + (cg / PBM) * d.vld * PBM;
+  const Hyp& h = d.hp;
+  double* L22 = sm;                          // L22 (row-major) | z2
+  double* Xn = sm + KINC * KINC + KINC;      // new rows' (x, y)
+  double* Gc = Xn + 2 * KINC;                // the workgroup's cells' (x, y)
+  f4 acc[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) acc[x] = f4{0.f, 0.f, 0.f, 0.f};
+  double vs[4] = {0.0, 0.0, 0.0, 0.0}, ms[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool mma = k > 0;
+  const bool zrow = mma && k < KINC && d.l21c_ok;
+  for (int e = tid; !FUSED && mma && e < KINC * KINC + KINC; e += NT) {
+    double v = 0.0;
+    if (e < KINC * KINC) {
+      const int ra = e / KINC, cb = e % KINC;
+      if (ra < k && cb <= ra) v = d.l21c_ok ? d.l22r[e] : d.A[(n0 + cb) * ld + n0 + ra];
+    } else if (e - KINC * KINC < k) {
+      v = d.l21c_ok ? d.l22r[e] : d.zv[n0 + e - KINC * KINC];
+    }
+    L22[e] = v;
+  }
+  if (mma) {
+    {
+      const int64_t cc = wgt * WF_WG + tid < M ? wgt * WF_WG + tid : M - 1;
+      reinterpret_cast<dv2*>(Gc)[tid] = *reinterpret_cast<const GLOBAL dv2*>(gp(d.grid) + 2 * cc);
+    }
+    if (tid < KINC) {
+      const double* p = row_pt(d, n0 + (tid < k ? tid : 0));
+      Xn[2 * tid] = p[0];
+      Xn[2 * tid + 1] = p[1];
+    }
+    __syncthreads();
+  }
+  if (live && mma) {
+    // the accumulators start at -psi_new (row 4q + v of cell 4r + x), in f32
+    const int e0 = WF_CELLS * w + 4 * r;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int a = 4 * q + v;
+      if (a < k) {
+        const double tx = Xn[2 * a], ty = Xn[2 * a + 1];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+          acc[x][v] = (float)(-psi_new(h, d.NL, n0 + a, Gc[2 * (e0 + x)], Gc[2 * (e0 + x) + 1], tx, ty));
+      }
+    }
+  }
+  if (FUSED && mma) wait_l21(d);
+  WsPrefetch pf{(FUSED && mma) ? d.sync + 2 : nullptr, d.epoch, d.l22r, 0u, 0.0, 0.0, false};
+  if (live && n0 > 0) {
+    const GLOBAL f4* vb = reinterpret_cast<const GLOBAL f4*>(gp(Vt)) + r;
+    if (zrow) {
+      const WfSrc src{vb, reinterpret_cast<const GLOBAL float*>(gp(d.l21c)) + r, nullptr, 0, nullptr, n0};
+      wf_stream<2>(src, q, true, acc, vs, ms, pf);
+    } else if (mma) {
+      const WfSrc src{vb, nullptr, gp(d.A) + n0 + (r < k ? r : 0), ld, gp(d.zv), n0};
+      wf_stream<1>(src, q, r < k, acc, vs, ms, pf);
+    } else {
+      const WfSrc src{vb, nullptr, nullptr, 0, gp(d.zv), n0};
+      wf_stream<0>(src, q, false, acc, vs, ms, pf);
+    }
+  }
+  // colsums over the lanes' row residues q
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    vs[x] += __shfl_xor(vs[x], 16);
+    vs[x] += __shfl_xor(vs[x], 32);
+    ms[x] += __shfl_xor(ms[x], 16);
+    ms[x] += __shfl_xor(ms[x], 32);
+  }
+  const bool pre = (FUSED && mma) ? __syncthreads_and(pf.have) != 0 : false;
+  if (pre) {
+    for (int e = tid, i = 0; e < KINC * KINC + KINC; e += NT, ++i) {
+      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+      L22[e] = use ? (i == 0 ? pf.r0 : pf.r1) : 0.0;
+    }
+  }
+  if (FUSED && mma && !pre) {
+    if (tid == 0) {
+      int it = 0;
+      while (__hip_atomic_load(d.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != d.epoch) {
+        __builtin_amdgcn_s_sleep(MFGP_SPIN_SLEEP);
+        if (++it == (1 << 22)) {
+          atomicMin(d.status, SYNC_FAIL);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < KINC * KINC + KINC; e += NT) {
+      const double v = d.l22r[e];
+      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+      L22[e] = use ? v : 0.0;
+    }
+  }
+  __syncthreads();
+  // epilogue: lane (r, q) finishes cell cg + 4r + q (slot x = q). Row a of T for
+  // slot x sits in acc[x][a % 4] of lane (r, a / 4).
+  const int x = q;
+  const int64_t c = cg + 4 * r + x;
+  double vsum = pick4(vs[0], vs[1], vs[2], vs[3], x);
+  double msum = pick4(ms[0], ms[1], ms[2], ms[3], x);
+  if (mma) {
+    double vn[KINC];
+#pragma unroll
+    for (int a = 0; a < KINC; ++a) {
+      vn[a] = 0.0;
+      if (a < k) {
+        const int src = r + 16 * (a / 4);
+        const double t0 = (double)__shfl(acc[0][a % 4], src);
+        const double t1 = (double)__shfl(acc[1][a % 4], src);
+        const double t2 = (double)__shfl(acc[2][a % 4], src);
+        const double t3 = (double)__shfl(acc[3][a % 4], src);
+        double t = -pick4(t0, t1, t2, t3, x);   // psi_new - L21 V_old
+#pragma unroll
+        for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+        vn[a] = t / L22[a * KINC + a];
+        vsum += vn[a] * vn[a];
+        msum += vn[a] * L22[KINC * KINC + a];
+      }
+    }
+    if (live && c < M) {
+#pragma unroll
+      for (int a = 0; a < KINC; ++a)
+        if (a < k) gp(Vt)[(n0 + a) * PBM + 4 * r + x] = (float)vn[a];
+    }
+  }
+  const double vc = h.kss - vsum;
+  const bool valid = live && c < M;
+  if (valid) {
+    d.mu[c] = msum + h.meanH;
+    d.var[c] = vc;
+  }
+  if ((d.vmax || d.vargmax) && live)
+    var_argmax_group(d, valid ? vc : -__builtin_inf(), valid ? c : INT64_MAX, cg / WF_CELLS,
+                     (M + WF_CELLS - 1) / WF_CELLS);
+}
+
+// Cells per one-pass-predict workgroup of descriptor d.
+template <class VT>
+__device__ __forceinline__ int64_t wg_cells(const GPDesc& d) {
+  if constexpr (sizeof(VT) == 8) return WS_WG / d.rsplit;
+  else return WF_WG;
+}
+
+template <class VT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_vstream(
     const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
-  if ((int64_t)blockIdx.x * (WS_WG / d.rsplit) >= d.M) return;
+  if ((int64_t)blockIdx.x * wg_cells<VT>(d) >= d.M) return;
   if (d.gate && *d.gate == 0) return;
-  __shared__ double sm[VS_LDS];
-  vstream_wg<false>(d, blockIdx.x, sm);
+  __shared__ double sm[VS_LDS > WF_LDS ? VS_LDS : WF_LDS];
+  if constexpr (sizeof(VT) == 8) vstream_wg<false>(d, blockIdx.x, sm);
+  else vstream_wg_f32<false>(d, blockIdx.x, sm);
 }
 
 // ---------------------------------------------------------------------------
@@ -1932,6 +2268,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
 // (8 GPs: 128 producers + 1024 cell workgroups) 1024 are resident at once and
 // the last 128 cell workgroups take the producers' slots as they finish (9-15 us).
 // ---------------------------------------------------------------------------
+template <class VT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream(
     const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.x];
@@ -1944,14 +2281,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
   const int64_t np = d.nprod, role = blockIdx.y;
   if (role >= np) {
     const int64_t wgt = role - np;
-    if (d.tiles && wgt * (WS_WG / d.rsplit) < d.M) vstream_wg<true>(d, wgt, sm);
+    if (d.tiles && wgt * wg_cells<VT>(d) < d.M) {
+      if constexpr (sizeof(VT) == 8) vstream_wg<true>(d, wgt, sm);
+      else vstream_wg_f32<true>(d, wgt, sm);
+    }
     return;
   }
   __shared__ int cell[KINC];
   __shared__ unsigned last;
   if (role == 0) FSTAMP(30);
   __builtin_amdgcn_s_setprio(3);   // producers and the finish before the cell streams
-  const bool gathered = inc_produce(d, role, FCH, cell, reinterpret_cast<double(*)[ISZ]>(sm));
+  const bool gathered = inc_produce<VT>(d, role, FCH, cell, reinterpret_cast<double(*)[ISZ]>(sm));
   FSTAMP(40);   // latest producer done storing (before the drain)
   drain_stores();
   __syncthreads();
@@ -1966,9 +2306,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
   FSTAMP(31);   // latest producer arrival
   __syncthreads();
   WTRACE(1);
-  if (last) inc_finish<true>(d, sm, FCH);
+  if (last) inc_finish<true, VT>(d, sm, FCH);
   if (last) WTRACE(2);   // the hand-off accesses: tiles may stream concurrently
   WTRACE(4);
+}
+
+// MFGP_F32 full predict: k_predict computed V in fp64 into the scratch d.V (the
+// left-looking solve re-reads its own earlier rows, so it runs in fp64); rows
+// [0, N) of every tile are rounded into the resident fp32 V. One workgroup per
+// tile, 16-byte loads / 8-byte stores along the rows.
+__global__ __launch_bounds__(NT) void k_vnarrow(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t t = blockIdx.x;
+  if (t >= ntiles_grid(d.M)) return;
+  const GLOBAL dv2* src = reinterpret_cast<const GLOBAL dv2*>(gp(d.V) + t * d.vld * PBM);
+  GLOBAL float* dst = gp(d.Vf) + t * d.vld * PBM;
+  const int64_t n2 = d.N * (PBM / 2);
+  for (int64_t e = threadIdx.x; e < n2; e += NT) {
+    const dv2 v = __builtin_nontemporal_load(src + e);
+    typedef float fv2 __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<GLOBAL fv2*>(dst + 2 * e) = fv2{(float)v.x, (float)v.y};
+  }
 }
 
 // One iteration of compute_sample_points (simulator.py:344-370) on the device:
@@ -2047,8 +2405,9 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
   hipLaunchKernelGGL(k_extract_z, dim3((unsigned)((max_n + NT - 1) / NT), count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
-hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, hipStream_t s) {
-  hipLaunchKernelGGL(k_inc_stream, dim3(count, (unsigned)max_nprod), dim3(NT), 0, s, d);
+hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, int vf32, hipStream_t s) {
+  if (vf32) hipLaunchKernelGGL(k_inc_stream<float>, dim3(count, (unsigned)max_nprod), dim3(NT), 0, s, d);
+  else hipLaunchKernelGGL(k_inc_stream<double>, dim3(count, (unsigned)max_nprod), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,
@@ -2056,12 +2415,19 @@ hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points,
   hipLaunchKernelGGL(k_choi_select, dim3(1), dim3(64), 0, s, d, threshold, points, max_points);
   return hipGetLastError();
 }
-hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_inc_stream, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, d);
+hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int vf32, hipStream_t s) {
+  if (vf32) hipLaunchKernelGGL(k_inc_stream<float>, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, d);
+  else hipLaunchKernelGGL(k_inc_stream<double>, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
-hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_vstream, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
+hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s) {
+  if (vf32) hipLaunchKernelGGL(k_vstream<float>, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
+  else hipLaunchKernelGGL(k_vstream<double>, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_vnarrow(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s) {
+  if (max_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_vnarrow, dim3((unsigned)max_tiles, count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 

@@ -119,11 +119,16 @@ class _DeviceGP:
     """Shared device plumbing of SFGP / MFGP."""
 
     _kind = None
+    # precision of the device-resident V = L^-1 psi^T: "f64" (the reference's) or
+    # "f32" (BASELINE configs[4]: V stored and streamed in fp32, the factor, solves
+    # and reductions in fp64); set on the instance before its first update
+    precision = "f64"
 
     def _dev(self):
         m = self.__dict__.get("_model")
         if m is None:
-            m = _lib.Model(_lib.context(), self._kind, self._hyp_vec(), self.jitter)
+            dt = _lib.F32 if self.precision == "f32" else _lib.F64
+            m = _lib.Model(_lib.context(), self._kind, self._hyp_vec(), self.jitter, dtype=dt)
             self.__dict__["_model"] = m
             self.__dict__["_synced"] = None
             self.__dict__["_grid"] = None

@@ -212,6 +212,34 @@ def parity_errors(mu, var, mu_ref, var_ref, kss):
 PARITY_TOL = 1e-6
 
 
+def parity_errors_f32(mu, var, mu_ref, var_ref, kss):
+    """Tolerance metric of the MFGP_F32 mode (BASELINE configs[4]: the resident V
+    stored and streamed in fp32, everything else fp64) against this fp64 oracle.
+    Returns (mu_err, var_err):
+
+    mu:  max |d| / max(|ref|, 1e-2 * max|ref|) -- fp32 storage of V puts an
+         absolute error of ~1e-8 on mu (2^-24 per V entry times |V^T z|); the
+         posterior mean of a [0, 1] field crosses zero, so the relative bound is
+         floored at 1 % of the field's largest |mu|;
+    var: max |d| / max(|ref|, 1e-6 * k**), the fp64 metric.
+    Measured on australia9 (128x128, N = 2048, numpy emulation of the kernels'
+    arithmetic): fp32 V alone 7e-7 / 3e-7; with the f32 accumulation of
+    psi_new - L21 V_old 1.2e-6 / 2.2e-6. Gate: F32_TOL.
+    """
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    var = np.asarray(var, dtype=np.float64).reshape(-1)
+    mu_ref = np.asarray(mu_ref, dtype=np.float64).reshape(-1)
+    var_ref = np.asarray(var_ref, dtype=np.float64).reshape(-1)
+    if not mu.size:
+        return 0.0, 0.0
+    mden = np.maximum(np.abs(mu_ref), 1e-2 * np.max(np.abs(mu_ref)))
+    vden = np.maximum(np.abs(var_ref), 1e-6 * kss)
+    return float(np.max(np.abs(mu - mu_ref) / mden)), float(np.max(np.abs(var - var_ref) / vden))
+
+
+F32_TOL = 1e-4
+
+
 # ---------------------------------------------------------------------------
 # Voronoi-cell reductions (simulator.py:105-136, 194-323) -- checker for
 # mfgp_cells.hip / geometry.py. Membership is in_polygon (sim:105-124), i.e.
