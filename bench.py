@@ -22,6 +22,15 @@ results (tests/test_gpu_incremental.py):
                     (k_predict).
 
 value = (ranks x seeds x steps) / max-over-ranks wall time.
+
+--workload configs4 (BASELINE configs[4]): 256x256 grid, N_L = N_H = 4096,
+australia9_mf, 32 seeds/GPU, the MFGP_F32 mode (V stored and streamed in fp32;
+factor, solves and reductions fp64); dtype "f32". The default workload is the
+headline (configs[3] sizes, fp64).
+
+--gpus N without a torch.distributed launcher: the process starts N ranks itself
+(python -m torch.distributed.run as a child; this process never touches the GPU)
+and exits with their status. Under a launcher WORLD_SIZE must equal N.
 roofline (value): k_inc_stream, HBM-bound; algorithmic bytes per launch =
   B x 8 x [M (n0 + k + 4) + n0 (3k + 1)] (V_old read once; V_new, mu, var
   written; grid read; L21 gathered from V, written to A and read back; z once)
@@ -50,28 +59,76 @@ sys.path.insert(0, ROOT)
 METRIC = "GP posterior updates/sec (128×128 grid, N_train=2048) at 1/2/4/8 MI355X"
 PEAK_F64_TFLOPS = 78.6   # MI355X f64 matrix (= vector) spec
 PEAK_HBM_GBS = 8000.0    # MI355X HBM3E
-TIMING_STRIDE = 8        # events bracket every 8th launch of the timed region
 FUSED = os.environ.get("MFGP_FUSED", "1") != "0"
+F32_RTOL = 1e-4          # oracle.gp_oracle.F32_TOL: incremental vs full VarMax in the fp32 mode
+
+
+def timing_stride(steps):
+    """Events bracket every stride-th launch of the timed region (an event pair
+    costs a few microseconds of stream time), at least 8 launches sampled."""
+    return max(1, min(8, steps // 8))
+
+
+def launch_plan(gpus, env):
+    """How this invocation runs: ("run", world) under a launcher or for one GPU,
+    ("spawn", gpus) to start `gpus` ranks as a child launcher, or ("error", msg)."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            return "error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+        return "run", world
+    return ("spawn", gpus) if gpus > 1 else ("run", 1)
+
+
+def spawn(gpus, argv):
+    """Start `gpus` ranks (one per GPU) with torch.distributed.run as a child
+    process; the parent initialises nothing on the GPU. Returns the exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--seeds-per-gpu", type=int, default=8)
-    p.add_argument("--grid", type=int, default=128)
-    p.add_argument("--nl", type=int, default=1024)
-    p.add_argument("--nh", type=int, default=1024)
+    p.add_argument("--workload", choices=["headline", "configs4"], default="headline",
+                   help="headline: BASELINE configs[3] sizes in fp64; configs4: BASELINE configs[4] in MFGP_F32")
+    p.add_argument("--steps", type=int, default=None)
+    p.add_argument("--warmup", type=int, default=None)
+    p.add_argument("--full-steps", type=int, default=None, help="timed steps of the full-recompute run")
+    p.add_argument("--seeds-per-gpu", type=int, default=None)
+    p.add_argument("--grid", type=int, default=None)
+    p.add_argument("--nl", type=int, default=None)
+    p.add_argument("--nh", type=int, default=None)
     p.add_argument("--agents", type=int, default=8)
-    p.add_argument("--hyp", default="australia8_mf")
+    p.add_argument("--hyp", default=None)
+    p.add_argument("--dtype", choices=["f64", "f32"], default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-faithful", type=int, default=1, help="also time the reference-faithful op sequence")
     p.add_argument("--no-full", action="store_true", help="skip the full-recompute comparison run")
-    return p.parse_args()
+    p.add_argument("--diagnostic", action="store_true",
+                   help="allow a diagnostic library (MFGP_LIB); its line is marked and is not a headline number")
+    a = p.parse_args()
+    pre = {"headline": dict(steps=200, warmup=20, full_steps=None, seeds_per_gpu=8, grid=128, nl=1024, nh=1024,
+                            hyp="australia8_mf", dtype="f64"),
+           "configs4": dict(steps=20, warmup=3, full_steps=2, seeds_per_gpu=32, grid=256, nl=4096, nh=4096,
+                            hyp="australia9_mf", dtype="f32")}[a.workload]
+    for key, v in pre.items():
+        if getattr(a, key) is None:
+            setattr(a, key, v)
+    if a.full_steps is None:
+        a.full_steps = a.steps
+    return a
 
 
-def pmc_traffic(kernel="k_predict"):
+def pmc_traffic(kernel="k_predict", tag=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
     summary (profiles/<round>_hbm_traffic.csv, written by tools/summarize_profile.py
     from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x2 per the gfx950
@@ -79,6 +136,9 @@ def pmc_traffic(kernel="k_predict"):
     import glob
     import csv
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.csv")))
+    # profiles/<round>_hbm_traffic.csv: the headline; <round>_<tag>_hbm_traffic.csv: another workload
+    files = [f for f in files if (f"_{tag}_" in os.path.basename(f)) == (tag is not None)
+             and (tag is not None or "configs4" not in os.path.basename(f))]
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -110,11 +170,7 @@ def cpu_baseline(wl, hyp, s, NL, NH0, k, reps=5):
     """Time the oracle on one seed's update (same inputs as step s): one untimed
     warm-up, then the median of `reps` updates."""
     from oracle import gp_oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:  # pragma: no cover
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = _blas_threads()
     XH = np.vstack([wl.XH[:NH0], wl.Xnew[s]])
     yH = np.concatenate([wl.yH[:NH0], wl.ynew[s]])
     O.mf_diag(wl.XL, wl.yL, XH, yH, hyp, wl.xs)   # warm-up (BLAS threads, page faults)
@@ -124,24 +180,89 @@ def cpu_baseline(wl, hyp, s, NL, NH0, k, reps=5):
         O.mf_diag(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
         ts.append(time.perf_counter() - t0)
     out = {"value": 1.0 / float(np.median(ts)), "unit": "GP-updates/s", "cores": int(threads), "kind": "port",
-           "sample": f"oracle.mf_diag (Cholesky + triangular solves + row-sum, fp64 NumPy/BLAS), 1 seed x "
-                     f"{reps} updates after one warm-up at the full config (M={wl.xs.shape[0]}, N={NL + NH0 + k}), median"}
+           "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "sample": f"oracle.mf_diag (Cholesky + triangular solves + row-sum, fp64 NumPy/BLAS, {threads} BLAS "
+                     f"threads), 1 seed x {reps} updates after one warm-up at the full config "
+                     f"(M={wl.xs.shape[0]}, N={NL + NH0 + k}), median"}
     return out, (XH, yH)
 
 
-def cpu_faithful(wl, hyp, XH, yH):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline_sampled(wl, hyp, s, NL, NH0, k, cells=4096, reps=3):
+    """configs[4] sizes (M = 65536, N = 8192): the diag oracle's full update needs
+    psi and V at 4.3 GB each and minutes of CPU, so it is timed on a bounded
+    sample -- the factor at the full N plus the solve, mean and variance for
+    `cells` grid cells -- and scaled linearly in M (the factor is per update, the
+    rest per cell). Median of `reps`."""
+    import scipy.linalg as sla
     from oracle import gp_oracle as O
-    t0 = time.perf_counter()
-    O.mf_faithful(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
-    dt = time.perf_counter() - t0
-    return {"value": 1.0 / dt, "unit": "GP-updates/s",
+    threads = _blas_threads()
+    XH = np.vstack([wl.XH[:NH0], wl.Xnew[s]])
+    yH = np.concatenate([wl.yH[:NH0], wl.ynew[s]])
+    M = wl.xs.shape[0]
+    sub = wl.xs[np.random.default_rng(0).choice(M, cells, replace=False)]
+    tf, tc = [], []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        K = O.mf_K(wl.XL, XH, hyp)
+        Lc = np.linalg.cholesky(K)
+        t1 = time.perf_counter()
+        psi = O.mf_psi(sub, wl.XL, XH, hyp)
+        V = sla.solve_triangular(Lc, psi.T, lower=True, check_finite=False)
+        _ = np.einsum("ij,ij->j", V, V)
+        t2 = time.perf_counter()
+        tf.append(t1 - t0)
+        tc.append(t2 - t1)
+    t = float(np.median(tf[1:])) + float(np.median(tc[1:])) * M / cells
+    return {"value": 1.0 / t, "unit": "GP-updates/s", "cores": int(threads), "kind": "port",
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"oracle.mf_diag steps (fp64 NumPy/BLAS, {threads} BLAS threads) for 1 seed at N={NL + NH0 + k}: "
+                      f"K + Cholesky at full N, psi / triangular solve / row-sums for {cells} of the M={M} cells, "
+                      f"scaled to M; median of {reps} after one warm-up"}
+
+
+def _blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:  # pragma: no cover
+        return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def cpu_faithful(wl, hyp, XH, yH, reps=3):
+    from oracle import gp_oracle as O
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        O.mf_faithful(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
+        ts.append(time.perf_counter() - t0)
+    return {"value": 1.0 / float(np.median(ts)), "unit": "GP-updates/s",
             "sample": "oracle.mf_faithful (the reference's op sequence: dense K(X*,X*), 4x np.linalg.solve, "
-                      "dense psi@beta), 1 update at the full config"}
+                      f"dense psi@beta), median of {reps} updates at the full config"}
 
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    plan, arg = launch_plan(a.gpus, os.environ)
+    if plan == "error":
+        sys.exit(f"bench.py: {arg}")
+    if plan == "spawn":
+        sys.exit(spawn(arg, sys.argv[1:]))
+    diag_lib = os.environ.get("MFGP_LIB")
+    if diag_lib and not a.diagnostic:
+        sys.exit("bench.py: MFGP_LIB selects a diagnostic library build; pass --diagnostic to time it "
+                 "(its line is marked and is not a headline number)")
+    world = arg
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -159,6 +280,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
     from mfgp_coverage_amd import _lib, synthetic
     from mfgp_coverage_amd.ensemble import gather_trajectories, shard_seeds
 
@@ -168,9 +290,12 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
 
+    f32 = a.dtype == "f32"
+    dtype = _lib.F32 if f32 else _lib.F64
     B, G, NL, NH, k = a.seeds_per_gpu, a.grid, a.nl, a.nh, a.agents
     NH0 = NH - k
     W, K = a.warmup, a.steps
+    KF = min(a.full_steps, K)
     total = W + K
     hyp = synthetic.HYP[a.hyp]
     M = G * G
@@ -182,7 +307,8 @@ def main():
     var = torch.empty(B * M, dtype=torch.float64, device=dev)
     ks = [k] * B
 
-    def run(incremental):
+    def run(incremental, W, K):
+        total = W + K
         ctx = _lib.context() if incremental else _lib.Context(local)
         ctx.set_stream(stream.cuda_stream)
         ctx.set_incremental(incremental)
@@ -190,7 +316,7 @@ def main():
         ctx.set_fused(FUSED)
         models = []
         for wl in wls:
-            mdl = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
+            mdl = _lib.Model(ctx, _lib.MF, hyp, 1e-8, dtype=dtype)
             mdl.set_grid(wl.xs)
             mdl.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
             models.append(mdl)
@@ -213,9 +339,10 @@ def main():
             step(s)
         aggregate(varmax[:W].transpose(0, 1).contiguous())   # first-use kernel loads / communicator setup
         ctx.synchronize()
-        # HIP events around every 8th predict launch inside the timed region
+        # HIP events around every stride-th predict launch inside the timed region
+        stride = timing_stride(K)
         ctx.enable_timing(not os.environ.get("MFGP_NO_TIMING"), predict_only=True)
-        ctx.set_timing_stride(TIMING_STRIDE)
+        ctx.set_timing_stride(stride)
         ctx.reset_timing()
         if world > 1:
             dist.barrier()
@@ -238,7 +365,7 @@ def main():
         ctx.enable_timing(True)
         ctx.set_timing_stride(1)
         ctx.reset_timing()
-        nb_steps = min(5, K)
+        nb_steps = min(5 if incremental else 1, K)
         for s in range(W, W + nb_steps):
             step(s)
         ctx.synchronize()
@@ -247,36 +374,61 @@ def main():
         el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        if not os.environ.get("MFGP_LIB"):   # diagnostic library builds compute garbage on purpose
+        if not diag_lib:   # diagnostic library builds compute garbage on purpose
             assert torch.isfinite(agg).all()
         st = models[0].stats()
         del models
         return {"elapsed": float(el.item()), "tm": tm, "host_ms": 1e3 * float(np.mean(host_t)), "stats": st,
-                "traj": traj.cpu().numpy(),
+                "traj": traj.cpu().numpy(), "stride": stride,
                 "breakdown": {"predict": tb["predict_ms"] / nb_steps, "factor": tb["factor_ms"] / nb_steps}}
 
-    inc = run(True)
-    full = None if a.no_full else run(False)
+    inc = run(True, W, K)
+    full = None if a.no_full else run(False, W, KF)
     if os.environ.get("MFGP_BENCH_DUMP") and rank == 0:
         np.savez(os.environ["MFGP_BENCH_DUMP"], inc=inc["traj"], full=full["traj"] if full else inc["traj"])
-    if full is not None and rank == 0 and not os.environ.get("MFGP_LIB"):
-        # the two paths produce the same posterior (VarMax trajectories to rounding)
-        np.testing.assert_allclose(inc["traj"], full["traj"], rtol=1e-9)
+    if full is not None and rank == 0 and not diag_lib:
+        # the two paths produce the same posterior (VarMax trajectories to rounding;
+        # the fp32 mode's to its tolerance) on the steps both ran
+        np.testing.assert_allclose(inc["traj"][:, :KF], full["traj"], rtol=F32_RTOL if f32 else 1e-9)
 
     if rank == 0:
         elapsed, tm = inc["elapsed"], inc["tm"]
         assert inc["stats"]["inc_factor"] >= K and inc["stats"]["vstream"] >= K, inc["stats"]
         n0 = N - k
-        vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (3 * k + 1))
+        es = 4 if f32 else 8
+        # algorithmic bytes of one k_inc_stream launch: V_old read once, V_new written,
+        # grid read and mu / var written, and per training row the L21 gather, its
+        # store into A and read back, the compact rows and z
+        if f32:
+            vbytes = B * (4 * M * (n0 + k) + 32 * M + n0 * (16 * k + 4 * 16 + 8))
+        else:
+            vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (3 * k + 1))
         v_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
         v_gbs = vbytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
+        value = world * B * K / elapsed
+        # SURVEY.md section 8d's algorithmic cost of one update as the reference
+        # computes it (refactor + V from scratch): F = N^3/3 + M N^2 + 2 N^2 + 4 M N flop,
+        # B_8d = 8 (4M + 3N + 2 N^2) bytes. The incremental path does not do that work
+        # (it reuses the resident V): expressed in F per second it exceeds the f64
+        # MFMA peak, which is the point of the algorithm, not a measurement error.
+        F8d = N ** 3 / 3 + M * N * N + 2 * N * N + 4 * M * N
+        B8d = 8 * (4 * M + 3 * N + 2 * N * N)
         # PMC bytes come from the committed profile of the default configuration
-        default_cfg = (G, NL, NH, B, k, a.hyp) == (128, 1024, 1024, 8, 8, "australia8_mf")
+        default_cfg = (a.workload, G, NL, NH, B, k, a.hyp, a.dtype) == ("headline", 128, 1024, 1024, 8, 8,
+                                                                         "australia8_mf", "f64")
+        c4_cfg = (G, NL, NH, B, a.hyp, a.dtype) == (256, 4096, 4096, 32, "australia9_mf", "f32")
         kern = "k_inc_stream" if FUSED else "k_vstream"
-        traffic, traffic_src = pmc_traffic(kern) if default_cfg else (None, None)
+        traffic, traffic_src = pmc_traffic(kern, "configs4" if c4_cfg else None) if (default_cfg or c4_cfg) \
+            else (None, None)
+        if default_cfg:
+            wl_name = "australia8_mf MFGP seed ensemble (BASELINE configs[3])"
+        elif c4_cfg:
+            wl_name = "BASELINE configs[4]: synthetic australia9_mf MFGP seed ensemble"
+        else:
+            wl_name = f"{a.hyp} MFGP seed ensemble"
         out = {
-            "metric": METRIC,
-            "value": world * B * K / elapsed,
+            "metric": METRIC if not diag_lib else f"DIAGNOSTIC library {diag_lib}: " + METRIC,
+            "value": value,
             "unit": "GP-updates/s",
             "n_gpus": world,
             "steps": K,
@@ -285,15 +437,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": a.dtype,
             "data": "synthetic",
             "config": {
-                "workload": f"{a.hyp} MFGP seed ensemble"
-                            f"{' (BASELINE configs[3])' if default_cfg else ''}"
-                            f"{' (BASELINE configs[4] sizes, computed in fp64)' if (G, NL, NH, B) == (256, 4096, 4096, 32) else ''}"
-                            f": {B} seeds/GPU, "
+                "workload": f"{wl_name}: {B} seeds/GPU, "
                             f"{G}x{G} grid (M={M}), N_L={NL} lofi + N_H={NH} hifi ({NH0} + {k} new agent "
-                            f"samples appended per update), factor update + mean/var at every cell, fp64",
+                            f"samples appended per update), factor update + mean/var at every cell, "
+                            + ("MFGP_F32: V = L^-1 psi^T stored and streamed in fp32, factor / solves / "
+                               "reductions in fp64" if f32 else "fp64"),
                 "update": ("incremental, one launch per step (k_inc_stream): bordered-Cholesky append + one "
                            "pass over the resident V = L^-1 psi^T" if FUSED else
                            "incremental: bordered-Cholesky append (k_inc_stream) + one pass over the resident "
@@ -305,7 +456,19 @@ def main():
                 "bound": "hbm", "achieved": v_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": v_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": kern, "bytes_per_launch": vbytes, "avg_launch_ms": v_ms,
-                "timing": f"HIP events around every {TIMING_STRIDE}th launch of the timed region",
+                "launches_timed": tm["predict_launches"],
+                "timing": f"HIP events around every {inc['stride']}th launch of the timed region",
+                "design_bytes_note": f"{es}-byte V: bytes_per_launch = the resident V read once plus the new rows, "
+                                     "grid, outputs and per-row L21 / z terms (DESIGN.md section 4)",
+            },
+            "algorithmic_8d": {
+                "flops_per_update": F8d, "bytes_per_update": B8d,
+                "flop_equivalent_tflops": F8d * value / 1e12,
+                "frac_of_f64_mfma_peak": F8d * value / 1e12 / PEAK_F64_TFLOPS,
+                "byte_rate_gbs": B8d * value / 1e9,
+                "note": "SURVEY.md 8d's per-update work is the reference's (refactor + V from scratch); the "
+                        "incremental path reuses the resident V, so this flop-equivalent rate is above the MFMA "
+                        "peak by construction; the roofline above is the kernel's own (HBM, its bytes)",
             },
             "host_enqueue_ms_per_step": inc["host_ms"],
             "breakdown_ms_per_step": inc["breakdown"],
@@ -317,22 +480,27 @@ def main():
             achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else float("nan")
             ftraffic, _ = pmc_traffic("k_predict") if default_cfg else (None, None)
             out["full_recompute"] = {
-                "value": world * B * K / full["elapsed"],
-                "ms_per_step": full["elapsed"] / K * 1e3,
+                "value": world * B * KF / full["elapsed"],
+                "steps": KF,
+                "ms_per_step": full["elapsed"] / KF * 1e3,
                 "roofline": {
                     "bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / PEAK_F64_TFLOPS, "traffic": ftraffic,
-                    "kernel": "k_predict", "flops_per_launch": flops, "avg_launch_ms": avg_ms,
+                    "kernel": "k_predict" + (" (+ k_vnarrow: V computed in fp64, stored fp32)" if f32 else ""),
+                    "flops_per_launch": flops, "avg_launch_ms": avg_ms,
                     "pmc": pmc_mfma("k_predict") if default_cfg else None,
                 },
                 "host_enqueue_ms_per_step": full["host_ms"],
                 "breakdown_ms_per_step": full["breakdown"],
             }
         if world == 1 and not a.no_cpu_baseline:
-            cb, (XH, yH) = cpu_baseline(wls[0], hyp, W, NL, NH0, k)
-            if a.cpu_faithful:
-                cb["faithful"] = cpu_faithful(wls[0], hyp, XH, yH)
-            out["cpu_baseline"] = cb
+            if M * N > 16384 * 2048:
+                out["cpu_baseline"] = cpu_baseline_sampled(wls[0], hyp, W, NL, NH0, k)
+            else:
+                cb, (XH, yH) = cpu_baseline(wls[0], hyp, W, NL, NH0, k)
+                if a.cpu_faithful:
+                    cb["faithful"] = cpu_faithful(wls[0], hyp, XH, yH)
+                out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -9,7 +9,7 @@ for v in "$@"; do
   L=$R/build/libmfgp_$v.so
   [ "$v" = "default" ] && L=$R/mfgp_coverage_amd/libmfgp_hip.so
   for B in 8 1; do
-    MFGP_LIB=$L timeout -k 10 120 python -u bench.py --seeds-per-gpu $B --no-full --no-cpu-baseline --steps 400 --warmup 40 \
+    MFGP_LIB=$L timeout -k 10 120 python -u bench.py --diagnostic --seeds-per-gpu $B --no-full --no-cpu-baseline --steps 400 --warmup 40 \
       > gpurun_out/ab_${v}_$B.json 2> gpurun_out/ab_${v}_$B.err || { echo "$v failed"; tail -5 gpurun_out/ab_${v}_$B.err; exit 1; }
     python - "$v" $B gpurun_out/ab_${v}_$B.json <<'PY'
 import json, sys

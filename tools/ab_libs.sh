@@ -8,7 +8,7 @@ for rep in 1 2; do
 for v in "$@"; do
   L=$R/build/libmfgp_$v.so
   [ "$v" = "default" ] && L=$R/mfgp_coverage_amd/libmfgp_hip.so
-  MFGP_LIB=$L timeout -k 10 120 python -u bench.py --no-full --no-cpu-baseline --steps 300 --warmup 30 > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { echo "$v failed rc=$?"; tail -5 gpurun_out/ab_$v.err; exit 1; }
+  MFGP_LIB=$L timeout -k 10 120 python -u bench.py --diagnostic --no-full --no-cpu-baseline --steps 300 --warmup 30 > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { echo "$v failed rc=$?"; tail -5 gpurun_out/ab_$v.err; exit 1; }
   python - "$v" gpurun_out/ab_$v.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

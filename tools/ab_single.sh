@@ -6,7 +6,7 @@ cd $R
 for v in "$@"; do
   L=$R/build/libmfgp_$v.so
   [ "$v" = "default" ] && L=$R/mfgp_coverage_amd/libmfgp_hip.so
-  MFGP_LIB=$L timeout -k 10 120 python -u bench.py --seeds-per-gpu 1 --no-full --no-cpu-baseline --steps 300 --warmup 30 \
+  MFGP_LIB=$L timeout -k 10 120 python -u bench.py --diagnostic --seeds-per-gpu 1 --no-full --no-cpu-baseline --steps 300 --warmup 30 \
     > gpurun_out/single_$v.json 2> gpurun_out/single_$v.err || { echo "$v failed"; tail -5 gpurun_out/single_$v.err; exit 1; }
   python - "$v" gpurun_out/single_$v.json <<'PY'
 import json, sys
