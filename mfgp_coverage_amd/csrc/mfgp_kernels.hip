@@ -1145,8 +1145,17 @@ __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, i
 // [chunk * ch, +ch) and store the chunk's partials. Returns false when L21 is not
 // a set of V columns (off the grid / no resident V): the finish solves for it.
 // All NTHR threads take part; `cell` and `red` are in LDS.
+// Test build only (tests/test_codeobj.py): MFGP_NOINLINE_PRODUCE outlines the
+// producer, the shape that once stalled k_inc_stream for seconds; the test checks
+// that such a build is caught (a call inside the kernel) and the product one is not.
+#ifdef MFGP_NOINLINE_PRODUCE
+#define MFGP_PRODUCE_INLINE __attribute__((noinline))
+#else
+#define MFGP_PRODUCE_INLINE __forceinline__
+#endif
 template <class VT>
-__device__ __forceinline__ bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell, double (*red)[ISZ]) {
+__device__ MFGP_PRODUCE_INLINE bool inc_produce(const GPDesc& d, int64_t chunk, int64_t ch, int* cell,
+                                                double (*red)[ISZ]) {
   constexpr int NTHR = NT;
   constexpr bool XW = true;
   const int64_t n0 = d.n0, N = d.N;
@@ -2267,6 +2276,34 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
 // Four workgroups per CU (128 VGPRs; 26.5 KB of LDS): at the headline size
 // (8 GPs: 128 producers + 1024 cell workgroups) 1024 are resident at once and
 // the last 128 cell workgroups take the producers' slots as they finish (9-15 us).
+//
+// Why the in-kernel hand-off is safe (gfx950: 8 XCDs, each with its own L2;
+// per-CU L1; kernel boundaries write back and invalidate both):
+//  * Forward progress. The dispatcher hands workgroups to the XCDs round-robin
+//    in linear order (x = GP fastest, then role) and each XCD dispatches its
+//    share in that order. Every producer has a lower linear id than every cell
+//    workgroup, so on each XCD all its producers are dispatched before any of its
+//    cell workgroups, and producers wait for nothing (the last arriver's finish
+//    included). Producers therefore always run to completion even when they do
+//    not all fit at once (configs[4]: 32 GPs x 64 producers = 2048 > 1024 slots),
+//    and the cells waiting for them are released. The waits are bounded anyway
+//    (~1 s, then MFGP_ERR_DEVICE via *status), and tests/test_codeobj.py checks
+//    the code has no out-of-line calls (an outlined producer stalled it once).
+//  * Visibility. Everything a producer hands over (L21 rows in A, the compact
+//    rows, chunk partials, L22 record, z2) is stored with agent-scope atomic
+//    stores (global_store ... sc1: written through the XCD's L2 to memory), then
+//    drained (s_waitcnt vmcnt(0): the stores are acknowledged), and only then is
+//    the flag stored (sc1). A consumer reads the flag with an agent-scope load
+//    (sc1: not served from a stale L2 line). Data behind the flag is then read
+//    either with sc1 loads (ldx<true>) or with plain loads of lines that no
+//    workgroup of the launch reads before the flag is up (compact rows only after
+//    every chunk's flag, the L22 record only after sync[2]); such a line cannot
+//    be in this XCD's L2 or this CU's L1 (both invalidated at the kernel
+//    boundary, never filled since), so the plain load fetches the written data.
+//  * Cost. A release (buffer_wbl2 sc1) writes back the whole L2 -- +80 us per
+//    step when 2048 workgroups did it -- and an acquire adds a buffer_inv sc1;
+//    the construction above needs neither, at the price of the two rules: drain
+//    before the flag, and no early read of a handed-over line.
 // ---------------------------------------------------------------------------
 template <class VT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream(
