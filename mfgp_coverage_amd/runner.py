@@ -7,10 +7,10 @@ per-simulation logs in seed order before writing ``<out>_loss.csv``,
 simulator.py:918-931). Here one process per GPU owns a contiguous block of
 seeds (``ensemble.shard_seeds``); each process runs its simulations (e.g. the
 reference's ``run_sim`` with this package's SFGP/MFGP as the GP classes) and the
-logs meet on rank 0 in ONE gather per log over the process group (RCCL over
+logs meet on rank 0 over the process group (RCCL over
 xGMI with the "nccl" backend, gloo on CPU): the records are encoded as float64
-columns in the reference's column order, so the exchange is a plain tensor
-all_gather. Rank 0 then writes the same CSVs and can summarise losses the way
+columns in the reference's column order, so the exchange is two plain tensor
+all_gathers for the three logs (row counts, then the packed rows). Rank 0 then writes the same CSVs and can summarise losses the way
 analysis.py:62-73 does.
 """
 from __future__ import annotations
@@ -55,37 +55,56 @@ def decode(arr, columns):
     return df.dropna(axis=1, how="all")
 
 
-def gather_table(arr, world, group=None, device=None):
-    """All-gather a [rows, cols] float64 block per rank (row counts may differ) ->
-    the rows of every rank concatenated in rank order (every rank gets them)."""
+def gather_tables(arrs, world, group=None, device=None):
+    """All-gather several [rows, cols] float64 blocks per rank (row counts may differ
+    between ranks and blocks) -> for each block, the rows of every rank concatenated
+    in rank order (every rank gets them). Two collectives in all: the row counts,
+    then every block padded to its largest count and packed into one flat tensor."""
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in arrs]
     if world <= 1:
-        return np.asarray(arr)
+        return arrs
     import torch
     import torch.distributed as dist
-    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64))
-    if device is not None:
-        t = t.to(device)
-    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    dev = device if device is not None else "cpu"
+    n = torch.tensor([a.shape[0] for a in arrs], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n, group=group)
-    counts = [int(c.item()) for c in counts]
-    rows = max(counts)
-    pad = torch.full((rows, t.shape[1]), float("nan"), dtype=torch.float64, device=t.device)
-    pad[:t.shape[0]] = t
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
-    return np.concatenate([p[:c].cpu().numpy() for p, c in zip(parts, counts)], axis=0)
+    counts = torch.stack(counts).cpu().numpy()            # [world, blocks]
+    rows = counts.max(axis=0)
+    sizes = [int(r) * a.shape[1] for r, a in zip(rows, arrs)]
+    flat = torch.full((sum(sizes),), float("nan"), dtype=torch.float64, device=dev)
+    off = 0
+    for a, sz in zip(arrs, sizes):
+        if a.size:
+            flat[off:off + a.size] = torch.from_numpy(a.reshape(-1)).to(dev)
+        off += sz
+    parts = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(parts, flat, group=group)
+    parts = [p.cpu().numpy() for p in parts]
+    out, off = [], 0
+    for b, (a, sz) in enumerate(zip(arrs, sizes)):
+        cols = a.shape[1]
+        out.append(np.concatenate([p[off:off + counts[r, b] * cols].reshape(-1, cols) for r, p in enumerate(parts)],
+                                  axis=0))
+        off += sz
+    return out
+
+
+def gather_table(arr, world, group=None, device=None):
+    """One block of gather_tables."""
+    return gather_tables([arr], world, group, device)[0]
 
 
 def run(sim_fn, simulations, world=1, rank=0, group=None, device=None, out_name=None):
     """Run sim_fn(sim_num) -> (loss_log, agent_log, sample_log) for this rank's seeds,
-    gather the logs (seed order) and, on rank 0, return the three DataFrames and
-    write ``<out_name>_{loss,agent,sample}.csv`` as runner.py:151-157 does."""
+    gather the logs (seed order; two collectives for the three logs) and, on rank 0,
+    return the three DataFrames and write ``<out_name>_{loss,agent,sample}.csv`` as
+    runner.py:151-157 does."""
     logs = ([], [], [])
     for sim_num in shard_seeds(simulations, world, rank):
         for acc, part in zip(logs, sim_fn(sim_num)):
             acc.extend(part)
-    tables = [gather_table(encode(recs, cols), world, group, device) for recs, cols in zip(logs, SCHEMAS)]
+    tables = gather_tables([encode(recs, cols) for recs, cols in zip(logs, SCHEMAS)], world, group, device)
     if rank != 0:
         return None
     dfs = [decode(t, cols) for t, cols in zip(tables, SCHEMAS)]
