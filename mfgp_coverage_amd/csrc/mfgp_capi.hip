@@ -75,7 +75,12 @@ struct mfgp_ctx {
   int64_t n_predict = 0, n_factor = 0;
   // deferred status words of ASYNC batches, with the model each belongs to (a
   // failed factor is dropped from its model at mfgp_ctx_synchronize)
-  std::vector<std::pair<mfgp_model*, int*>> async_status;
+  struct AsyncStatus {
+    mfgp_model* m;
+    int* dev;      // the model's status word (device)
+    int* host;     // its mapped host copy written by the launch (k_inc_stream1), or null: copy dev
+  };
+  std::vector<AsyncStatus> async_status;
   // fp64 scratch in which the full predicts of MFGP_F32 models compute V
   // (k_predict re-reads its own rows), then rounded into their fp32 V
   double* vscr = nullptr;
@@ -111,6 +116,8 @@ struct mfgp_model {
   double* zv = nullptr;     // [cap] z = L^-1 (y - m)
   double* iscr = nullptr;   // incremental-append scratch (inc_scratch_doubles(cap))
   int* status = nullptr;
+  int* status_host = nullptr;       // mapped pinned word the single-GP fused launch publishes status into
+  int* status_host_dev = nullptr;   // its device address
   bool factored = false;
   int64_t factor_N = -1;    // rows [0, factor_N) of A / Linv / zv hold the current factor
   int64_t ablk = 0;         // 64-row blocks of A / Linv initialised (assembled or padded)
@@ -377,6 +384,8 @@ int release_slot(mfgp_ctx* c, int slot) {
   return MFGP_OK;
 }
 
+constexpr int STATUS_UNSET = INT_MIN + 1;   // status_host before the launch writes it
+
 void fill_desc(GPDesc& d, mfgp_model* m) {
   d.X = m->X;
   d.y = m->y;
@@ -399,9 +408,11 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.tred = m->tred;
   d.gate = nullptr;
   d.status = m->status;
+  d.status_host = nullptr;
   d.srcX = nullptr;
   d.srcY = nullptr;
   d.k_new = 0;
+  d.rows_inline = 0;
   d.sync = nullptr;
   d.epoch = 0;
   d.nprod = 0;
@@ -813,16 +824,26 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
   int rc = ensure_h_status(c, c->async_status.size());
   if (rc) return rc;
   // the status words come back through pinned memory with the stream's last copies
+  // (or straight from the mapped word the launch itself published them into)
   for (size_t i = 0; i < c->async_status.size(); ++i)
-    HIP_TRY(hipMemcpyAsync(c->h_status + i, c->async_status[i].second, sizeof(int), hipMemcpyDeviceToHost,
-                           c->stream));
+    if (!c->async_status[i].host)
+      HIP_TRY(hipMemcpyAsync(c->h_status + i, c->async_status[i].dev, sizeof(int), hipMemcpyDeviceToHost,
+                             c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < c->async_status.size(); ++i) {
+    const auto& as = c->async_status[i];
+    if (as.host) {
+      c->h_status[i] = *reinterpret_cast<volatile int*>(as.host);
+      if (c->h_status[i] == STATUS_UNSET)   // not published (cannot happen with cell tiles): read the word
+        HIP_TRY(hipMemcpy(c->h_status + i, as.dev, sizeof(int), hipMemcpyDeviceToHost));
+    }
+  }
   for (size_t i = 0; i < c->async_status.size(); ++i) {
     const int st = c->h_status[i];
     if (st == INT_MAX) continue;
     // a failed factor leaves its model without one: the next use refactors (and
     // raises again), instead of serving the failed factor and its V
-    mfgp_model* m = c->async_status[i].first;
+    mfgp_model* m = c->async_status[i].m;
     m->factored = false;
     m->v_n = 0;
     m->l21c_N = -1;
@@ -920,10 +941,11 @@ void mfgp_model_destroy(mfgp_model* m) {
     (void)hipStreamSynchronize(m->ctx->stream);
     // an ASYNC batch's status word of this model dies with it (the work is done)
     auto& as = m->ctx->async_status;
-    as.erase(std::remove_if(as.begin(), as.end(), [m](const std::pair<mfgp_model*, int*>& e) { return e.first == m; }),
+    as.erase(std::remove_if(as.begin(), as.end(), [m](const mfgp_ctx::AsyncStatus& e) { return e.m == m; }),
              as.end());
   }
   if (m->spec_out) (void)hipHostFree(m->spec_out);
+  if (m->status_host) (void)hipHostFree(m->status_host);
   if (m->X) (void)hipFree(m->X);
   if (m->y) (void)hipFree(m->y);
   if (m->A) (void)hipFree(m->A);
@@ -1081,7 +1103,7 @@ int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL,
   return factor_one(m);
 }
 
-int spec_append_predict(mfgp_model* m);
+int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t k);
 
 int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
   int rc = check_model(m);
@@ -1092,13 +1114,18 @@ int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
   m->pred_since_append = false;
   const int64_t n = m->NL + m->NH;
   if ((rc = ensure_cap(m, n + k))) return rc;
-  if ((rc = copy_rows(m, n, X, y, k))) return rc;
+  if (k > 0 && (!X || !y)) return set_err(MFGP_ERR_ARG, "null data pointer with k=%lld", (long long)k);
   m->NH += k;
   if (!m->ctx->incremental) m->factored = false;   // reference behaviour: refactor from scratch
-  if (m->ctx->deferred && can_inc_factor(m)) return MFGP_OK;   // the next factor user runs the append
-  if (spec && m->ctx->fused && k > 0 && m->M > 0 && can_inc_factor(m) && m->V && m->v_n == m->factor_N &&
-      m->vtiles >= ntiles_grid(m->M))
-    return spec_append_predict(m);
+  const bool staged = m->ctx->deferred && can_inc_factor(m);   // the next factor user runs the append
+  const bool sp = !staged && spec && m->ctx->fused && k > 0 && m->M > 0 && can_inc_factor(m) && m->V &&
+                  m->v_n == m->factor_N && m->vtiles >= ntiles_grid(m->M);
+  m->NH -= k;
+  // the speculative step carries the rows in its launch (batch_run appends them)
+  if (sp) return spec_append_predict(m, X, y, k);
+  if ((rc = copy_rows(m, n, X, y, k))) return rc;
+  m->NH += k;
+  if (staged) return MFGP_OK;
   return update_factor(m);
 }
 
@@ -1124,12 +1151,11 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
 // The speculative form of an eager append (mfgp_append): the bordered append and
 // the one-pass predict as one launch, synchronised (a non-PD step is reported
 // here, as by update_factor), with mu | var kept for the next predict.
-int spec_append_predict(mfgp_model* m) {
+int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t k) {
   mfgp_ctx* c = m->ctx;
   int rc = ensure_spec_out(m);
   if (rc) return rc;
-  rc = batch_run(&m, 1, nullptr, nullptr, nullptr, m->spec_out_dev, m->spec_out_dev + m->M, nullptr, nullptr,
-                     MFGP_ASYNC, true, true);
+  rc = batch_run(&m, 1, X, y, &k, m->spec_out_dev, m->spec_out_dev + m->M, nullptr, nullptr, MFGP_ASYNC, true, true);
   if (rc == MFGP_OK) rc = mfgp_ctx_synchronize(c);
   if (rc != MFGP_OK) {
     m->factored = false;   // a failed step leaves no usable factor
@@ -1258,10 +1284,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     const int64_t n = m->NL + m->NH;
     if ((rc = ensure_cap(m, n + ki))) return rc;
     src_off[i] = off;
-    if (ki > 0) {
-      if (!dev_src && (rc = copy_rows(m, n, X + 2 * off, y + off, ki))) return rc;
-      m->NH += ki;
-    }
+    // host rows: the bordered appends carry them in their descriptors (rows_inline,
+    // landed by the producers); the others are copied below, before their launches
+    if (ki > 0) m->NH += ki;
     off += ki;
     if (!c->incremental) m->factored = false;   // reference behaviour: refactor every update
   }
@@ -1300,16 +1325,25 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
           fill_desc(hd[i], m);
         }
         const int mi = (int)(std::find(models + b0, models + b0 + nb, m) - models);
-        if (dev_src && k[mi] > 0) {
+        const int64_t ki = has_new ? k[mi] : 0;
+        if (ki <= 0) continue;
+        if (dev_src) {
           hd[i].srcX = X + 2 * src_off[mi];
           hd[i].srcY = y + src_off[mi];
-          hd[i].k_new = k[mi];
+          hd[i].k_new = ki;
+        } else if (i < ninc && ki <= KINC) {
+          std::memcpy(hd[i].rows_xy, X + 2 * src_off[mi], sizeof(double) * 2 * ki);
+          std::memcpy(hd[i].rows_y, y + src_off[mi], sizeof(double) * ki);
+          hd[i].rows_inline = 1;
+          hd[i].k_new = ki;
+        } else if ((rc = copy_rows(m, m->NL + m->NH - ki, X + 2 * src_off[mi], y + src_off[mi], ki))) {
+          return rc;
         }
       }
       for (int i = 0; i < ninc + nfull; ++i) {   // host bookkeeping of the factors enqueued below
         if (i < ninc) mark_inc_factor(order[i]);
         else mark_full_factor(order[i]);
-        c->async_status.emplace_back(order[i], order[i]->status);
+        c->async_status.push_back({order[i], order[i]->status, nullptr});
       }
     }
     // predict descriptors (state after the factor step), ordered
@@ -1359,6 +1393,33 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; fuse && i < ninc; ++i) hd[i].rsplit = hd[nb].rsplit;
     }
     if (np > nv && (rc = assign_predict_scratch(c, hd + nb + nv, np - nv))) return rc;
+    // one GP, append + one-pass predict fused, nothing else: launch with the
+    // descriptor by value (no upload) and the status published into a mapped word
+    if (fuse && nb == 1 && ninc == 1 && np == 1 && nv == 1) {
+      mfgp_model* m = order[0];
+      if (!m->status_host) {
+        HIP_TRY(hipHostMalloc(&m->status_host, sizeof(int), hipHostMallocMapped));
+        void* dev = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dev, m->status_host, 0));
+        m->status_host_dev = static_cast<int*>(dev);
+      }
+      *reinterpret_cast<volatile int*>(m->status_host) = STATUS_UNSET;
+      hd[0].status_host = m->status_host_dev;
+      for (auto it = c->async_status.rbegin(); it != c->async_status.rend(); ++it)
+        if (it->m == m) {
+          it->host = m->status_host;
+          break;
+        }
+      EvPair ev{};
+      if ((rc = ev_begin(c, ev, 0))) return rc;
+      HIP_TRY(launch_inc_stream1(hd[0], hd[0].nprod + ntiles_wg(hd[0].M, hd[0].rsplit, hd[0].vf32), hd[0].vf32,
+                                 c->stream));
+      if ((rc = ev_end(c, ev))) return rc;
+      if ((rc = release_slot(c, slot))) return rc;
+      m->v_n = m->NL + m->NH;
+      m->n_vstream += 1;
+      continue;
+    }
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
     if (do_factor) {

@@ -75,9 +75,15 @@ struct GPDesc {
   double* tred;        // [1 + 2 ceil(M/PBM)]: tiles' arrival counter, then per-tile (max, argmax) of var
   int* gate;           // device loop gate (null = always run); 0 makes the gated kernels no-ops
   int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
+  int* status_host;    // k_inc_stream with cell tiles: the launch's last cell group copies *status here
+                       // (mapped pinned host word: the host reads it without a copy), or null
   const double* srcX;  // device rows to append at row N - k_new (k_append), or null
   const double* srcY;
   int64_t k_new;
+  int rows_inline;     // 1: the k_new rows are rows_xy / rows_y below (a host append, k_new <= KINC)
+  int pad_rows;
+  double rows_xy[2 * KINC];
+  double rows_y[KINC];
   int64_t ld, N, NL, M;
   int64_t vld;         // rows per V tile (>= prow_blocks(N) * PRB)
   int64_t n0;          // incremental kernels: rows [n0, N) are new (factor / V rows valid below n0)
@@ -123,6 +129,9 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
 hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, int vf32, hipStream_t s);
 // bordered append + one-pass predict in one launch; max_blocks = max over GPs of nprod + cell tiles
 hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int vf32, hipStream_t s);
+// the same for ONE GP with its descriptor passed by value (kernel argument): no
+// descriptor upload, and with rows_inline no row copies either
+hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s);
 // MFGP_F32 full predict: round the fp64 V that k_predict wrote into d.V (rows [0, N)
 // of every tile) into the resident fp32 V (d.Vf)

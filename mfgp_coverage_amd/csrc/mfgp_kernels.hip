@@ -892,11 +892,15 @@ __device__ void wait_l21(const GPDesc& d) {
 // ([N - k_new, N), device source) are read from the source itself.
 __device__ __forceinline__ const double* row_pt(const GPDesc& d, int64_t row) {
   const int64_t at = d.N - d.k_new;
-  return (d.srcX && row >= at) ? d.srcX + 2 * (row - at) : d.X + 2 * row;
+  if (row >= at && d.srcX) return d.srcX + 2 * (row - at);
+  if (row >= at && d.rows_inline) return d.rows_xy + 2 * (row - at);
+  return d.X + 2 * row;
 }
 __device__ __forceinline__ double row_obs(const GPDesc& d, int64_t row) {
   const int64_t at = d.N - d.k_new;
-  return (d.srcY && row >= at) ? d.srcY[row - at] : d.y[row];
+  if (row >= at && d.srcY) return d.srcY[row - at];
+  if (row >= at && d.rows_inline) return d.rows_y[row - at];
+  return d.y[row];
 }
 
 // Identity padding for the 64-row blocks [ablk, nbf) entered for the first time,
@@ -1162,11 +1166,11 @@ __device__ MFGP_PRODUCE_INLINE bool inc_produce(const GPDesc& d, int64_t chunk, 
   const int k = (int)(N - n0);
   const int tid = threadIdx.x;
   const int64_t kn = d.k_new, at = N - kn;   // rows [at, N) arrive from srcX / srcY
-  if (chunk == 0 && kn > 0 && d.srcX) {
+  if (chunk == 0 && kn > 0 && (d.srcX || d.rows_inline)) {
     // consumers are later launches (this one reads the sources: row_pt / row_obs)
     for (int64_t e = tid; e < 3 * kn; e += NTHR) {
-      if (e < 2 * kn) const_cast<double*>(d.X)[2 * at + e] = d.srcX[e];
-      else const_cast<double*>(d.y)[at + e - 2 * kn] = d.srcY[e - 2 * kn];
+      if (e < 2 * kn) const_cast<double*>(d.X)[2 * at + e] = row_pt(d, at + e / 2)[e % 2];
+      else const_cast<double*>(d.y)[at + e - 2 * kn] = row_obs(d, at + e - 2 * kn);
     }
   }
   const bool try_v = n0 > 0 && d.vres >= n0 && vres_ptr<VT>(d) != nullptr && d.M > 0;
@@ -1251,7 +1255,9 @@ __device__ __forceinline__ void inc_finish(const GPDesc& d, double* sm, int64_t 
   const int64_t bb0 = n0 / NB;
   const int nO0 = (int)(n0 - bb0 * NB);   // old rows in block bb0
   STAMP(20);
-  if (tid == 0) *d.status = INT_MAX;
+  // write-through: with status_host the launch's last cell group reads it (drained
+  // with the L22 record before sync[2])
+  if (tid == 0) __hip_atomic_store(d.status, INT_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   {
     // one K22 entry per thread (gp:523-529 via k_entry)
     const int a = tid / KINC, b = tid % KINC;
@@ -1662,35 +1668,46 @@ __device__ __forceinline__ void ws_stream(const WsSrc<MODE>& src, int q0, bool a
   }
 }
 
-// (max, first argmax) of var over one wave's 32 cells (slot = the wave's cell
-// group) into tred; the last group of the launch to arrive reduces all of them.
+// Arrival of one wave's cell group (slot) of the launch, with its (max, first
+// argmax) of var when the fused var max / argmax is asked for. The last group of
+// the launch to arrive reduces the partials and, with status_host, copies the
+// GP's status word into the mapped host word (every status write of the launch
+// -- the finish's, a wait's timeout -- is drained before its group counts in).
 // Write-through partials, a drain and a relaxed counter: no fence (a release
 // fence writes the whole L2 back).
 __device__ void var_argmax_group(const GPDesc& d, double bv, int64_t bi, int64_t slot, int64_t nslots) {
   const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  const bool red = d.vmax || d.vargmax;
   unsigned* cnt = reinterpret_cast<unsigned*>(d.tred);   // tred = [counter | (max, argmax) per group]
   double* part = d.tred + 1;
+  if (red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  }
   unsigned old = 0;
   if (lane == 0) {
-    __hip_atomic_store(part + 2 * slot, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(part + 2 * slot + 1, (double)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (red) {
+      __hip_atomic_store(part + 2 * slot, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(part + 2 * slot + 1, (double)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   old = __shfl(old, 0);
   if (old != (unsigned)(nslots - 1)) return;
-  bv = -__builtin_inf();
-  bi = INT64_MAX;
-  for (int64_t t = lane; t < nslots; t += 64)
-    argmax_pair(bv, bi, __hip_atomic_load(part + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                (int64_t)__hip_atomic_load(part + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (red) {
+    bv = -__builtin_inf();
+    bi = INT64_MAX;
+    for (int64_t t = lane; t < nslots; t += 64)
+      argmax_pair(bv, bi, __hip_atomic_load(part + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                  (int64_t)__hip_atomic_load(part + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+    for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  }
   if (lane == 0) {
     if (d.vmax) *d.vmax = bv;
     if (d.vargmax) *d.vargmax = bi;
+    if (d.status_host) *d.status_host = __hip_atomic_load(d.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -1935,7 +1952,7 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
     d.mu[c] = msum + h.meanH;
     d.var[c] = vc;
   }
-  if ((d.vmax || d.vargmax) && cg < M && si == 0)
+  if ((d.vmax || d.vargmax || d.status_host) && cg < M && si == 0)
     var_argmax_group(d, valid ? vc : -__builtin_inf(), valid ? c : INT64_MAX, cg / WS_CELLS,
                      (M + WS_CELLS - 1) / WS_CELLS);
   if (FUSED) WTRACE(4);
@@ -2234,7 +2251,7 @@ __device__ __forceinline__ void vstream_wg_f32(const GPDesc& d, int64_t wgt, dou
     d.mu[c] = msum + h.meanH;
     d.var[c] = vc;
   }
-  if ((d.vmax || d.vargmax) && live)
+  if ((d.vmax || d.vargmax || d.status_host) && live)
     var_argmax_group(d, valid ? vc : -__builtin_inf(), valid ? c : INT64_MAX, cg / WF_CELLS,
                      (M + WF_CELLS - 1) / WF_CELLS);
 }
@@ -2306,9 +2323,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
 //    before the flag, and no early read of a handed-over line.
 // ---------------------------------------------------------------------------
 template <class VT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream(
-    const GPDesc* __restrict__ descs) {
-  const GPDesc& d = descs[blockIdx.x];
+__device__ __forceinline__ void inc_stream_wg(const GPDesc& d) {
   const int k = (int)(d.N - d.n0);
   if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
   if (d.gate && *d.gate == 0) return;
@@ -2346,6 +2361,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
   if (last) inc_finish<true, VT>(d, sm, FCH);
   if (last) WTRACE(2);   // the hand-off accesses: tiles may stream concurrently
   WTRACE(4);
+}
+
+template <class VT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream(
+    const GPDesc* __restrict__ descs) {
+  inc_stream_wg<VT>(descs[blockIdx.x]);
+}
+
+// One GP, descriptor by value (kernarg segment: no upload copy before the launch).
+template <class VT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream1(
+    const GPDesc d) {
+  inc_stream_wg<VT>(d);
 }
 
 // MFGP_F32 full predict: k_predict computed V in fp64 into the scratch d.V (the
@@ -2455,6 +2483,11 @@ hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points,
 hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int vf32, hipStream_t s) {
   if (vf32) hipLaunchKernelGGL(k_inc_stream<float>, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, d);
   else hipLaunchKernelGGL(k_inc_stream<double>, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s) {
+  if (vf32) hipLaunchKernelGGL(k_inc_stream1<float>, dim3(1, (unsigned)blocks), dim3(NT), 0, s, d);
+  else hipLaunchKernelGGL(k_inc_stream1<double>, dim3(1, (unsigned)blocks), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s) {
