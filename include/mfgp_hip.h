@@ -36,7 +36,9 @@ extern "C" {
 #define MFGP_MF 1           /* MFGP, gaussian_process.py:271-578, hyp [mu_lo,s2_lo,L_lo,mu_hi,s2_hi,
                                L_hi,rho,noise_lo,noise_hi] (all log-scaled, simulator.py:53-56)     */
 #define MFGP_F64 0
-#define MFGP_F32 1          /* reserved (config 5); not accepted yet */
+#define MFGP_F32 1          /* BASELINE configs[4]: the resident V = L^-1 psi^T stored and streamed
+                               in fp32; factor, solves and reductions fp64. Tolerance vs the fp64
+                               oracle: oracle/gp_oracle.py parity_errors_f32 (F32_TOL = 1e-4) */
 
 #define MFGP_ASYNC 1        /* batch flag: do not synchronise; status via mfgp_ctx_synchronize */
 
