@@ -320,6 +320,9 @@ def main():
             mdl.set_grid(wl.xs)
             mdl.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
             models.append(mdl)
+        # the posterior of the base rows (N - k), as the simulator predicts before
+        # every update (sim:885-892); the incremental steps start from it
+        _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
         varmax = torch.zeros(total, B, dtype=torch.float64, device=dev)
 
         def step(s):
@@ -396,6 +399,7 @@ def main():
         assert inc["stats"]["inc_factor"] >= K and inc["stats"]["vstream"] >= K, inc["stats"]
         n0 = N - k
         es = 4 if f32 else 8
+        lattice = inc["stats"].get("lattice", 0) >= K
         # algorithmic bytes of one k_inc_stream launch: V_old read once, V_new written,
         # grid read and mu / var written, and per training row the L21 gather, its
         # store into A and read back, the compact rows and z
@@ -405,6 +409,15 @@ def main():
             vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (3 * k + 1))
         v_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
         v_gbs = vbytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
+        # the lattice-separable step (k_inc_lat): its work is
+        # the GEMM over the separable terms, 2 KA M n_terms flop per GP (KA = 8 rows
+        # of new points, n_terms = n0 + the hifi rows' second term), plus the w pass
+        # over F's lower triangle (MFMA, 16 rows: 16 n0^2 flop) -- f64 MFMA-bound
+        ka = 8 if k <= 8 else 16
+        n_terms = n0 + (n0 - NL)
+        lat_flops = B * (2 * ka * M * n_terms + 16 * n0 * n0)
+        lat_bytes = B * 8 * (n0 * n0 / 2 + M * (k + 4) + n_terms * G * 2 + 3 * n0 * k)
+        lat_tf = lat_flops / (v_ms * 1e-3) / 1e12 if v_ms > 0 else float("nan")
         value = world * B * K / elapsed
         # SURVEY.md section 8d's algorithmic cost of one update as the reference
         # computes it (refactor + V from scratch): F = N^3/3 + M N^2 + 2 N^2 + 4 M N flop,
@@ -417,9 +430,35 @@ def main():
         default_cfg = (a.workload, G, NL, NH, B, k, a.hyp, a.dtype) == ("headline", 128, 1024, 1024, 8, 8,
                                                                          "australia8_mf", "f64")
         c4_cfg = (G, NL, NH, B, a.hyp, a.dtype) == (256, 4096, 4096, 32, "australia9_mf", "f32")
-        kern = "k_inc_stream" if FUSED else "k_vstream"
+        kern = "k_inc_lat" if lattice else ("k_inc_stream" if FUSED else "k_vstream")
         traffic, traffic_src = pmc_traffic(kern, "configs4" if c4_cfg else None) if (default_cfg or c4_cfg) \
             else (None, None)
+        if lattice:
+            update = ("incremental, lattice-separable, one launch per step (k_inc_lat): bordered-Cholesky append, "
+                      "w = K11^-1 K12 from the resident L^-1, the SE kernel's separability over the grid axes turns "
+                      "L21 V_old into an f64 MFMA GEMM over the training terms (no pass over V), mean / variance "
+                      "updated from the previous posterior")
+            roof = {"bound": "mfma", "achieved": lat_tf, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
+                    "frac": lat_tf / PEAK_F64_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": kern, "flops_per_launch": lat_flops, "bytes_per_launch": lat_bytes,
+                    "hbm_gbs": lat_bytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan"),
+                    "avg_launch_ms": v_ms, "launches_timed": tm["predict_launches"],
+                    "timing": f"HIP events around every {inc['stride']}th launch of the timed region",
+                    "design_note": f"flops_per_launch = B x (2 KA M n_terms + 16 n0^2): the separable GEMM (KA={ka}, "
+                                   f"n_terms={n_terms}) and the w pass; bytes = F's lower triangle, the outputs and "
+                                   "new V rows, the tables (DESIGN.md section 2.4)"}
+        else:
+            update = ("incremental, one launch per step (k_inc_stream): bordered-Cholesky append + one pass over "
+                      "the resident V = L^-1 psi^T" if FUSED else
+                      "incremental: bordered-Cholesky append (k_inc_stream) + one pass over the resident "
+                      "V = L^-1 psi^T (k_vstream)")
+            roof = {"bound": "hbm", "achieved": v_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": v_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": kern, "bytes_per_launch": vbytes, "avg_launch_ms": v_ms,
+                    "launches_timed": tm["predict_launches"],
+                    "timing": f"HIP events around every {inc['stride']}th launch of the timed region",
+                    "design_bytes_note": f"{es}-byte V: bytes_per_launch = the resident V read once plus the new "
+                                         "rows, grid, outputs and per-row L21 / z terms (DESIGN.md section 4)"}
         if default_cfg:
             wl_name = "australia8_mf MFGP seed ensemble (BASELINE configs[3])"
         elif c4_cfg:
@@ -445,30 +484,19 @@ def main():
                             f"samples appended per update), factor update + mean/var at every cell, "
                             + ("MFGP_F32: V = L^-1 psi^T stored and streamed in fp32, factor / solves / "
                                "reductions in fp64" if f32 else "fp64"),
-                "update": ("incremental, one launch per step (k_inc_stream): bordered-Cholesky append + one "
-                           "pass over the resident V = L^-1 psi^T" if FUSED else
-                           "incremental: bordered-Cholesky append (k_inc_stream) + one pass over the resident "
-                           "V = L^-1 psi^T (k_vstream)") + "; full_recompute below is the reference's per-update work",
+                "update": update + "; full_recompute below is the reference's per-update work",
                 "seeds_per_gpu": B, "grid": G, "N_train": N, "N_lofi": NL, "N_hifi": NH, "agents": k,
                 "global_seeds": world * B, "parallelism": f"seed-sharded x{world}, 1 RCCL all_gather",
             },
-            "roofline": {
-                "bound": "hbm", "achieved": v_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": v_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": kern, "bytes_per_launch": vbytes, "avg_launch_ms": v_ms,
-                "launches_timed": tm["predict_launches"],
-                "timing": f"HIP events around every {inc['stride']}th launch of the timed region",
-                "design_bytes_note": f"{es}-byte V: bytes_per_launch = the resident V read once plus the new rows, "
-                                     "grid, outputs and per-row L21 / z terms (DESIGN.md section 4)",
-            },
+            "roofline": roof,
             "algorithmic_8d": {
                 "flops_per_update": F8d, "bytes_per_update": B8d,
                 "flop_equivalent_tflops": F8d * value / 1e12,
                 "frac_of_f64_mfma_peak": F8d * value / 1e12 / PEAK_F64_TFLOPS,
                 "byte_rate_gbs": B8d * value / 1e9,
                 "note": "SURVEY.md 8d's per-update work is the reference's (refactor + V from scratch); the "
-                        "incremental path reuses the resident V, so this flop-equivalent rate is above the MFMA "
-                        "peak by construction; the roofline above is the kernel's own (HBM, its bytes)",
+                        "incremental path does not recompute V, so this flop-equivalent rate is above the MFMA "
+                        "peak by construction; the roofline above is the kernel's own work",
             },
             "host_enqueue_ms_per_step": inc["host_ms"],
             "breakdown_ms_per_step": inc["breakdown"],

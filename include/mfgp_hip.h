@@ -73,6 +73,17 @@ int mfgp_ctx_set_fused(mfgp_ctx* ctx, int enable);
  * call instead of by mfgp_append (the reference raises in updt / updt_hifi,
  * gp:254 / gp:529). */
 int mfgp_ctx_set_deferred_appends(mfgp_ctx* ctx, int enable);
+/* Lattice-separable appends (default on): when the grid is a lattice, kss /
+ * (smallest noise + jitter) <= 1e4 and the model holds the posterior of the old
+ * rows, a bordered append + predict of k <= 16 rows runs as k_inc_lat: w =
+ * K11^-1 K12 from the resident explicit inverse L^-1, then the SE kernel's
+ * separability over the two lattice axes turns L21 V_old into a GEMM over the
+ * training terms (f64 MFMA) -- no pass over V -- and var / mu are updated from the
+ * previous posterior. Batches with too few GEMM tiles to fill the GPU (one GP
+ * at the headline size) keep the V stream; 2 = take it for them too (tests).
+ * 0 = always the V stream (k_inc_stream). Same numbers to rounding (DESIGN.md
+ * section 2.4). */
+int mfgp_ctx_set_lattice(mfgp_ctx* ctx, int enable);
 /* Kernel timing with HIP events on the launch stream: enable = 1 times every
  * predict-kernel launch (fused predict or one-pass incremental predict) and
  * every factor stage; 2 times the predict launches only (each event pair is a
@@ -127,8 +138,8 @@ int64_t mfgp_model_nl(const mfgp_model* m);
 int64_t mfgp_model_m(const mfgp_model* m);
 /* Path introspection (tests / benchmarks): out[0..n) = {factor rows (-1 = none),
  * resident V rows, full refactors, bordered appends, full predicts, one-pass
- * predicts, grid lattice axes nx, ny (0 = the grid is not a lattice: appends
- * locate new points by a scan)}. */
+ * predicts (V stream or lattice step), grid lattice axes nx, ny (0 = the grid is
+ * not a lattice: appends locate new points by a scan), lattice steps}. */
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n);
 /* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
 int mfgp_get_factor(mfgp_model* m, double* L_out);

@@ -32,6 +32,7 @@ SIGNATURES = {
     "mfgp_ctx_set_incremental": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_deferred_appends": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mfgp_ctx_set_lattice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_timing_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "mfgp_batch_append_predict_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -158,6 +159,13 @@ class Context:
         the reference; deferred, it raises in the predict that runs it)."""
         check(lib().mfgp_ctx_set_deferred_appends(self.handle, 1 if on else 0))
 
+    def set_lattice(self, on=True):
+        """Lattice-separable appends (k_inc_lat, default on where they apply: lattice
+        grid, kss / (noise + jitter) <= 1e4, the old rows' posterior resident, enough
+        GEMM tiles in the batch to fill the GPU), or always the one-pass V stream.
+        on="force": also for batches too small to fill the GPU (tests)."""
+        check(lib().mfgp_ctx_set_lattice(self.handle, 2 if on == "force" else (1 if on else 0)))
+
     def enable_timing(self, on=True, predict_only=False):
         """HIP-event timing of the predict launches (and, unless predict_only, the factor stages)."""
         check(lib().mfgp_ctx_enable_timing(self.handle, (2 if predict_only else 1) if on else 0))
@@ -272,11 +280,13 @@ class Model:
 
     def stats(self):
         """{factor_rows, v_rows, full_factor, inc_factor, full_predict, vstream} (path
-        counters) and the grid's lattice axes {lattice_nx, lattice_ny} (0: not a lattice)."""
-        out = (ctypes.c_int64 * 8)()
-        check(lib().mfgp_model_stats(self.handle, out, 8))
+        counters; vstream counts every one-pass predict, lattice steps included), the
+        grid's lattice axes {lattice_nx, lattice_ny} (0: not a lattice) and {lattice}:
+        the steps that took the lattice-separable path (k_inc_lat)."""
+        out = (ctypes.c_int64 * 9)()
+        check(lib().mfgp_model_stats(self.handle, out, 9))
         keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream",
-                "lattice_nx", "lattice_ny")
+                "lattice_nx", "lattice_ny", "lattice")
         return dict(zip(keys, (int(v) for v in out)))
 
     def sample_points(self, threshold, max_points):

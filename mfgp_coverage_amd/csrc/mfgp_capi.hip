@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -45,6 +46,11 @@ constexpr int RING = 64;       // descriptor upload slots
 constexpr int MAXB = 256;      // GPs per launch
 constexpr int64_t MAX_FULL_CAP = 16319;   // largest training capacity the full predict serves (ld <= 16383)
 constexpr size_t F32_SCRATCH = size_t(16) << 30;   // bytes of fp64 V scratch for MFGP_F32 full predicts
+// lattice-separable step (k_inc_lat): taken when kss / (smallest noise + jitter)
+// <= LAT_RMAX (its error grows with the conditioning of K),
+// and for at most LAT_MAXD consecutive steps before var / mu are recomputed from V
+constexpr double LAT_RMAX = 1e4;
+constexpr int LAT_MAXD = 256;
 
 struct EvPair {
   hipEvent_t a, b;
@@ -91,6 +97,9 @@ struct mfgp_ctx {
   bool incremental = true;
   bool fused = true;          // bordered append + one-pass predict in one launch (k_inc_stream)
   bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
+  bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
+  int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
+  bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
   // pinned host staging of the status words
   int* h_status = nullptr;
   size_t h_status_n = 0;
@@ -147,7 +156,32 @@ struct mfgp_model {
   bool spec_valid = false;
   bool pred_since_append = false;   // a predict came after the last append
   // path counters (mfgp_model_stats)
-  int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0;
+  int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0, n_lattice = 0;
+  // state generation: a new factor from scratch, a new grid or new hyperparameters
+  // start a new one (the resident posterior, F and the tables belong to one)
+  uint64_t gen = 1;
+  // resident posterior: two buffers [mu | var] of M each, written by every predict
+  // (incremental mode); buffer b holds the posterior of the res_n[b] leading rows
+  double* res = nullptr;
+  int64_t res_M = 0;
+  int64_t res_n[2] = {-1, -1};
+  uint64_t res_gen[2] = {0, 0};
+  int res_depth[2] = {0, 0};   // lattice steps since var / mu were computed from V
+  uint64_t res_tick[2] = {0, 0}, tick = 0;
+  // lattice-separable step state (allocated on first use)
+  double* F = nullptr;        // explicit L^-1 [F_ld][F_ld], rows [0, F_n) current for generation F_gen
+  int64_t F_ld = 0, F_n = 0;
+  uint64_t F_gen = 0;
+  double* tab = nullptr;      // separable tables [4][tab_ld][tabw], rows [0, tab_n)
+  int64_t tab_ld = 0, tabw = 0, tab_n = 0;
+  uint64_t tab_gen = 0;
+  double* wv = nullptr;       // w [wv_ld][KINC]
+  int64_t wv_ld = 0;
+  unsigned* wflag = nullptr;  // [wv_ld / 64 + 2]
+  double* gpart = nullptr;    // split-K partials
+  size_t gpart_n = 0;
+  unsigned* gcnt = nullptr;   // per GEMM tile
+  int64_t gcnt_n = 0;
 };
 
 namespace {
@@ -292,7 +326,30 @@ int ensure_cap(mfgp_model* m, int64_t need) {
     HIP_TRY(hipMemcpyAsync(Li, m->Linv, sizeof(double) * (m->ld / NB) * TILE, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(zv, m->zv, sizeof(double) * m->cap, hipMemcpyDeviceToDevice, c->stream));
   }
+  // the lattice step's F and tables move to the new leading dimension too
+  double *F = nullptr, *tab = nullptr;
+  if (keep && m->F && m->F_n > 0) {
+    HIP_TRY(hipMalloc(&F, sizeof(double) * ld * ld));
+    HIP_TRY(hipMemsetAsync(F, 0, sizeof(double) * ld * ld, c->stream));
+    HIP_TRY(hipMemcpy2DAsync(F, sizeof(double) * ld, m->F, sizeof(double) * m->F_ld, sizeof(double) * m->F_ld,
+                             m->F_ld, hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (m->tab && m->tab_n > 0) {
+    HIP_TRY(hipMalloc(&tab, sizeof(double) * 4 * ld * m->tabw));
+    HIP_TRY(hipMemsetAsync(tab, 0, sizeof(double) * 4 * ld * m->tabw, c->stream));
+    for (int t = 0; t < 4; ++t)
+      HIP_TRY(hipMemcpyAsync(tab + (size_t)t * ld * m->tabw, m->tab + (size_t)t * m->tab_ld * m->tabw,
+                             sizeof(double) * m->tab_n * m->tabw, hipMemcpyDeviceToDevice, c->stream));
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (m->F) HIP_TRY(hipFree(m->F));
+  if (m->tab) HIP_TRY(hipFree(m->tab));
+  m->F = F;
+  m->F_ld = F ? ld : 0;
+  if (!F) m->F_n = 0;
+  m->tab = tab;
+  m->tab_ld = tab ? ld : 0;
+  if (!tab) m->tab_n = 0;
   if (m->X) HIP_TRY(hipFree(m->X));
   if (m->y) HIP_TRY(hipFree(m->y));
   if (m->A) HIP_TRY(hipFree(m->A));
@@ -427,8 +484,148 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.n0 = 0;
   d.vres = 0;
   d.ablk = m->ablk;
+  d.F = nullptr;
+  d.tab = nullptr;
+  d.wv = nullptr;
+  d.wflag = nullptr;
+  d.gpart = nullptr;
+  d.gcnt = nullptr;
+  d.rmu_in = nullptr;
+  d.rvar_in = nullptr;
+  d.rmu = nullptr;
+  d.rvar = nullptr;
+  d.tabw = 0;
+  d.tab_lo = 0;
+  d.ka = 8;
+  d.ksplit = 1;
+  d.lat_tiles = 0;
+  d.nwb = 0;
+  d.lat_fbuild = 0;
   d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
   d.hp = d.hf;
+}
+
+// ---- resident posterior (two buffers, tagged with the rows and generation) ----
+int ensure_res(mfgp_model* m) {
+  if (m->res && m->res_M >= m->M) return MFGP_OK;
+  HIP_TRY(hipStreamSynchronize(m->ctx->stream));
+  if (m->res) HIP_TRY(hipFree(m->res));
+  m->res = nullptr;
+  m->res_M = 0;
+  m->res_n[0] = m->res_n[1] = -1;
+  HIP_TRY(hipMalloc(&m->res, sizeof(double) * 4 * (size_t)m->M));
+  m->res_M = m->M;
+  return MFGP_OK;
+}
+double* res_mu(mfgp_model* m, int b) { return m->res + (size_t)b * 2 * m->res_M; }
+double* res_var(mfgp_model* m, int b) { return m->res + (size_t)b * 2 * m->res_M + m->res_M; }
+// the buffer holding the posterior of the n leading rows (-1: none)
+int res_find(const mfgp_model* m, int64_t n) {
+  for (int b = 0; b < 2; ++b)
+    if (m->res && m->res_n[b] == n && m->res_gen[b] == m->gen) return b;
+  return -1;
+}
+// the buffer a predict writes: not `keep`, else the least recently written
+int res_out(const mfgp_model* m, int keep) {
+  if (keep >= 0) return 1 - keep;
+  return m->res_tick[0] <= m->res_tick[1] ? 0 : 1;
+}
+void res_tag(mfgp_model* m, int b, int64_t n, int depth) {
+  m->res_n[b] = n;
+  m->res_gen[b] = m->gen;
+  m->res_depth[b] = depth;
+  m->res_tick[b] = ++m->tick;
+}
+// Point a predict descriptor's resident outputs at a buffer (incremental mode);
+// returns the buffer (-1: none). Tag it once the launch is enqueued.
+int set_res_out(mfgp_model* m, GPDesc& d, int keep) {
+  if (!m->ctx->incremental || m->M <= 0 || ensure_res(m) != MFGP_OK) return -1;
+  const int b = res_out(m, keep);
+  d.rmu = res_mu(m, b);
+  d.rvar = res_var(m, b);
+  return b;
+}
+
+// ---- lattice-separable step ----
+bool lat_cond_ok(const mfgp_model* m) {
+  const Hyp h = derive_hyp(m->kind, m->hyp, m->jitter);
+  const double noise = (m->kind == MFGP_SF ? h.noiseL : std::min(h.noiseL, h.noiseH)) + h.jitter;
+  return noise > 0.0 && h.kss / noise <= LAT_RMAX;
+}
+int64_t lat_tabw(const mfgp_model* m) { return round_up(std::max<int64_t>(m->lat.nx, m->lat.ny), 64); }
+int64_t lat_tiles(const mfgp_model* m, int ka) {
+  return ((m->lat.nx + 64 / ka - 1) / (64 / ka)) * ((m->lat.ny + 63) / 64);
+}
+// Can the bordered append of rows [n0, N) and its predict take k_inc_lat?
+bool lat_eligible(const mfgp_model* m, int64_t n0) {
+  const int64_t k = m->NL + m->NH - n0;
+  if (!m->ctx->lattice || m->lat.nx <= 0 || m->M <= 0 || k < 1 || k > KINC || n0 < 1) return false;
+  if (!lat_cond_ok(m)) return false;
+  const int b = res_find(m, n0);
+  return b >= 0 && m->res_depth[b] < LAT_MAXD;
+}
+// F, the tables, w and the flags at the model's leading dimension (contents kept
+// across capacity growth: ensure_cap moves them)
+int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit) {
+  hipStream_t s = m->ctx->stream;
+  const int64_t ld = m->ld, tabw = lat_tabw(m);
+  if (!m->F || m->F_ld != ld) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->F) HIP_TRY(hipFree(m->F));
+    m->F = nullptr;
+    HIP_TRY(hipMalloc(&m->F, sizeof(double) * ld * ld));
+    HIP_TRY(hipMemsetAsync(m->F, 0, sizeof(double) * ld * ld, s));   // F's upper triangle stays zero
+    m->F_ld = ld;
+    m->F_n = 0;
+  }
+  if (!m->tab || m->tab_ld != ld || m->tabw != tabw) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->tab) HIP_TRY(hipFree(m->tab));
+    m->tab = nullptr;
+    HIP_TRY(hipMalloc(&m->tab, sizeof(double) * 4 * ld * tabw));
+    HIP_TRY(hipMemsetAsync(m->tab, 0, sizeof(double) * 4 * ld * tabw, s));
+    m->tab_ld = ld;
+    m->tabw = tabw;
+    m->tab_n = 0;
+  }
+  if (!m->wv || m->wv_ld != ld) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->wv) HIP_TRY(hipFree(m->wv));
+    if (m->wflag) HIP_TRY(hipFree(m->wflag));
+    m->wv = nullptr;
+    m->wflag = nullptr;
+    HIP_TRY(hipMalloc(&m->wv, sizeof(double) * ld * KINC));
+    HIP_TRY(hipMemsetAsync(m->wv, 0, sizeof(double) * ld * KINC, s));
+    HIP_TRY(hipMalloc(&m->wflag, sizeof(unsigned) * (ld / 64 + 2)));
+    HIP_TRY(hipMemsetAsync(m->wflag, 0, sizeof(unsigned) * (ld / 64 + 2), s));   // below every epoch
+    m->wv_ld = ld;
+  }
+  if (m->gcnt_n < tiles) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->gcnt) HIP_TRY(hipFree(m->gcnt));
+    m->gcnt = nullptr;
+    HIP_TRY(hipMalloc(&m->gcnt, sizeof(unsigned) * tiles));
+    HIP_TRY(hipMemsetAsync(m->gcnt, 0, sizeof(unsigned) * tiles, s));
+    m->gcnt_n = tiles;
+  }
+  const size_t need = ksplit > 1 ? (size_t)tiles * ksplit * 4096 : 0;
+  if (need > m->gpart_n) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->gpart) HIP_TRY(hipFree(m->gpart));
+    m->gpart = nullptr;
+    HIP_TRY(hipMalloc(&m->gpart, sizeof(double) * need));
+    m->gpart_n = need;
+  }
+  return MFGP_OK;
+}
+void free_lat(mfgp_model* m) {
+  if (m->F) (void)hipFree(m->F);
+  if (m->tab) (void)hipFree(m->tab);
+  if (m->wv) (void)hipFree(m->wv);
+  if (m->wflag) (void)hipFree(m->wflag);
+  if (m->gpart) (void)hipFree(m->gpart);
+  if (m->gcnt) (void)hipFree(m->gcnt);
+  if (m->res) (void)hipFree(m->res);
 }
 
 // Enqueue assembly + blocked Cholesky for `count` models (descriptors already uploaded).
@@ -616,6 +813,25 @@ int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
   return ev_end(c, ev);
 }
 
+// Lattice-separable appends + predicts (k_inc_lat), after the explicit inverses
+// and the separable tables they need (k_trinv_f / k_lat_tables: only when a model
+// enters the mode with a new factor, grid or hyperparameters).
+int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
+  int64_t max_blocks = 0, max_nbr = 0, max_rows = 0;
+  for (int i = 0; i < count; ++i) {
+    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwb + (int64_t)hd[i].lat_tiles * hd[i].ksplit);
+    if (hd[i].lat_fbuild) max_nbr = std::max(max_nbr, nblocks_rows(hd[i].n0));
+    max_rows = std::max(max_rows, hd[i].n0 - hd[i].tab_lo);
+  }
+  if (max_nbr > 0) HIP_TRY(launch_trinv_f(dd, count, max_nbr, c->stream));
+  if (max_rows > 0) HIP_TRY(launch_lat_tables(dd, count, max_rows, c->stream));
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 0);
+  if (rc) return rc;
+  HIP_TRY(launch_inc_lat(dd, count, max_blocks, hd[0].ka, hd[0].vf32, c->stream));
+  return ev_end(c, ev);
+}
+
 // Row splits of the one-pass predict for a launch over these descriptors: 128-cell
 // workgroups while they fill the chip (~4 per CU), else 64 or 32 cells with the
 // rows split 2 or 4 ways (the drop-in simulator predicts one GP at a time).
@@ -654,6 +870,7 @@ bool can_vstream(const mfgp_model* m) {
 
 void mark_full_factor(mfgp_model* m) {
   m->n_full_factor += 1;
+  m->gen += 1;   // a factor from scratch: new rounding of everything derived from it
   m->factored = true;
   m->factor_N = m->NL + m->NH;
   std::memcpy(m->factor_hyp, m->hyp, sizeof(m->hyp));
@@ -784,6 +1001,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
       c->ncu = ncu;
   }
   c->stream = c->own;
+  if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   HIP_TRY(hipHostMalloc(&c->h_ring, sizeof(GPDesc) * RING * MAXB, hipHostMallocDefault));
   HIP_TRY(hipMalloc(&c->d_ring, sizeof(GPDesc) * RING * MAXB));
   for (int i = 0; i < RING; ++i) {
@@ -875,6 +1093,14 @@ int mfgp_ctx_set_deferred_appends(mfgp_ctx* c, int enable) {
   return MFGP_OK;
 }
 
+int mfgp_ctx_set_lattice(mfgp_ctx* c, int enable) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->lattice = enable != 0;
+  c->lat_force = enable == 2;
+  return MFGP_OK;
+}
+
 int mfgp_ctx_enable_timing(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   c->timing = (enable == 2) ? 2 : (enable != 0 ? 1 : 0);
@@ -957,6 +1183,7 @@ void mfgp_model_destroy(mfgp_model* m) {
   if (m->V) (void)hipFree(m->V);
   if (m->tred) (void)hipFree(m->tred);
   if (m->sync) (void)hipFree(m->sync);
+  free_lat(m);
   delete m;
 }
 
@@ -1013,7 +1240,10 @@ int mfgp_model_set_hyp(mfgp_model* m, const double* hyp, int nhyp, double jitter
   if (rc) return rc;
   if (!hyp || nhyp != m->nhyp)
     return set_err(MFGP_ERR_ARG, "Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)");
-  if (jitter != m->jitter || std::memcmp(hyp, m->hyp, sizeof(double) * nhyp) != 0) m->spec_valid = false;
+  if (jitter != m->jitter || std::memcmp(hyp, m->hyp, sizeof(double) * nhyp) != 0) {
+    m->spec_valid = false;
+    m->gen += 1;
+  }
   std::memcpy(m->hyp, hyp, sizeof(double) * nhyp);
   m->jitter = jitter;
   return MFGP_OK;
@@ -1068,6 +1298,7 @@ int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
   mfgp_ctx* c = m->ctx;
   m->v_n = 0;   // V columns belong to the previous grid
   m->spec_valid = false;
+  m->gen += 1;
   if (M > m->Mcap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (m->grid) HIP_TRY(hipFree(m->grid));
@@ -1140,6 +1371,10 @@ int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
     const int64_t N = m->NL + m->NH;
     if (m->factored && m->factor_N > N) m->factor_N = N;
     m->v_n = std::min(m->v_n, N);
+    m->F_n = std::min(m->F_n, N);
+    m->tab_n = std::min(m->tab_n, N);
+    for (int b = 0; b < 2; ++b)
+      if (m->res_n[b] > N) m->res_n[b] = -1;   // the posterior of rows that are gone
   }
   return MFGP_OK;
 }
@@ -1207,6 +1442,7 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   fill_desc(hd[0], m);
   hd[0].mu = kmu;
   hd[0].var = kvar;
+  const int rb = set_res_out(m, hd[0], -1);
   const bool vst = can_vstream(m);
   set_vstream_rows(hd[0], m);
   set_rsplit(c, hd, 1);
@@ -1216,6 +1452,7 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   if ((rc = vst ? enqueue_vstream(c, dd, hd, 1) : enqueue_predict(c, dd, hd, 1))) return rc;
   (vst ? m->n_vstream : m->n_full_predict) += 1;
   m->v_n = m->NL + m->NH;
+  if (rb >= 0) res_tag(m, rb, m->v_n, 0);
   if ((rc = release_slot(c, slot))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   model_out_done(m, mu, var, host);
@@ -1226,9 +1463,9 @@ int64_t mfgp_model_n(const mfgp_model* m) { return m ? m->NL + m->NH : -1; }
 
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
   if (!m || !out) return set_err(MFGP_ERR_ARG, "null model/out");
-  const int64_t v[8] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
-                        m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny};
-  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  const int64_t v[9] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+                        m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice};
+  for (int i = 0; i < n && i < 9; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
@@ -1292,6 +1529,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
   }
   std::vector<mfgp_model*> order, porder;
   std::vector<int64_t> oo_ord;
+  std::vector<int> res_b, res_depth;
   constexpr int CB = MAXB / 2;   // one descriptor slot per sub-batch: [factor order | predict order]
   for (int b0 = 0; b0 < count; b0 += CB) {
     const int nb = std::min(CB, count - b0);
@@ -1361,9 +1599,11 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         }
       np = (int)porder.size();
       while (nv < np && can_vstream(porder[nv])) ++nv;
+      res_b.assign(np, -1);
       for (int i = 0; i < np; ++i) {
         GPDesc& pd = hd[nb + i];
         fill_desc(pd, porder[i]);
+        res_b[i] = set_res_out(porder[i], pd, -1);
         if (i < nv) set_vstream_rows(pd, porder[i]);
         pd.mu = mu + oo_ord[i];
         pd.var = var + oo_ord[i];
@@ -1385,7 +1625,63 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.var = pd.var;
         fd.vmax = pd.vmax;
         fd.vargmax = pd.vargmax;
+        fd.rmu = pd.rmu;
+        fd.rvar = pd.rvar;
         fd.tiles = 1;
+      }
+    }
+    // lattice grids, well-conditioned K and a resident posterior of the old rows:
+    // the separable step (k_inc_lat) instead of the V stream
+    bool lat = fuse;
+    for (int i = 0; lat && i < ninc; ++i) lat = lat_eligible(order[i], hd[i].n0);
+    res_depth.assign(ninc, 0);
+    int ka = 8;
+    int64_t tiles_sum = 0, ns_min = INT64_MAX;
+    if (lat) {
+      for (int i = 0; i < ninc; ++i) {
+        if (order[i]->NL + order[i]->NH - hd[i].n0 > 8) ka = 16;
+      }
+      for (int i = 0; i < ninc; ++i) {
+        const mfgp_model* m = order[i];
+        tiles_sum += lat_tiles(m, ka);
+        const int64_t nwb = (hd[i].n0 + 63) / 64;
+        const int64_t jh = m->kind == MFGP_SF ? nwb : std::min(m->NL / 64, nwb);
+        ns_min = std::min(ns_min, (nwb - jh) * 8 + jh * 4);
+      }
+      // too few GEMM tiles to fill the chip (one GP at the headline size: 32 tiles):
+      // the w pass and the split-K reductions cost more than the V stream they save
+      if (tiles_sum * 2 < c->ncu && !c->lat_force) lat = false;
+    }
+    if (lat) {
+      // split-K so that the GEMM tiles fill the chip about twice, >= 4 stages each
+      int S = (int)std::min<int64_t>(8, std::max<int64_t>(1, (2 * c->ncu + tiles_sum - 1) / tiles_sum));
+      S = (int)std::max<int64_t>(1, std::min<int64_t>(S, ns_min / 4));
+      if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, ns_min / 4));
+      for (int i = 0; i < ninc; ++i) {
+        mfgp_model* m = order[i];
+        GPDesc& fd = hd[i];
+        const int64_t tiles = lat_tiles(m, ka);
+        if ((rc = ensure_lat(m, tiles, S))) return rc;
+        const int bin = res_find(m, fd.n0);
+        fd.rmu_in = res_mu(m, bin);
+        fd.rvar_in = res_var(m, bin);
+        fd.rmu = res_mu(m, 1 - bin);
+        fd.rvar = res_var(m, 1 - bin);
+        res_b[i] = 1 - bin;
+        res_depth[i] = m->res_depth[bin] + 1;
+        fd.F = m->F;
+        fd.tab = m->tab;
+        fd.tabw = m->tabw;
+        fd.wv = m->wv;
+        fd.wflag = m->wflag;
+        fd.gpart = m->gpart;
+        fd.gcnt = m->gcnt;
+        fd.ka = ka;
+        fd.ksplit = S;
+        fd.lat_tiles = (int)tiles;
+        fd.nwb = (int)((fd.n0 + 63) / 64);
+        fd.lat_fbuild = (m->F_gen == m->gen && m->F_n >= fd.n0) ? 0 : 1;
+        fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }
     }
     if (nv > 0) {
@@ -1395,7 +1691,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     if (np > nv && (rc = assign_predict_scratch(c, hd + nb + nv, np - nv))) return rc;
     // one GP, append + one-pass predict fused, nothing else: launch with the
     // descriptor by value (no upload) and the status published into a mapped word
-    if (fuse && nb == 1 && ninc == 1 && np == 1 && nv == 1) {
+    if (fuse && !lat && nb == 1 && ninc == 1 && np == 1 && nv == 1) {
       mfgp_model* m = order[0];
       if (!m->status_host) {
         HIP_TRY(hipHostMalloc(&m->status_host, sizeof(int), hipHostMallocMapped));
@@ -1418,21 +1714,33 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       if ((rc = release_slot(c, slot))) return rc;
       m->v_n = m->NL + m->NH;
       m->n_vstream += 1;
+      if (res_b[0] >= 0) res_tag(m, res_b[0], m->v_n, 0);
       continue;
     }
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
     if (do_factor) {
       if (dev_src && nfull > 0) HIP_TRY(launch_append(dd + ninc, nfull, c->stream));
-      if (ninc > 0 && (rc = fuse ? enqueue_inc_stream(c, dd, hd, ninc) : enqueue_inc_factor(c, dd, hd, ninc))) return rc;
+      if (ninc > 0 && (rc = lat ? enqueue_inc_lat(c, dd, hd, ninc)
+                                : (fuse ? enqueue_inc_stream(c, dd, hd, ninc) : enqueue_inc_factor(c, dd, hd, ninc))))
+        return rc;
       if (nfull > 0 && (rc = enqueue_factor(c, dd + ninc, hd + ninc, nfull))) return rc;
     }
     if (nv > 0 && !fuse && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
     if (np > nv && (rc = enqueue_predict(c, dd + nb + nv, hd + nb + nv, np - nv))) return rc;
     if ((rc = release_slot(c, slot))) return rc;
     for (int i = 0; i < np; ++i) {
-      porder[i]->v_n = porder[i]->NL + porder[i]->NH;
-      (i < nv ? porder[i]->n_vstream : porder[i]->n_full_predict) += 1;
+      mfgp_model* m = porder[i];
+      m->v_n = m->NL + m->NH;
+      (i < nv ? m->n_vstream : m->n_full_predict) += 1;
+      if (res_b[i] >= 0) res_tag(m, res_b[i], m->v_n, (lat && i < ninc) ? res_depth[i] : 0);
+      if (lat && i < ninc) {
+        m->n_lattice += 1;
+        m->F_n = m->v_n;   // F's new rows and the new rows' tables came with the step
+        m->F_gen = m->gen;
+        m->tab_n = m->v_n;
+        m->tab_gen = m->gen;
+      }
     }
   }
   if (flags & MFGP_ASYNC) return MFGP_OK;

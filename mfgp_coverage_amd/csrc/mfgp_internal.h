@@ -98,6 +98,24 @@ struct GPDesc {
   int l21c_ok;         // one-pass predict: l21c holds the rows [n0, N) bordered onto V's n0 rows
   int rsplit;          // one-pass predict: row splits per cell group (1, 2, 4; 128 / rsplit cells per workgroup)
   int vf32;            // 1 = the resident V is Vf (fp32; the one-pass predict streams 256 cells per workgroup)
+  // lattice-separable step (k_inc_lat, mfgp_lattice.inl)
+  double* F;           // explicit L^-1, [ld][ld] column-major: lower triangle, zeros above
+  double* tab;         // separable tables [4][ld][tabw]: c_L(j) ex_L, ey_L, c_H(j) ex_H, ey_H per training row j
+  double* wv;          // w = L11^-T L21^T, [ld][KINC] (row j: w[j][0..KINC))
+  unsigned* wflag;     // per 64-row block of w: the epoch of the launch that stored it
+  double* gpart;       // split-K partial tiles [lat_tiles][ksplit][LAT_PART]
+  unsigned* gcnt;      // per GEMM tile: arrivals of its splits (zero between launches)
+  const double* rmu_in;   // resident posterior (mean, variance) of the n0 leading rows, [M]
+  const double* rvar_in;
+  double* rmu;         // resident posterior out [M]: every predict kernel writes it when non-null
+  double* rvar;
+  int64_t tabw;        // row width of the tables (a multiple of 64, >= nx, ny)
+  int64_t tab_lo;      // k_lat_tables: rows [tab_lo, n0) are filled
+  int ka;              // rows (new points) of a cell group in the GEMM: 8 (k <= 8) or 16
+  int ksplit;          // split-K factor of the GEMM tiles
+  int lat_tiles;       // GEMM tiles per GP: ceil(nx / (64 / ka)) * ceil(ny / 64)
+  int nwb;             // 64-row blocks of w: ceil(n0 / 64)
+  int lat_fbuild;      // k_trinv_f: 1 = compute F for the n0 factor rows
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -132,6 +150,13 @@ hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int
 // the same for ONE GP with its descriptor passed by value (kernel argument): no
 // descriptor upload, and with rows_inline no row copies either
 hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s);
+// lattice-separable append + predict (k_inc_lat); max_blocks = max over GPs of
+// nprod + nwb + lat_tiles * ksplit
+hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
+// separable tables of rows [tab_lo, n0); max_rows = max over GPs of n0 - tab_lo
+hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s);
+// F = L^-1 of the n0 factor rows (block column per workgroup); max_nbr = max nblocks_rows(n0)
+hipError_t launch_trinv_f(const GPDesc* d, int count, int64_t max_nbr, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s);
 // MFGP_F32 full predict: round the fp64 V that k_predict wrote into d.V (rows [0, N)
 // of every tile) into the resident fp32 V (d.Vf)

@@ -787,6 +787,10 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
     if (c < M) {
       d.mu[c] = ms + h.meanH;
       d.var[c] = vc;
+      if (d.rmu) {
+        d.rmu[c] = ms + h.meanH;
+        d.rvar[c] = vc;
+      }
     }
     if (d.vmax || d.vargmax) var_argmax_tile(d, vc, c, c < M, blockIdx.x);
   }
@@ -1951,6 +1955,10 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
   if (valid) {
     d.mu[c] = msum + h.meanH;
     d.var[c] = vc;
+    if (d.rmu) {
+      d.rmu[c] = msum + h.meanH;
+      d.rvar[c] = vc;
+    }
   }
   if ((d.vmax || d.vargmax || d.status_host) && cg < M && si == 0)
     var_argmax_group(d, valid ? vc : -__builtin_inf(), valid ? c : INT64_MAX, cg / WS_CELLS,
@@ -2250,6 +2258,10 @@ __device__ __forceinline__ void vstream_wg_f32(const GPDesc& d, int64_t wgt, dou
   if (valid) {
     d.mu[c] = msum + h.meanH;
     d.var[c] = vc;
+    if (d.rmu) {
+      d.rmu[c] = msum + h.meanH;
+      d.rvar[c] = vc;
+    }
   }
   if ((d.vmax || d.vargmax || d.status_host) && live)
     var_argmax_group(d, valid ? vc : -__builtin_inf(), valid ? c : INT64_MAX, cg / WF_CELLS,
@@ -2322,25 +2334,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
 //    the construction above needs neither, at the price of the two rules: drain
 //    before the flag, and no early read of a handed-over line.
 // ---------------------------------------------------------------------------
+// Producer role `role` < nprod of a fused append launch (k_inc_stream, k_inc_lat):
+// gather its chunk of L21 and the partials, drain, count the arrival (sync[0]);
+// the last one signals sync[1] (L21 complete, when gathered), runs inc_finish
+// (which signals sync[1] itself when it solves L21, then sync[2]) and resets
+// sync[0] for the next launch.
+// `cell` [KINC] and `last` are LDS words of the caller's.
 template <class VT>
-__device__ __forceinline__ void inc_stream_wg(const GPDesc& d) {
-  const int k = (int)(d.N - d.n0);
-  if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
-  if (d.gate && *d.gate == 0) return;
-  static_assert(VS_LDS <= FIN_LDS, "one LDS image serves every role");
-  __shared__ double sm[FIN_LDS];
-  WTRACE(0);
-  const int64_t np = d.nprod, role = blockIdx.y;
-  if (role >= np) {
-    const int64_t wgt = role - np;
-    if (d.tiles && wgt * wg_cells<VT>(d) < d.M) {
-      if constexpr (sizeof(VT) == 8) vstream_wg<true>(d, wgt, sm);
-      else vstream_wg_f32<true>(d, wgt, sm);
-    }
-    return;
-  }
-  __shared__ int cell[KINC];
-  __shared__ unsigned last;
+__device__ __forceinline__ void inc_producer_role(const GPDesc& d, int64_t role, double* sm, int* cell,
+                                                  unsigned& last) {
+  const int64_t np = d.nprod;
   if (role == 0) FSTAMP(30);
   __builtin_amdgcn_s_setprio(3);   // producers and the finish before the cell streams
   const bool gathered = inc_produce<VT>(d, role, FCH, cell, reinterpret_cast<double(*)[ISZ]>(sm));
@@ -2364,6 +2367,28 @@ __device__ __forceinline__ void inc_stream_wg(const GPDesc& d) {
 }
 
 template <class VT>
+__device__ __forceinline__ void inc_stream_wg(const GPDesc& d) {
+  const int k = (int)(d.N - d.n0);
+  if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
+  if (d.gate && *d.gate == 0) return;
+  static_assert(VS_LDS <= FIN_LDS, "one LDS image serves every role");
+  __shared__ double sm[FIN_LDS];
+  WTRACE(0);
+  const int64_t np = d.nprod, role = blockIdx.y;
+  if (role >= np) {
+    const int64_t wgt = role - np;
+    if (d.tiles && wgt * wg_cells<VT>(d) < d.M) {
+      if constexpr (sizeof(VT) == 8) vstream_wg<true>(d, wgt, sm);
+      else vstream_wg_f32<true>(d, wgt, sm);
+    }
+    return;
+  }
+  __shared__ int cell[KINC];
+  __shared__ unsigned last;
+  inc_producer_role<VT>(d, role, sm, cell, last);
+}
+
+template <class VT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream(
     const GPDesc* __restrict__ descs) {
   inc_stream_wg<VT>(descs[blockIdx.x]);
@@ -2375,6 +2400,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
     const GPDesc d) {
   inc_stream_wg<VT>(d);
 }
+
+#include "mfgp_lattice.inl"
 
 // MFGP_F32 full predict: k_predict computed V in fp64 into the scratch d.V (the
 // left-looking solve re-reads its own earlier rows, so it runs in fp64); rows
@@ -2493,6 +2520,19 @@ hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStre
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s) {
   if (vf32) hipLaunchKernelGGL(k_vstream<float>, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
   else hipLaunchKernelGGL(k_vstream<double>, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s) {
+  const dim3 g(count, (unsigned)max_blocks);
+  if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat<8, float>), g, dim3(NT), 0, s, d);
+  else if (ka == 8) hipLaunchKernelGGL((k_inc_lat<8, double>), g, dim3(NT), 0, s, d);
+  else if (vf32) hipLaunchKernelGGL((k_inc_lat<16, float>), g, dim3(NT), 0, s, d);
+  else hipLaunchKernelGGL((k_inc_lat<16, double>), g, dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s) {
+  if (max_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_lat_tables, dim3((unsigned)((max_rows + 3) / 4), count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
 hipError_t launch_vnarrow(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s) {

@@ -122,6 +122,52 @@ __global__ __launch_bounds__(NT) void k_trinv(const GPDesc* __restrict__ descs, 
   }
 }
 
+// The same for a batch (grid (block columns, GPs)): F = L^-1 of the n0 leading
+// factor rows into each GP's resident F (the lattice step's explicit inverse;
+// k_inc_lat then appends its rows).
+__global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t ld = d.ld, nbr = nblocks_rows(d.n0);
+  const int64_t J = blockIdx.x;
+  if (J >= nbr || !d.lat_fbuild) return;
+  __shared__ double As[TILE], Bs[TILE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  double* Xi = d.F;
+  for (int64_t I = J; I < nbr; ++I) {
+    Acc acc;
+    acc_zero(acc);
+    for (int64_t K = J; K < I; ++K) {
+      load_tile_cm(As, d.A, ld, I * NB, K * NB, tid);          // As[k][i] = L_IK[i][k]
+      load_tile_rm(Bs, Xi, ld, K * NB, J * NB, ld, tid);       // Bs[k][j] = X_KJ[k][j]
+      __syncthreads();
+      tile_mma<true>(As, Bs, acc, wm, wn, lane);               // acc -= L_IK X_KJ
+      __syncthreads();
+    }
+    load_tile_cm(As, d.Linv + I * TILE, NB, 0, 0, tid);        // As[k][i] = Linv_II[i][k]
+    if (I == J) {
+      for (int e = tid; e < TILE; e += NT) {
+        const int i = e & 63, k = e >> 6;
+        Bs[swz(k, i)] = (i == k) ? 1.0 : 0.0;
+      }
+    } else {
+      const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) Bs[swz(acc_row(wm, mt, q, v), acc_col(wn, nt, r))] = acc.c[mt][nt][v];
+    }
+    __syncthreads();
+    Acc o;
+    acc_zero(o);
+    tile_mma<false>(As, Bs, o, wm, wn, lane);
+    store_acc_cm(o, Xi, ld, I * NB, J * NB, 1.0, wm, wn, lane);
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
 // K^-1 = X^T X over the real rows (k < N): tile (I, J), I >= J, sums K >= I.
 __global__ __launch_bounds__(NT) void k_kinv(const GPDesc* __restrict__ descs, const double* __restrict__ Xi,
                                              double* __restrict__ Kv) {
@@ -221,6 +267,11 @@ __global__ __launch_bounds__(NT) void k_nlml_grad(const GPDesc* __restrict__ des
   if (tid < NHYP) part[(int64_t)blockIdx.x * NHYP + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
+hipError_t launch_trinv_f(const GPDesc* d, int count, int64_t max_nbr, hipStream_t s) {
+  if (max_nbr <= 0 || count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_trinv_f, dim3((unsigned)max_nbr, count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
 hipError_t launch_nlml_value(const GPDesc* d, int count, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_nlml_value, dim3(count), dim3(NT), 0, s, d, out);
   return hipGetLastError();

@@ -4,8 +4,9 @@ predict steps, from N_L = 1024 lofi and no hifi data to N = 2224 -- every step
 a bordered append on the resident V, across two 1.5x capacity reallocations
 (the V rows move to the new row stride) -- checked against the oracle at every
 cell at steps 1, 50, 100 and 150 (rounding drift over a real horizon). Also a
-batch of 4 GPs growing the same way through the batched C ABI, and an
-MFGP_F32 model over the same horizon at the fp32 tolerance."""
+batch of 4 GPs growing the same way through the batched C ABI (every step the
+lattice-separable k_inc_lat, so its drift is checked too), and an MFGP_F32 model
+over the same horizon at the fp32 tolerance."""
 import numpy as np
 import pytest
 
@@ -83,3 +84,5 @@ def test_long_horizon_batched_growth(dtype):
     for m in models:
         st = m.stats()
         assert st["full_factor"] == 1 and st["inc_factor"] == STEPS and st["full_predict"] == 1, st
+        # a lattice grid, kss / noise <= 1e4 and 4 x 32 GEMM tiles: every step is the separable one
+        assert st["lattice"] == STEPS, st

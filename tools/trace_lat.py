@@ -1,0 +1,73 @@
+"""Diagnostic: per-workgroup timeline of k_inc_lat (a -DMFGP_STAMPS build, argv[1]).
+Slots: producers 0 start / 1 arrival / 4 end; w blocks 0 start / 1 past the L21 wait /
+2 published; GEMM 0 start / 1 past the first w waits / 2 K loop done / 3 past the
+L22 wait (reducers) / 4 end. Launches back to back; the trace is the last launch's."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["MFGP_LIB"] = sys.argv[1]
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+from mfgp_coverage_amd import _lib, synthetic
+
+B = int(os.environ.get("TRACE_B", "8"))
+G, NL, NH, k = 128, 1024, 1024, 8
+T = 12
+NH0 = NH - k
+M = G * G
+hyp = synthetic.HYP["australia8_mf"]
+wls = [synthetic.Workload(G, NL, NH0, k, T, seed=s) for s in range(B)]
+dev = torch.device("cuda", 0)
+NWG = B * 2048
+st = torch.zeros(64 + 8 * NWG + 64, dtype=torch.int64, device=dev)
+L = _lib.lib()
+L.mfgp_debug_set_stamps.argtypes = [ctypes.c_void_p]
+assert L.mfgp_debug_set_stamps(ctypes.c_void_p(st.data_ptr())) == 0
+Xnew = torch.from_numpy(np.ascontiguousarray(np.stack([w.Xnew for w in wls], 1).reshape(T, B * k, 2))).to(dev)
+ynew = torch.from_numpy(np.ascontiguousarray(np.stack([w.ynew for w in wls], 1).reshape(T, B * k))).to(dev)
+ctx = _lib.context()
+models = []
+for wl in wls:
+    m = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
+    m.set_grid(wl.xs)
+    m.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
+    models.append(m)
+mu = torch.empty(B * M, dtype=torch.float64, device=dev)
+var = torch.empty(B * M, dtype=torch.float64, device=dev)
+_lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
+for s in range(T):
+    for m in models:
+        m.truncate(NH0)
+    if s == T - 1:
+        torch.cuda.synchronize()
+        st.zero_()
+    _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
+                              asynchronous=True)
+ctx.synchronize()
+assert models[0].stats()["lattice"] == T, models[0].stats()
+raw = st.cpu().numpy()[64:64 + 8 * NWG].reshape(NWG, 8)
+tr = raw[:, :6].astype(np.float64)
+used = tr[:, 0] > 0
+t0 = tr[used, 0].min()
+tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)   # us (100 MHz realtime counter)
+nprod, nwb = 16, 32
+role = np.arange(NWG) // B
+q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
+print(f"B={B}: percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
+for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w block", (role >= nprod) & (role < nprod + nwb), (0, 1, 2)),
+                         ("gemm", (role >= nprod + nwb) & used, (0, 1, 2, 3, 4))):
+    for sl in slots:
+        print(f"  {name:9s} slot {sl}: {q(tr[sel, sl])}")
+gm = (role >= nprod + nwb) & used
+w = tr[(role >= nprod) & (role < nprod + nwb)]
+jb = nwb - 1 - (role[(role >= nprod) & (role < nprod + nwb)] - nprod)
+for b in (31, 24, 16, 8, 0):
+    print(f"  w block jb={b:2d} published at {np.nanmedian(w[jb == b, 2]):7.1f} us")
+print(f"  gemm K-loop durations (slot2 - slot1): {q(tr[gm, 2] - tr[gm, 1])}")
+S = int(os.environ.get("MFGP_LAT_KSPLIT", "0")) or None
+if S:
+    g = role - nprod - nwb
+    tiles = 32
+    for sp in range(S):
+        sel = gm & (g // tiles == sp)
+        print(f"  split {sp}: start {q(tr[sel, 1])} | mid {q(tr[sel, 5])} | loop end {q(tr[sel, 2])}")
