@@ -178,6 +178,8 @@ struct mfgp_model {
   double* wv = nullptr;       // w [wv_ld][KINC]
   int64_t wv_ld = 0;
   unsigned* wflag = nullptr;  // [wv_ld / 64 + 2]
+  unsigned* wcnt = nullptr;   // [wv_ld / 64 + 2]
+  double* wpart = nullptr;    // [lat_wunits(wv_ld)][1024]
   double* gpart = nullptr;    // split-K partials
   size_t gpart_n = 0;
   unsigned* gcnt = nullptr;   // per GEMM tile
@@ -501,6 +503,9 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.lat_tiles = 0;
   d.nwb = 0;
   d.lat_fbuild = 0;
+  d.nwu = 0;
+  d.wpart = nullptr;
+  d.wcnt = nullptr;
   d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
   d.hp = d.hf;
 }
@@ -554,7 +559,7 @@ bool lat_cond_ok(const mfgp_model* m) {
 }
 int64_t lat_tabw(const mfgp_model* m) { return round_up(std::max<int64_t>(m->lat.nx, m->lat.ny), 64); }
 int64_t lat_tiles(const mfgp_model* m, int ka) {
-  return ((m->lat.nx + 64 / ka - 1) / (64 / ka)) * ((m->lat.ny + 63) / 64);
+  return ((m->lat.nx + 128 / ka - 1) / (128 / ka)) * ((m->lat.ny + 63) / 64);
 }
 // Can the bordered append of rows [n0, N) and its predict take k_inc_lat?
 bool lat_eligible(const mfgp_model* m, int64_t n0) {
@@ -592,12 +597,19 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit) {
     HIP_TRY(hipStreamSynchronize(s));
     if (m->wv) HIP_TRY(hipFree(m->wv));
     if (m->wflag) HIP_TRY(hipFree(m->wflag));
+    if (m->wcnt) HIP_TRY(hipFree(m->wcnt));
+    if (m->wpart) HIP_TRY(hipFree(m->wpart));
     m->wv = nullptr;
     m->wflag = nullptr;
+    m->wcnt = nullptr;
+    m->wpart = nullptr;
     HIP_TRY(hipMalloc(&m->wv, sizeof(double) * ld * KINC));
     HIP_TRY(hipMemsetAsync(m->wv, 0, sizeof(double) * ld * KINC, s));
     HIP_TRY(hipMalloc(&m->wflag, sizeof(unsigned) * (ld / 64 + 2)));
     HIP_TRY(hipMemsetAsync(m->wflag, 0, sizeof(unsigned) * (ld / 64 + 2), s));   // below every epoch
+    HIP_TRY(hipMalloc(&m->wcnt, sizeof(unsigned) * (ld / 64 + 2)));
+    HIP_TRY(hipMemsetAsync(m->wcnt, 0, sizeof(unsigned) * (ld / 64 + 2), s));
+    HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 1024 * lat_wunits(ld)));
     m->wv_ld = ld;
   }
   if (m->gcnt_n < tiles) {
@@ -608,7 +620,7 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit) {
     HIP_TRY(hipMemsetAsync(m->gcnt, 0, sizeof(unsigned) * tiles, s));
     m->gcnt_n = tiles;
   }
-  const size_t need = ksplit > 1 ? (size_t)tiles * ksplit * 4096 : 0;
+  const size_t need = ksplit > 1 ? (size_t)tiles * ksplit * 8192 : 0;   // LAT_PART doubles per split tile
   if (need > m->gpart_n) {
     HIP_TRY(hipStreamSynchronize(s));
     if (m->gpart) HIP_TRY(hipFree(m->gpart));
@@ -623,6 +635,8 @@ void free_lat(mfgp_model* m) {
   if (m->tab) (void)hipFree(m->tab);
   if (m->wv) (void)hipFree(m->wv);
   if (m->wflag) (void)hipFree(m->wflag);
+  if (m->wcnt) (void)hipFree(m->wcnt);
+  if (m->wpart) (void)hipFree(m->wpart);
   if (m->gpart) (void)hipFree(m->gpart);
   if (m->gcnt) (void)hipFree(m->gcnt);
   if (m->res) (void)hipFree(m->res);
@@ -819,7 +833,7 @@ int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
 int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_blocks = 0, max_nbr = 0, max_rows = 0;
   for (int i = 0; i < count; ++i) {
-    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwb + (int64_t)hd[i].lat_tiles * hd[i].ksplit);
+    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + (int64_t)hd[i].lat_tiles * hd[i].ksplit);
     if (hd[i].lat_fbuild) max_nbr = std::max(max_nbr, nblocks_rows(hd[i].n0));
     max_rows = std::max(max_rows, hd[i].n0 - hd[i].tab_lo);
   }
@@ -1636,7 +1650,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     for (int i = 0; lat && i < ninc; ++i) lat = lat_eligible(order[i], hd[i].n0);
     res_depth.assign(ninc, 0);
     int ka = 8;
-    int64_t tiles_sum = 0, ns_min = INT64_MAX;
+    int64_t tiles_sum = 0, nwb_min = INT64_MAX;
     if (lat) {
       for (int i = 0; i < ninc; ++i) {
         if (order[i]->NL + order[i]->NH - hd[i].n0 > 8) ka = 16;
@@ -1645,18 +1659,21 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         const mfgp_model* m = order[i];
         tiles_sum += lat_tiles(m, ka);
         const int64_t nwb = (hd[i].n0 + 63) / 64;
-        const int64_t jh = m->kind == MFGP_SF ? nwb : std::min(m->NL / 64, nwb);
-        ns_min = std::min(ns_min, (nwb - jh) * 8 + jh * 4);
+        nwb_min = std::min(nwb_min, nwb);
       }
-      // too few GEMM tiles to fill the chip (one GP at the headline size: 32 tiles):
-      // the w pass and the split-K reductions cost more than the V stream they save
-      if (tiles_sum * 2 < c->ncu && !c->lat_force) lat = false;
+      // too few GEMM tiles to fill the chip (headline size: 16 tiles per GP): the w
+      // pass and the split-K reductions cost more than the V stream they save.
+      // Measured at 128x128, N = 2048 (tools/bench_lattice.py, us per launch,
+      // V stream / lattice): B = 1 60 / 107, B = 2 108 / 115, B = 4 184 / 141,
+      // B = 6 269 / 192, B = 8 345 / 220
+      if (tiles_sum * 4 < c->ncu && !c->lat_force) lat = false;
     }
     if (lat) {
       // split-K so that the GEMM tiles fill the chip about twice, >= 4 stages each
       int S = (int)std::min<int64_t>(8, std::max<int64_t>(1, (2 * c->ncu + tiles_sum - 1) / tiles_sum));
-      S = (int)std::max<int64_t>(1, std::min<int64_t>(S, ns_min / 4));
-      if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, ns_min / 4));
+      // (split s takes every S-th 64-row block of terms: at least one block each)
+      S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nwb_min));
+      if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, nwb_min));
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
@@ -1680,6 +1697,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.ksplit = S;
         fd.lat_tiles = (int)tiles;
         fd.nwb = (int)((fd.n0 + 63) / 64);
+        fd.nwu = (int)lat_wunits(fd.n0);
+        fd.wpart = m->wpart;
+        fd.wcnt = m->wcnt;
         fd.lat_fbuild = (m->F_gen == m->gen && m->F_n >= fd.n0) ? 0 : 1;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }

@@ -99,7 +99,7 @@ struct GPDesc {
   int rsplit;          // one-pass predict: row splits per cell group (1, 2, 4; 128 / rsplit cells per workgroup)
   int vf32;            // 1 = the resident V is Vf (fp32; the one-pass predict streams 256 cells per workgroup)
   // lattice-separable step (k_inc_lat, mfgp_lattice.inl)
-  double* F;           // explicit L^-1, [ld][ld] column-major: lower triangle, zeros above
+  double* F;           // explicit L^-1, [ld][ld] ROW-major (F[i][j] at i * ld + j): lower triangle, zeros above
   double* tab;         // separable tables [4][ld][tabw]: c_L(j) ex_L, ey_L, c_H(j) ex_H, ey_H per training row j
   double* wv;          // w = L11^-T L21^T, [ld][KINC] (row j: w[j][0..KINC))
   unsigned* wflag;     // per 64-row block of w: the epoch of the launch that stored it
@@ -116,10 +116,24 @@ struct GPDesc {
   int lat_tiles;       // GEMM tiles per GP: ceil(nx / (64 / ka)) * ceil(ny / 64)
   int nwb;             // 64-row blocks of w: ceil(n0 / 64)
   int lat_fbuild;      // k_trinv_f: 1 = compute F for the n0 factor rows
+  int nwu;             // w work units: 64-column blocks x LAT_WCH-row chunks (lat_wunits(n0))
+  double* wpart;       // the units' partial w blocks [nwu][16 x 64]
+  unsigned* wcnt;      // per 64-row block of w: arrivals of its units (zero between launches)
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
 
+// lattice step: w is computed in units of 64 columns x LAT_WCH rows of F's lower
+// triangle (column block jb: rows [64 jb, n0) in chunks), top block first
+constexpr int64_t LAT_WCH = 1024;
+inline __host__ __device__ int64_t lat_wunits_block(int64_t n0, int64_t jb) {
+  return (n0 - 64 * jb + LAT_WCH - 1) / LAT_WCH;
+}
+inline __host__ __device__ int64_t lat_wunits(int64_t n0) {
+  int64_t u = 0;
+  for (int64_t jb = 0; jb * 64 < n0; ++jb) u += lat_wunits_block(n0, jb);
+  return u;
+}
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
 inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
 inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1) / PBM; }
@@ -151,7 +165,7 @@ hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int
 // descriptor upload, and with rows_inline no row copies either
 hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s);
 // lattice-separable append + predict (k_inc_lat); max_blocks = max over GPs of
-// nprod + nwb + lat_tiles * ksplit
+// nprod + nwu + lat_tiles * ksplit
 hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
 // separable tables of rows [tab_lo, n0); max_rows = max over GPs of n0 - tab_lo
 hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s);

@@ -15,7 +15,8 @@
 //   T = psi_new - T~,  v_new = L22^-1 T,  var = var_old - |v_new|^2,
 //   mu = mu_old + v_new^T z2                                  (bordered update)
 // with var_old / mu_old the model's resident posterior of the n0 leading rows.
-// w comes from the explicit inverse F = L^-1 (resident, lower triangular):
+// w comes from the explicit inverse F = L^-1 (resident, lower triangular, stored
+// row-major):
 // w = F11^T L21^T, one parallel pass over F's lower triangle (HBM-bound, 8 n0^2/2
 // bytes); F's new rows are -L22^-1 w^T and L22^-1, so F grows with the factor.
 // The new rows of V (v_new) are still stored, so the V-stream path stays valid.
@@ -28,9 +29,10 @@
 //
 // One launch per batch, grid (GPs, roles); per GP the roles are
 //   [0, nprod)                 producers + finish, exactly as k_inc_stream's
-//   [nprod, nprod + nwb)       w blocks (64 rows of w each, top block first):
-//                              wait for the compact rows of their rows, then
-//                              w[j][a] = sum_{i >= j} F[i][j] L21c[i][a] on MFMA,
+//   [nprod, nprod + nwu)       w units (64 rows of w x LAT_WCH rows of F, top
+//                              block first): wait for the compact rows of their
+//                              rows, then w[j][a] = sum_{i >= j} F[i][j] L21c[i][a]
+//                              on MFMA; the block's last unit adds the chunks,
 //                              write-through + drain + wflag[jb] = epoch; then a
 //                              share of the new rows' separable tables
 //   [.., + tiles * ksplit)     GEMM tiles: 64 (a, ix) rows x 64 iy columns, the
@@ -49,31 +51,44 @@ constexpr int LKS = 16;                   // term rows (j) per pipeline stage
 constexpr int LNST = MFGP_LAT_NST;        // stages in the LDS ring
 constexpr int LBS = LKS * 64;             // Bs: Ey rows [LKS][64 iy], swizzled (swz)
 constexpr int LWS = LKS * KINC;           // Ws: w rows [LKS][16 a]
-constexpr int LXS = LKS * 8;              // Xs: Ex rows [LKS][8 ix of the tile]
+constexpr int LXS = LKS * 16;             // Xs: Ex rows [LKS][16 ix of the tile]
 constexpr int LSTG = LBS + LWS + LXS;      // doubles per stage
-constexpr int LAT_TS = 65;                // row stride of the epilogue's T~ image [64][65]
-constexpr int LAT_LDS = LNST * LSTG + LNST * 32 + 272 + 256 + 32;   // ring + flag words | epilogue: 37.6 KB
+constexpr int LAT_EPI = 272 + 256 + 32 + 2 * 16 * (8 + 64);   // epilogue: L22, z2 | L22^-1 | new rows | their factors (later: a w block)
+static_assert(2 * 16 * (8 + 64) >= 64 * KINC, "a w block fits the factors' place");
+constexpr int LAT_RING = LNST * LSTG + LNST * 32;       // the ring | its flag words
+constexpr int LAT_LDS = LAT_RING > LAT_EPI ? LAT_RING : LAT_EPI;   // 37.6 KB: four workgroups per CU
 static_assert(LAT_LDS >= FIN_LDS, "the ring also holds the finish's LDS image");
-static_assert(64 * LAT_TS + 272 + 256 + 32 <= LAT_LDS, "the epilogue image fits");
-static_assert(LNST > 3 || LAT_LDS + 16 <= 5120, "four workgroups per CU (40 KB of LDS each)");
-constexpr int LAT_PART = 4 * 16 * 64;     // doubles of one split-K partial tile (4 waves x 16 acc x 64 lanes)
 
-// Stage s of the descending term order: blocks jb >= jh have L and H parts (8
-// stages of 16 rows), blocks below jh the L part only (4 stages).
-__device__ __forceinline__ void lat_stage(int64_t s, int64_t nwb, int64_t jh, int64_t& jb, int& part, int64_t& j0) {
-  const int64_t nh = (nwb - jh) * 8;
-  if (s < nh) {
-    jb = nwb - 1 - s / 8;
-    part = (int)((s % 8) / 4);
-    j0 = 64 * jb + 16 * (s % 4);
+static_assert(LNST > 3 || LAT_LDS + 16 <= 5120, "four workgroups per CU (40 KB of LDS each)");
+constexpr int LAT_PART = 4 * 32 * 64;     // doubles of one split-K partial tile (4 waves x 32 acc x 64 lanes)
+
+// The term blocks of split sp of S: every S-th block from the top (jb = nwb - 1
+// - sp - m S, m = 0, 1, ..), so every split starts at the blocks whose w is ready
+// first and all of them move down together as w becomes ready. Blocks jb >= jh
+// have L and H parts (8 stages of 16 rows), blocks below jh the L part only (4).
+__device__ __forceinline__ int64_t lat_nblk(int64_t from, int64_t S) { return from >= 0 ? from / S + 1 : 0; }
+__device__ __forceinline__ void lat_stage(int64_t t, int64_t nwb, int64_t jh, int64_t sp, int64_t S, int64_t& jb,
+                                          int& part, int64_t& j0) {
+  const int64_t top = nwb - 1 - sp;
+  const int64_t nh = top >= jh ? (top - jh) / S + 1 : 0;   // this split's blocks with H parts
+  int64_t m;
+  if (t < 8 * nh) {
+    m = t / 8;
+    part = (int)((t % 8) / 4);
   } else {
-    s -= nh;
-    jb = jh - 1 - s / 4;
+    t -= 8 * nh;
+    m = nh + t / 4;
     part = 0;
-    j0 = 64 * jb + 16 * (s % 4);
   }
+  jb = top - m * S;
+  j0 = 64 * jb + 16 * (t % 4);
 }
-__device__ __forceinline__ int64_t lat_nstages(int64_t nwb, int64_t jh) { return (nwb - jh) * 8 + jh * 4; }
+__device__ __forceinline__ int64_t lat_nstages(int64_t nwb, int64_t jh, int64_t sp, int64_t S) {
+  const int64_t top = nwb - 1 - sp;
+  const int64_t nb = lat_nblk(top, S);
+  const int64_t nh = top >= jh ? (top - jh) / S + 1 : 0;
+  return 8 * nh + 4 * (nb - nh);
+}
 __device__ __forceinline__ int64_t lat_jh(const GPDesc& d) {
   const int64_t nwb = d.nwb;
   if (d.hp.kind == 0) return nwb;
@@ -142,62 +157,44 @@ __device__ __forceinline__ double l21c_at(const double* l21c, int64_t i, int a) 
   else return (double)gp(reinterpret_cast<const float*>(l21c))[i * KINC + a];
 }
 
-// One 64-row block jb of w = F11^T L21^T (+ row k: F^T z1, unused): wave w owns
-// columns j = 64 jb + 16 w + r, lanes sum over rows i in [64 jb, n0) -- F's lower
-// triangle below the block -- with two MFMAs per 8 rows (B = F[i][j] as one
-// 16-byte load of rows 2q, 2q + 1; A = the compact rows L21c[i][a]). Four
-// accumulators keep four MFMA chains in flight.
+// w unit u (in role order: column blocks from the top, chunks of LAT_WCH rows
+// within a block): its block jb, chunk c, the block's first unit u0 and units nc.
+__device__ __forceinline__ void lat_wunit(int64_t n0, int64_t nwb, int64_t u, int64_t& jb, int64_t& c,
+                                          int64_t& u0, int64_t& nc) {
+  u0 = 0;
+  for (jb = nwb - 1; jb > 0; --jb) {
+    nc = lat_wunits_block(n0, jb);
+    if (u < u0 + nc) break;
+    u0 += nc;
+  }
+  nc = lat_wunits_block(n0, jb);
+  c = u - u0;
+}
+
+// One w unit: columns j = 64 jb + [0, 64) of w = F11^T L21^T (+ row k: F^T z1,
+// unused), rows i of chunk c of [64 jb, n0) -- F's lower triangle below the
+// block. Wave w owns columns 64 jb + 16 w + r; one MFMA per 4 rows (B = F[i][j],
+// F row-major: a wave's load is four full 128-byte lines; A = the compact rows
+// L21c[i][a]), four accumulators in flight. A block of one chunk stores w itself; otherwise each
+// chunk stores its partial and the last of the block to arrive adds them in
+// chunk order. Either way the block's flag is raised once w is stored.
 template <class VT>
-__device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t jb) {
-  const int64_t n0 = d.n0, ld = d.ld, i_lo = 64 * jb;
+__device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
+  const int64_t n0 = d.n0, ld = d.ld;
+  int64_t jb, c, u0, nc;
+  lat_wunit(n0, d.nwb, u, jb, c, u0, nc);
+  const int64_t i_lo = 64 * jb + LAT_WCH * c;
+  const int64_t i_hi = i_lo + LAT_WCH < n0 ? i_lo + LAT_WCH : n0;
   const double* const l21c = d.l21c;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
   WTRACE(0);
-  wait_l21_from(d, i_lo);
-  WTRACE(1);
-  const int64_t j = i_lo + 16 * w + r;
-  const GLOBAL dv2* Fc = reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + j * ld);
-  d4 acc[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) acc[u] = d4{0.0, 0.0, 0.0, 0.0};
-  constexpr int IU = 8;
-  for (int64_t i0 = i_lo; i0 < n0; i0 += 8 * IU) {
-    dv2 f[IU];
-    double a0[IU], a1[IU];
-#pragma unroll
-    for (int u = 0; u < IU; ++u) {
-      const int64_t i = i0 + 8 * u + 2 * q;
-      const int64_t ii = i < n0 ? i : i_lo;
-      // F is read once per step and would evict the GEMM tiles' tables from L2
-      f[u] = __builtin_nontemporal_load(Fc + (ii >> 1));
-      a0[u] = l21c_at<VT>(l21c, ii, r);
-      a1[u] = l21c_at<VT>(l21c, ii + 1 < n0 ? ii + 1 : ii, r);
-    }
-#pragma unroll
-    for (int u = 0; u < IU; ++u) {
-      const int64_t i = i0 + 8 * u + 2 * q;
-      const double x0 = i < n0 ? a0[u] : 0.0;
-      const double x1 = i + 1 < n0 ? a1[u] : 0.0;
-      acc[(u & 1) * 2] = mfma(x0, f[u].x, acc[(u & 1) * 2]);
-      acc[(u & 1) * 2 + 1] = mfma(x1, f[u].y, acc[(u & 1) * 2 + 1]);
-    }
-  }
-  // lane (r, g) register v: row a = g + 4v of column j
-  double* const wv = d.wv;
-#pragma unroll
-  for (int v = 0; v < 4; ++v)
-    stx<true>(&wv[j * KINC + q + 4 * v], (acc[0][v] + acc[1][v]) + (acc[2][v] + acc[3][v]));
-  drain_stores();
-  __syncthreads();
-  if (tid == 0) publish(d.wflag + jb, d.epoch);
-  WTRACE(2);
   // a share of the new rows' separable tables (read from the next launch on)
   const int k = (int)(d.N - n0);
   const int64_t tabw = d.tabw, tstride = (d.ld) * tabw;
   const int64_t tot = 4 * (int64_t)k * tabw;
-  const int64_t per = (tot + d.nwb - 1) / d.nwb, e0 = (d.nwb - 1 - jb) * per;
+  const int64_t per = (tot + d.nwu - 1) / d.nwu, e0 = u * per;
   const int64_t e1 = e0 + per < tot ? e0 + per : tot;
   for (int64_t e = e0 + tid; e < e1; e += NT) {
     const int t = (int)(e / (k * tabw));
@@ -207,6 +204,69 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t jb) {
     const double* p = row_pt(d, n0 + a);
     d.tab[t * tstride + (n0 + a) * tabw + col] = lat_tab_value(d, t, n0 + a, col, p[0], p[1]);
   }
+  wait_l21_from(d, i_lo);
+  WTRACE(1);
+  const int64_t j = 64 * jb + 16 * w + r;
+  const GLOBAL double* Fr = gp(d.F) + j;   // F[i][j] at Fr[i * ld]
+  d4 acc[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
+  constexpr int IU = 16;
+  for (int64_t i0 = i_lo; i0 < i_hi; i0 += 4 * IU) {
+    double f[IU], a[IU];
+#pragma unroll
+    for (int x = 0; x < IU; ++x) {
+      const int64_t i = i0 + 4 * x + q;
+      const int64_t ii = i < i_hi ? i : i_lo;
+      // F is read once per step and would evict the GEMM tiles' tables from L2
+#ifdef MFGP_DIAG_FPLAIN
+      f[x] = Fr[ii * ld];
+#else
+      f[x] = __builtin_nontemporal_load(Fr + ii * ld);
+#endif
+      a[x] = l21c_at<VT>(l21c, ii, r);
+    }
+#pragma unroll
+    for (int x = 0; x < IU; ++x) {
+      const int64_t i = i0 + 4 * x + q;
+      acc[x & 3] = mfma(i < i_hi ? a[x] : 0.0, f[x], acc[x & 3]);
+    }
+  }
+  WTRACE(3);
+  // lane (r, g) register v: row a = g + 4v of column j
+  double* const wv = d.wv;
+  double sum[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) sum[v] = (acc[0][v] + acc[1][v]) + (acc[2][v] + acc[3][v]);
+  if (nc == 1) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) stx<true>(&wv[j * KINC + q + 4 * v], sum[v]);
+  } else {
+    // partial [a][64 columns] of this chunk; the block's last unit adds them in chunk order
+    double* part = d.wpart + (u0 + c) * 1024 + (16 * w + r);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) stx<true>(part + (q + 4 * v) * 64, sum[v]);
+    drain_stores();
+    __syncthreads();
+    unsigned& wlast = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 10);
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(d.wcnt + jb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      wlast = old == (unsigned)(nc - 1) ? 1u : 0u;
+      if (wlast) __hip_atomic_store(d.wcnt + jb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!wlast) return;
+    for (int e = tid; e < 1024; e += NT) {
+      const int a = e >> 6, jl = e & 63;
+      double t = 0.0;
+      for (int64_t cc = 0; cc < nc; ++cc) t += ldx<true>(d.wpart + (u0 + cc) * 1024 + e);
+      stx<true>(&wv[(64 * jb + jl) * KINC + a], t);
+    }
+  }
+  drain_stores();
+  __syncthreads();
+  if (tid == 0) publish(d.wflag + jb, d.epoch);
+  WTRACE(2);
 }
 
 // Geometry of one GEMM tile, and its buffer-descriptor LDS-DMA plan (as
@@ -215,31 +275,35 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t jb) {
 struct LatGeo {
   __amdgpu_buffer_rsrc_t rtab, rw;   // the four tables; w
   int64_t tstride, tabw;
-  int64_t nwb, jh;
+  int64_t nwb, jh, sp, S;
   int64_t ix0, iy0;
   unsigned vB, vW, vX;               // lane byte offsets: Bs, Ws, Xs
 };
 
 // Issue the DMAs of stage st into `slot` (waves 1..3; wave 0 only loads the w
 // flags, so its vmcnt never waits for a flag's memory round trip behind a table
-// load, nor theirs for a flag): Bs = 16 Ey rows x 64 iy (8 two-row DMAs:
-// waves 1, 2 three each, wave 3 two, swizzled as swz), Ws = 16 w rows (waves 2,
-// 3: 8 rows each), Xs = 16 Ex rows x 8 ix (wave 1).
+// load, nor theirs for a flag): Bs = 16 Ey rows x 64 iy (8 two-row DMAs, waves
+// 1 and 2, swizzled as swz), Ws = 16 w rows and Xs = 16 Ex rows x 16 ix (wave 3,
+// two 8-row DMAs each).
 __device__ __forceinline__ void lat_issue(const LatGeo& G, int64_t st, double* slot, int w) {
   int64_t jb, j0;
   int part;
-  lat_stage(st, G.nwb, G.jh, jb, part, j0);
+  lat_stage(st, G.nwb, G.jh, G.sp, G.S, jb, part, j0);
   const int64_t tx = (2 * part) * G.tstride, ty = tx + G.tstride;
-  const int p0 = w == 1 ? 0 : (w == 2 ? 3 : 6), np = w == 3 ? 2 : 3;
+  if (w < 3) {
+    const int p0 = 4 * (w - 1);
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    if (u < np) {
+    for (int u = 0; u < 4; ++u) {
       const int p = p0 + u;
       dma_buf(G.rtab, slot + 2 * p * 64, G.vB, (unsigned)(8 * (ty + (j0 + 2 * p) * G.tabw + G.iy0)));
     }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      dma_buf(G.rw, slot + LBS + 8 * h * KINC, G.vW, (unsigned)(8 * (j0 + 8 * h) * KINC));
+      dma_buf(G.rtab, slot + LBS + LWS + 8 * h * 16, G.vX, (unsigned)(8 * (tx + (j0 + 8 * h) * G.tabw + G.ix0)));
+    }
   }
-  if (w >= 2) dma_buf(G.rw, slot + LBS + 8 * (w - 2) * KINC, G.vW, (unsigned)(8 * (j0 + 8 * (w - 2)) * KINC));
-  else dma_buf(G.rtab, slot + LBS + LWS, G.vX, (unsigned)(8 * (tx + j0 * G.tabw + G.ix0)));
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n in [0, 4], then the raw barrier (no
@@ -255,52 +319,55 @@ __device__ __forceinline__ void vm_wait_bar(int n) {
 }
 
 // acc += A B over one stage: A[(a, ix)][j] = w[j][a] * Ex[j][ix] (formed from the
-// Ws / Xs rows), B[j][iy] = Ey[j][iy]. Wave (wm, wn): rows 32 wm.., columns 32 wn..
+// Ws / Xs rows), B[j][iy] = Ey[j][iy]. Wave w: rows 32 w + 16 m + r (m = 0, 1), all
+// 64 columns (blocks n = 0..3): per 4-row k-step 7 LDS reads, 2 products and 8
+// MFMAs. The reads of two k-steps are issued ahead of their MFMAs.
 template <int KA>
-__device__ __forceinline__ void lat_compute(const double* slot, d4 (&acc)[2][2], int wn, int r, int q, int ar,
-                                            int ixl0, int ixl1) {
+__device__ __forceinline__ void lat_compute(const double* slot, d4 (&acc)[2][4], int r, int q, int ar, int ixl0,
+                                            int ixl1) {
   const double* Bs = slot;
   const double* Ws = slot + LBS;
   const double* Xs = slot + LBS + LWS;
-  // every operand of the stage first (20 LDS reads in flight), then the MFMAs:
-  // the reads return in order, so the first k-step's MFMAs start after 5 of them
-  double wa[LKS / 4], x0[LKS / 4], x1[LKS / 4], b0[LKS / 4], b1[LKS / 4];
 #pragma unroll
-  for (int ks = 0; ks < LKS / 4; ++ks) {
-    const int j = 4 * ks + q;
-    wa[ks] = Ws[j * KINC + ar];
-    x0[ks] = Xs[j * 8 + ixl0];
-    x1[ks] = Xs[j * 8 + ixl1];
-    b0[ks] = Bs[swz(j, 32 * wn + r)];
-    b1[ks] = Bs[swz(j, 32 * wn + 16 + r)];
-  }
-  __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
+  for (int hh = 0; hh < 2; ++hh) {
+    double wa[2], x0[2], x1[2], b[2][4];
 #pragma unroll
-  for (int ks = 0; ks < LKS / 4; ++ks) {
-    const double a0 = wa[ks] * x0[ks];
-    const double a1 = wa[ks] * x1[ks];
+    for (int e = 0; e < 2; ++e) {
+      const int j = 4 * (2 * hh + e) + q;
+      wa[e] = Ws[j * KINC + ar];
+      x0[e] = Xs[j * 16 + ixl0];
+      x1[e] = Xs[j * 16 + ixl1];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) b[e][n] = Bs[swz(j, 16 * n + r)];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const double a0 = wa[e] * x0[e];
+      const double a1 = wa[e] * x1[e];
 #ifdef MFGP_DIAG_LATNOMMA   // diagnostic build: the loop without its MFMAs (timing only)
-    acc[0][0][0] += a0 + b0[ks];
-    acc[1][1][0] += a1 + b1[ks];
-    continue;
+      acc[0][0][0] += a0 + b[e][0];
+      acc[1][1][0] += a1 + b[e][1];
+      continue;
 #endif
-    acc[0][0] = mfma(a0, b0[ks], acc[0][0]);
-    acc[0][1] = mfma(a0, b1[ks], acc[0][1]);
-    acc[1][0] = mfma(a1, b0[ks], acc[1][0]);
-    acc[1][1] = mfma(a1, b1[ks], acc[1][1]);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        acc[0][n] = mfma(a0, b[e][n], acc[0][n]);
+        acc[1][n] = mfma(a1, b[e][n], acc[1][n]);
+      }
+    }
   }
 }
 
-// One GEMM tile (split s of ksplit) and, for the last split to arrive, the cell
-// epilogue of its (64 / KA) x 64 cells, F's new rows for its column blocks and
-// the fused var max / argmax partials.
+// One GEMM tile (split s of ksplit): 128 (a, ix) rows x 64 iy columns, i.e.
+// (128 / KA) x 64 cells; and, for the last split to arrive, the cell epilogue,
+// F's new rows for its column blocks and the fused var max / argmax partials.
 template <int KA, class VT>
 __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t s, double* sm) {
-  constexpr int IXPT = 64 / KA;   // lattice columns x per tile
+  constexpr int IXPT = 128 / KA;   // lattice columns x per tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
-  const int wm = w >> 1, wn = w & 1;
   const GridLattice lat = d.lat;
   const int64_t ntiy = (lat.ny + 63) / 64;
   const int64_t tix = tile / ntiy, tiy = tile % ntiy;
@@ -312,37 +379,38 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   G.rw = make_rsrc(d.wv, (int64_t)8 * d.ld * KINC);
   G.vB = (unsigned)(8 * ((lane >> 5) * G.tabw + (((lane & 31) * 2) ^ ((lane >> 5) << 4))));
   G.vW = (unsigned)(8 * ((lane >> 3) * KINC + 2 * (lane & 7)));
-  G.vX = (unsigned)(8 * ((lane >> 2) * G.tabw + 2 * (lane & 3)));
+  G.vX = (unsigned)(8 * ((lane >> 3) * G.tabw + 2 * (lane & 7)));
   G.nwb = d.nwb;
   G.jh = lat_jh(d);
   G.ix0 = tix * IXPT;
   G.iy0 = tiy * 64;
-  const int64_t ns = lat_nstages(G.nwb, G.jh);
-  const int64_t lo = ns * s / S, hi = ns * (s + 1) / S;
+  G.sp = s;
+  G.S = S;
+  const int64_t lo = 0, hi = lat_nstages(G.nwb, G.jh, s, S);
   WTRACE(0);
-  // this lane's A rows: a = row % KA, lattice column ixl = row / KA (rows 32 wm + 16 m + r)
+  // this lane's A rows: a = row % KA, lattice column ixl = row / KA (rows 32 w + 16 m + r)
   const int ar = KA == 8 ? (r & 7) : r;
-  const int ixl0 = KA == 8 ? 4 * wm + (r >> 3) : 2 * wm;
-  const int ixl1 = KA == 8 ? 4 * wm + 2 + (r >> 3) : 2 * wm + 1;
-  d4 acc[2][2];
+  const int ixl0 = KA == 8 ? 4 * w + (r >> 3) : 2 * w;
+  const int ixl1 = KA == 8 ? 4 * w + 2 + (r >> 3) : 2 * w + 1;
+  d4 acc[2][4];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n) acc[m][n] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int n = 0; n < 4; ++n) acc[m][n] = d4{0.0, 0.0, 0.0, 0.0};
   // w's readiness: wave 0 loads the flag word of each stage's block into LDS (an
   // agent-scope 4-byte LDS-DMA) two iterations before that stage's DMAs are
   // issued; waves 2 and 3, which stage the w rows, check it there after the
   // barrier (an LDS read, not a memory round trip) and spin on memory only if it
   // was not yet set. Wave 0 issues nothing else, so the flags' round trips never
   // sit in front of a table load in any wave's vmcnt order.
-  const int cnt = w == 0 ? 1 : (w == 3 ? 3 : 4);   // vector-memory ops per issued stage
+  const int cnt = w == 0 ? 1 : 4;   // vector-memory ops per issued stage
   unsigned* const fl = reinterpret_cast<unsigned*>(sm + LNST * LSTG);   // [LNST][64]
   const __amdgpu_buffer_rsrc_t rfl = make_rsrc(reinterpret_cast<const double*>(d.wflag),
                                                (int64_t)4 * (d.nwb + 1));
   auto blk = [&](int64_t st) {
     int64_t jb, j0;
     int part;
-    lat_stage(st < hi ? st : hi - 1, G.nwb, G.jh, jb, part, j0);
+    lat_stage(st < hi ? st : hi - 1, G.nwb, G.jh, G.sp, G.S, jb, part, j0);
     return jb;
   };
   auto issue = [&](int64_t st, int64_t fst) {   // stage st's DMAs (waves 1..3), flag of stage fst (wave 0)
@@ -357,7 +425,7 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   constexpr int D = LNST - 1;   // stages in flight ahead of the one consumed
   static_assert(D * 4 <= 12, "vm_wait_bar covers the outstanding ops");
   if (lo < hi) {
-    if (w >= 2)
+    if (w == 3)
       for (int64_t st = lo; st < lo + D && st < hi; ++st) spin_wave(d, d.wflag + blk(st), d.epoch);
     WTRACE(1);
     for (int64_t st = lo; st < lo + D && st < hi; ++st) issue(st, st + D);
@@ -367,11 +435,11 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
       const int64_t after = (hi - 1 - t) < (D - 1) ? (hi - 1 - t) : (D - 1);
       vm_wait_bar((int)after * cnt);
       if (t + D < hi) {
-        if (w >= 2 && fl[((t + D - lo) % LNST) * 64] != d.epoch) spin_wave(d, d.wflag + blk(t + D), d.epoch);
+        if (w == 3 && fl[((t + D - lo) % LNST) * 64] != d.epoch) spin_wave(d, d.wflag + blk(t + D), d.epoch);
         issue(t + D, t + 2 * D);
       }
 #ifndef MFGP_DIAG_LATNOCOMP   // diagnostic build: the pipeline without its compute (timing only)
-      lat_compute<KA>(sm + ((t - lo) % LNST) * LSTG, acc, wn, r, q, ar, ixl0, ixl1);
+      lat_compute<KA>(sm + ((t - lo) % LNST) * LSTG, acc, r, q, ar, ixl0, ixl1);
 #endif
       if (t == (lo + hi) / 2) WTRACE(5);
     }
@@ -382,13 +450,13 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   // split-K: partials through memory, the last split reduces them in split order
   if (S > 1) {
     unsigned& lat_last = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 9);
-    double* part = d.gpart + (tile * S + s) * LAT_PART + (int64_t)w * 16 * 64 + lane;
+    double* part = d.gpart + (tile * S + s) * LAT_PART + (int64_t)w * 32 * 64 + lane;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
+      for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) stx<true>(part + ((m * 2 + n) * 4 + v) * 64, acc[m][n][v]);
+        for (int v = 0; v < 4; ++v) stx<true>(part + ((m * 4 + n) * 4 + v) * 64, acc[m][n][v]);
     drain_stores();
     __syncthreads();
     if (tid == 0) {
@@ -398,39 +466,48 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     }
     __syncthreads();
     if (!lat_last) return;
-    d4 tot[2][2];
+    // every split's partial (this one's too) from memory, added in split order
+    // (p0 + p1) + p2 ...: the same bits whichever split arrives last
+    const double* p0 = d.gpart + tile * S * LAT_PART + (int64_t)w * 32 * 64 + lane;
     for (int s2 = 0; s2 < S; ++s2) {
-      const double* p2 = d.gpart + (tile * S + s2) * LAT_PART + (int64_t)w * 16 * 64 + lane;
+      double x[32];
+#pragma unroll
+      for (int e = 0; e < 32; ++e) x[e] = ldx<true>(p0 + s2 * LAT_PART + e * 64);
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+        for (int n = 0; n < 4; ++n)
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            const double x = (s2 == s) ? acc[m][n][v] : ldx<true>(p2 + ((m * 2 + n) * 4 + v) * 64);
-            tot[m][n][v] = s2 == 0 ? x : tot[m][n][v] + x;
+            const double xv = x[(m * 4 + n) * 4 + v];
+            acc[m][n][v] = s2 == 0 ? xv : acc[m][n][v] + xv;
           }
     }
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) acc[m][n] = tot[m][n];
   }
-  // ---- epilogue: T~ to LDS, L22 / z2 (sync[2]), the new rows, L22^-1 ----
+  // ---- epilogue: L22 / z2 (sync[2]), the new rows, L22^-1 (LDS: the ring is dead) ----
   const int64_t n0 = d.n0, ld = d.ld;
   const int k = (int)(d.N - n0);
-  const Hyp& h = d.hp;
-  double* Ts = sm;                               // T~ [64 rows (a, ixl)][LAT_TS], column = iy - iy0
-  double* L22 = sm + 64 * LAT_TS;                // [16][16] | z2 [16]
+  double* L22 = sm;                              // [16][16] | z2 [16]
   double* Li = L22 + KINC * KINC + KINC;         // L22^-1 [16][16]
   double* Xn = Li + KINC * KINC;                 // new rows (x, y)
-  __syncthreads();   // the ring's last reads are done (split-K: nothing of it is live)
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) Ts[(32 * wm + 16 * m + q + 4 * v) * LAT_TS + 32 * wn + 16 * n + r] = acc[m][n][v];
+  // psi(cell, new row a) = c_L exL[a][ix] eyL[a][iy] + c_H exH[a][ix] eyH[a][iy] for
+  // the tile's IXPT x 64 cells: the factors of the k new rows (c_L, c_H folded into
+  // ex), [KA][IXPT + 64] per kind (separable like the GEMM's terms)
+  double* Fn = Xn + 2 * KINC;
+  constexpr int FW = IXPT + 64;
+  // the old posterior of the tile's cells, fetched while the epilogue waits for L22
+  double* Ro = Fn + 2 * KA * FW;   // [2][IXPT * 64]: var_old | mu_old
+  static_assert(560 + 2 * 16 * (8 + 64) + 2 * 8 * 64 <= LAT_LDS && 560 + 2 * 8 * 80 + 2 * 16 * 64 <= LAT_LDS,
+                "the epilogue's LDS fits the ring's");
+  __syncthreads();   // the ring's last reads are done
+  for (int u = tid; u < IXPT * 64; u += NT) {
+    const int64_t ix = G.ix0 + (u >> 6), iy = G.iy0 + (u & 63);
+    if (ix < lat.nx && iy < lat.ny) {
+      const int64_t c = ix * lat.sx + iy * lat.sy;
+      Ro[u] = d.rvar_in[c];
+      Ro[IXPT * 64 + u] = d.rmu_in[c];
+    }
+  }
   wait_flag(d, d.sync + 2, d.epoch);
   WTRACE(3);
   for (int e = tid; e < KINC * KINC + KINC; e += NT) {
@@ -446,6 +523,14 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     Xn[2 * a + 1] = p[1];
   }
   __syncthreads();
+  for (int e = tid; e < 2 * k * FW; e += NT) {
+    const int kind2 = e / (k * FW), rem = e % (k * FW);
+    const int a = rem / FW, col = rem % FW;
+    const bool isx = col < IXPT;
+    const int t = 2 * kind2 + (isx ? 0 : 1);
+    const int64_t idx = isx ? G.ix0 + col : G.iy0 + (col - IXPT);
+    Fn[(kind2 * KA + a) * FW + col] = lat_tab_value(d, t, n0 + a, idx, Xn[2 * a], Xn[2 * a + 1]);
+  }
   if (tid < KINC) {
     // column c of L22^-1 by forward substitution
     const int c = tid;
@@ -460,63 +545,89 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     }
   }
   __syncthreads();
-  // ---- cells: thread u of the tile's (64 / KA) x 64 cells (iy fastest) ----
+  // ---- cells, block by block from the accumulators: block (m, n) holds rows
+  // 32 w + 16 m + (g + 4v) and columns 16 n + r. KA = 8: a 16-row block is two
+  // lattice columns x (h = 0, 1) of 8 rows a, the value of a for x h in lane
+  // (r, a % 4), register 2 h + a / 4; lanes (r, h < 2) finish cell (x h, column r).
+  // KA = 16: one x per block, register a / 4; lanes (r, 0) finish the cells. ----
   double bv = -__builtin_inf();
   int64_t bi = INT64_MAX;
   VT* const Vr = const_cast<VT*>(vres_ptr<VT>(d));
-  const GLOBAL double* grid = gp(d.grid);
-  for (int u = tid; u < IXPT * 64; u += NT) {
-    const int ixl = u >> 6, iyl = u & 63;
-    const int64_t ix = G.ix0 + ixl, iy = G.iy0 + iyl;
-    if (ix >= lat.nx || iy >= lat.ny) continue;
-    const int64_t c = ix * lat.sx + iy * lat.sy;
-    const double gx = grid[2 * c], gy = grid[2 * c + 1];
-    const double* tt = Ts + (KA * ixl) * LAT_TS + iyl;   // T~ of row a at tt[a * LAT_TS]
-    double vn[KA];
-    double vs = 0.0, ms = 0.0;
+  const bool elane = KA == 8 ? q < 2 : q == 0;
 #pragma unroll
-    for (int a = 0; a < KA; ++a) {
-      vn[a] = 0.0;
-      if (a < k) {
-        double t = psi_new(h, d.NL, n0 + a, gx, gy, Xn[2 * a], Xn[2 * a + 1]) - tt[a * LAT_TS];
+  for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
-        vn[a] = t / L22[a * KINC + a];
-        vs += vn[a] * vn[a];
-        ms += vn[a] * L22[KINC * KINC + a];
+    for (int n = 0; n < 4; ++n) {
+      double tt[KA];
+#pragma unroll
+      for (int a = 0; a < KA; ++a) {
+        if (KA == 8) {
+          const double t0 = lane_get(acc[m][n][a / 4], r + 16 * (a % 4));
+          const double t1 = lane_get(acc[m][n][2 + a / 4], r + 16 * (a % 4));
+          tt[a] = (q & 1) ? t1 : t0;
+        } else {
+          tt[a] = lane_get(acc[m][n][a / 4], r + 16 * (a % 4));
+        }
       }
-    }
-    const double vc = d.rvar_in[c] - vs;
-    const double mc = d.rmu_in[c] + ms;
-    VT* vt = Vr + (c / PBM) * d.vld * PBM + (c % PBM);
+      const int64_t ix = G.ix0 + (KA == 8 ? 4 * w + 2 * m + (q & 1) : 2 * w + m);
+      const int64_t iy = G.iy0 + 16 * n + r;
+      if (!(elane && ix < lat.nx && iy < lat.ny)) continue;
+      const int64_t c = ix * lat.sx + iy * lat.sy;
+      const int ixc = (int)(ix - G.ix0), iyc = IXPT + (int)(iy - G.iy0);
+      double vn[KA];
+      double vs = 0.0, ms = 0.0;
 #pragma unroll
-    for (int a = 0; a < KA; ++a)
-      if (a < k) vt[(n0 + a) * PBM] = (VT)vn[a];
-    d.mu[c] = mc;
-    d.var[c] = vc;
-    if (d.rmu) {
-      d.rmu[c] = mc;
-      d.rvar[c] = vc;
+      for (int a = 0; a < KA; ++a) {
+        vn[a] = 0.0;
+        if (a < k) {
+          const double* fL = Fn + a * FW;
+          const double* fH = Fn + (KA + a) * FW;
+          const double pn = fL[ixc] * fL[iyc] + fH[ixc] * fH[iyc];
+          double t = pn - tt[a];
+#pragma unroll
+          for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+          vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
+          vs += vn[a] * vn[a];
+          ms += vn[a] * L22[KINC * KINC + a];
+        }
+      }
+      const int uc = (ixc << 6) + (int)(iy - G.iy0);
+      const double vc = Ro[uc] - vs;
+      const double mc = Ro[IXPT * 64 + uc] + ms;
+      VT* vt = Vr + (c / PBM) * d.vld * PBM + (c % PBM);
+#pragma unroll
+      for (int a = 0; a < KA; ++a)
+        if (a < k) vt[(n0 + a) * PBM] = (VT)vn[a];
+      d.mu[c] = mc;
+      d.var[c] = vc;
+      if (d.rmu) {
+        d.rmu[c] = mc;
+        d.rvar[c] = vc;
+      }
+      argmax_pair(bv, bi, vc, c);
     }
-    argmax_pair(bv, bi, vc, c);
-  }
   // ---- F's new rows: -L22^-1 w^T for this tile's column blocks, L22^-1 (tile 0) ----
   const int64_t tiles = d.lat_tiles;
+  // (every block's flag was seen by one of this tile's splits before the tile's
+  // last split arrived; w is read with L2-bypassing loads all the same)
+  double* Wb = Fn;   // the block's w [64][16] (the cells are done with Fn)
   for (int64_t jb = tile; jb < d.nwb; jb += tiles) {
-    wait_flag(d, d.wflag + jb, d.epoch);
+    __syncthreads();
+    for (int e = tid; e < 64 * KINC; e += NT) Wb[e] = ldx<true>(&d.wv[64 * jb * KINC + e]);   // all in flight
+    __syncthreads();
     for (int e = tid; e < 64 * k; e += NT) {
-      const int a = e >> 6;
-      const int64_t j = 64 * jb + (e & 63);
+      const int a = e >> 6, jl = e & 63;
+      const int64_t j = 64 * jb + jl;
       if (j >= n0) continue;
       double t = 0.0;
-      for (int b = 0; b <= a; ++b) t -= Li[a * KINC + b] * d.wv[j * KINC + b];
-      d.F[j * ld + n0 + a] = t;
+      for (int b = 0; b <= a; ++b) t -= Li[a * KINC + b] * Wb[jl * KINC + b];
+      d.F[(n0 + a) * ld + j] = t;   // F row-major
     }
   }
   if (tile == 0)
     for (int e = tid; e < k * k; e += NT) {
       const int a = e / k, b = e % k;
-      if (b <= a) d.F[(n0 + b) * ld + n0 + a] = Li[a * KINC + b];
+      if (b <= a) d.F[(n0 + a) * ld + n0 + b] = Li[a * KINC + b];
     }
   if (d.vmax || d.vargmax || d.status_host)
     var_argmax_group(d, bv, bi, tile * 4 + w, tiles * 4);
@@ -538,11 +649,14 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
                           *reinterpret_cast<unsigned*>(sm + LAT_LDS + 8));
     return;
   }
-  if (role < np + d.nwb) {
-    lat_wblock<VT>(d, d.nwb - 1 - (role - np));
+  if (role < np + d.nwu) {
+    lat_wblock<VT>(d, role - np, sm);
     return;
   }
-  const int64_t g = role - np - d.nwb;
+#ifdef MFGP_DIAG_LATNOGEMM   // diagnostic build: producers and w only (timing only)
+  return;
+#endif
+  const int64_t g = role - np - d.nwu;
   if (g >= (int64_t)d.lat_tiles * d.ksplit) return;
   const int64_t tile = g % d.lat_tiles, s = g / d.lat_tiles;
   lat_gemm<KA, VT>(d, tile, s, sm);

@@ -123,8 +123,9 @@ __global__ __launch_bounds__(NT) void k_trinv(const GPDesc* __restrict__ descs, 
 }
 
 // The same for a batch (grid (block columns, GPs)): F = L^-1 of the n0 leading
-// factor rows into each GP's resident F (the lattice step's explicit inverse;
-// k_inc_lat then appends its rows).
+// factor rows into each GP's resident F, stored ROW-major (F[i][j] at i * ld + j:
+// the lattice step reads F's rows i over 64 consecutive columns j, one cache line
+// per 16 columns; k_inc_lat then appends its rows).
 __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
   const int64_t ld = d.ld, nbr = nblocks_rows(d.n0);
@@ -132,13 +133,14 @@ __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs
   if (J >= nbr || !d.lat_fbuild) return;
   __shared__ double As[TILE], Bs[TILE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
-  double* Xi = d.F;
+  const int r = lane & 15, q = lane >> 4;
+  double* Xt = d.F;
   for (int64_t I = J; I < nbr; ++I) {
     Acc acc;
     acc_zero(acc);
     for (int64_t K = J; K < I; ++K) {
       load_tile_cm(As, d.A, ld, I * NB, K * NB, tid);          // As[k][i] = L_IK[i][k]
-      load_tile_rm(Bs, Xi, ld, K * NB, J * NB, ld, tid);       // Bs[k][j] = X_KJ[k][j]
+      load_tile_cm(Bs, Xt, ld, J * NB, K * NB, tid);           // Bs[k][j] = X_KJ[k][j] (row-major X)
       __syncthreads();
       tile_mma<true>(As, Bs, acc, wm, wn, lane);               // acc -= L_IK X_KJ
       __syncthreads();
@@ -150,7 +152,6 @@ __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs
         Bs[swz(k, i)] = (i == k) ? 1.0 : 0.0;
       }
     } else {
-      const int r = lane & 15, q = lane >> 4;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -162,7 +163,13 @@ __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs
     Acc o;
     acc_zero(o);
     tile_mma<false>(As, Bs, o, wm, wn, lane);
-    store_acc_cm(o, Xi, ld, I * NB, J * NB, 1.0, wm, wn, lane);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          Xt[(I * NB + acc_row(wm, mt, q, v)) * ld + J * NB + acc_col(wn, nt, r)] = o.c[mt][nt][v];
     __threadfence_block();
     __syncthreads();
   }

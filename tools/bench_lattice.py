@@ -29,7 +29,7 @@ yn = torch.from_numpy(np.ascontiguousarray(np.stack([w.ynew for w in wls], 1).re
 res = {}
 for mode in ("vstream", "lattice"):
     ctx = _lib.Context(0)
-    ctx.set_lattice(mode == "lattice")
+    ctx.set_lattice(("force" if os.environ.get("MFGP_LAT_FORCE") else True) if mode == "lattice" else False)
     models = []
     for w in wls:
         m = _lib.Model(ctx, _lib.MF, hyp, 1e-8)

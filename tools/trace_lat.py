@@ -51,23 +51,24 @@ used = tr[:, 0] > 0
 t0 = tr[used, 0].min()
 tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)   # us (100 MHz realtime counter)
 nprod, nwb = 16, 32
+import math
+nwu = sum(math.ceil((2040 - 64 * j) / 1024) for j in range(32))
 role = np.arange(NWG) // B
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
 print(f"B={B}: percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
-for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w block", (role >= nprod) & (role < nprod + nwb), (0, 1, 2)),
-                         ("gemm", (role >= nprod + nwb) & used, (0, 1, 2, 3, 4))):
+for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w unit", (role >= nprod) & (role < nprod + nwu), (0, 1, 3, 2)),
+                         ("gemm", (role >= nprod + nwu) & used, (0, 1, 2, 3, 4))):
     for sl in slots:
         print(f"  {name:9s} slot {sl}: {q(tr[sel, sl])}")
-gm = (role >= nprod + nwb) & used
-w = tr[(role >= nprod) & (role < nprod + nwb)]
-jb = nwb - 1 - (role[(role >= nprod) & (role < nprod + nwb)] - nprod)
-for b in (31, 24, 16, 8, 0):
-    print(f"  w block jb={b:2d} published at {np.nanmedian(w[jb == b, 2]):7.1f} us")
+gm = (role >= nprod + nwu) & used
+w = tr[(role >= nprod) & (role < nprod + nwu)]
+print(f"  w units published (slot 2, last arrivers): {q(w[:, 2])}")
+print(f"  w unit F loop (slot 3 - slot 1): {q(w[:, 3] - w[:, 1])}; reduce+publish (2 - 3): {q(w[:, 2] - w[:, 3])}")
 print(f"  gemm K-loop durations (slot2 - slot1): {q(tr[gm, 2] - tr[gm, 1])}")
 S = int(os.environ.get("MFGP_LAT_KSPLIT", "0")) or None
 if S:
-    g = role - nprod - nwb
-    tiles = 32
+    g = role - nprod - nwu
+    tiles = 16
     for sp in range(S):
         sel = gm & (g // tiles == sp)
         print(f"  split {sp}: start {q(tr[sel, 1])} | mid {q(tr[sel, 5])} | loop end {q(tr[sel, 2])}")
