@@ -1016,6 +1016,12 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   }
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
+  // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
+  if (const char* e = std::getenv("MFGP_LATTICE")) {
+    const int v = std::atoi(e);
+    c->lattice = v != 0;
+    c->lat_force = v == 2;
+  }
   HIP_TRY(hipHostMalloc(&c->h_ring, sizeof(GPDesc) * RING * MAXB, hipHostMallocDefault));
   HIP_TRY(hipMalloc(&c->d_ring, sizeof(GPDesc) * RING * MAXB));
   for (int i = 0; i < RING; ++i) {
