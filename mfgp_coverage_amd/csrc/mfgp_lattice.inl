@@ -171,13 +171,42 @@ __device__ __forceinline__ void lat_wunit(int64_t n0, int64_t nwb, int64_t u, in
   c = u - u0;
 }
 
-// One w unit: columns j = 64 jb + [0, 64) of w = F11^T L21^T (+ row k: F^T z1,
-// unused), rows i of chunk c of [64 jb, n0) -- F's lower triangle below the
-// block. Wave w owns columns 64 jb + 16 w + r; one MFMA per 4 rows (B = F[i][j],
-// F row-major: a wave's load is four full 128-byte lines; A = the compact rows
-// L21c[i][a]), four accumulators in flight. A block of one chunk stores w itself; otherwise each
-// chunk stores its partial and the last of the block to arrive adds them in
-// chunk order. Either way the block's flag is raised once w is stored.
+// L22^-1 (rows / columns >= k zero) into Li [16][16] from the L22 record (sync[2]
+// must have been seen; plain loads: no line of the record is read in this launch
+// before that flag). L22 is scratch [16][16 | 16].
+__device__ __forceinline__ void lat_l22inv(const GPDesc& d, int k, double* L22, double* Li) {
+  const int tid = threadIdx.x;
+  for (int e = tid; e < KINC * KINC; e += NT) {
+    const double v = d.l22r[e];
+    L22[e] = (e / KINC < k && e % KINC <= e / KINC) ? v : 0.0;
+  }
+  __syncthreads();
+  if (tid < KINC) {
+    // column c of L22^-1 by forward substitution
+    const int c = tid;
+    double x[KINC];
+#pragma unroll
+    for (int i = 0; i < KINC; ++i) {
+      double t = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int b = 0; b < i; ++b) t -= L22[i * KINC + b] * x[b];
+      x[i] = (i < k && i >= c) ? t / L22[i * KINC + i] : 0.0;
+      Li[i * KINC + c] = x[i];
+    }
+  }
+  __syncthreads();
+}
+
+// One w unit: columns j = 64 jb + [0, 64) of w = F11^T L21^T, rows i of chunk c
+// of [64 jb, n0) -- F's lower triangle below the block. Each wave takes 32 of
+// every 128 rows and all 64 columns: lane (r, q) loads F[i][64 jb + 16 cb + r]
+// (four 128-byte lines per load, F row-major) for cb = 0..3 and the compact row
+// entry L21c[i][r] once for all four (MFMA A = L21c, B = F), so 80 VGPRs hold
+// 16 KB of F per wave in flight. The waves' sums meet in LDS in wave order. A
+// block of one chunk stores w itself; otherwise each chunk stores its partial
+// and the last of the block to arrive adds them in chunk order. Either way the
+// block's flag is raised once w is stored; then the same workgroup writes F's
+// new rows for the block, -L22^-1 w^T (and the top block's unit L22^-1).
 template <class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
   const int64_t n0 = d.n0, ld = d.ld;
@@ -202,50 +231,73 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     const int a = (int)(rem / tabw);
     const int64_t col = rem % tabw;
     const double* p = row_pt(d, n0 + a);
-    d.tab[t * tstride + (n0 + a) * tabw + col] = lat_tab_value(d, t, n0 + a, col, p[0], p[1]);
+    // written through: the GEMM tiles' epilogues read them in this launch (after
+    // the w flags, which follow the drain below)
+    stx<true>(&d.tab[t * tstride + (n0 + a) * tabw + col], lat_tab_value(d, t, n0 + a, col, p[0], p[1]));
   }
   wait_l21_from(d, i_lo);
   WTRACE(1);
-  const int64_t j = 64 * jb + 16 * w + r;
-  const GLOBAL double* Fr = gp(d.F) + j;   // F[i][j] at Fr[i * ld]
+  const GLOBAL double* Fr = gp(d.F) + 64 * jb + r;   // F[i][64 jb + 16 cb + r] at Fr[i * ld + 16 cb]
   d4 acc[4];
 #pragma unroll
   for (int x = 0; x < 4; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
-  constexpr int IU = 16;
-  for (int64_t i0 = i_lo; i0 < i_hi; i0 += 4 * IU) {
-    double f[IU], a[IU];
+#ifndef MFGP_DIAG_LATNOW
+  constexpr int RG = 8;   // 4-row groups per wave per batch (128 rows per batch)
+  for (int64_t i0 = i_lo + 32 * w; i0 < i_hi; i0 += 128) {
+    double f[RG][4], a[RG];
 #pragma unroll
-    for (int x = 0; x < IU; ++x) {
+    for (int x = 0; x < RG; ++x) {
       const int64_t i = i0 + 4 * x + q;
       const int64_t ii = i < i_hi ? i : i_lo;
       // F is read once per step and would evict the GEMM tiles' tables from L2
-#ifdef MFGP_DIAG_FPLAIN
-      f[x] = Fr[ii * ld];
-#else
-      f[x] = __builtin_nontemporal_load(Fr + ii * ld);
-#endif
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) f[x][cb] = __builtin_nontemporal_load(Fr + ii * ld + 16 * cb);
       a[x] = l21c_at<VT>(l21c, ii, r);
     }
 #pragma unroll
-    for (int x = 0; x < IU; ++x) {
+    for (int x = 0; x < RG; ++x) {
       const int64_t i = i0 + 4 * x + q;
-      acc[x & 3] = mfma(i < i_hi ? a[x] : 0.0, f[x], acc[x & 3]);
+      const double av = i < i_hi ? a[x] : 0.0;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(av, f[x][cb], acc[cb]);
     }
   }
+#endif
   WTRACE(3);
-  // lane (r, g) register v: row a = g + 4v of column j
-  double* const wv = d.wv;
-  double sum[4];
+  // the waves' sums in wave order: lane (r, g) register v of acc[cb] is w row
+  // a = g + 4 v, column jl = 16 cb + r; Wb [64 jl][16 a] after the sum
+  double* const red = sm;             // [4 w][4 cb][4 v][64 lanes]
+  double* const Wb = sm;              // [64][16], once the sums are read
+  double* const L22 = Wb + 64 * KINC;  // [16][16]
+  double* const Li = L22 + KINC * KINC;
+  static_assert(4096 <= LAT_LDS, "the w unit's LDS fits");
 #pragma unroll
-  for (int v = 0; v < 4; ++v) sum[v] = (acc[0][v] + acc[1][v]) + (acc[2][v] + acc[3][v]);
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) red[((w * 4 + cb) * 4 + v) * 64 + lane] = acc[cb][v];
+  __syncthreads();
+  double* const wv = d.wv;
+  // thread tid sums outputs e = tid + 256 m: (jl, a) = (e >> 4, e & 15)
+  double own[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int e = tid + NT * m, jl = e >> 4, a = e & 15;
+    const int cb = jl >> 4, rr = jl & 15, v = a >> 2, g = a & 3;
+    const int o = (cb * 4 + v) * 64 + 16 * g + rr;
+    own[m] = (red[o] + red[1024 + o]) + (red[2048 + o] + red[3072 + o]);
+  }
+  __syncthreads();
   if (nc == 1) {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) stx<true>(&wv[j * KINC + q + 4 * v], sum[v]);
+    for (int m = 0; m < 4; ++m) {
+      const int e = tid + NT * m;
+      stx<true>(&wv[64 * jb * KINC + e], own[m]);
+      Wb[e] = own[m];
+    }
   } else {
-    // partial [a][64 columns] of this chunk; the block's last unit adds them in chunk order
-    double* part = d.wpart + (u0 + c) * 1024 + (16 * w + r);
+    double* part = d.wpart + (u0 + c) * 1024;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) stx<true>(part + (q + 4 * v) * 64, sum[v]);
+    for (int m = 0; m < 4; ++m) stx<true>(part + tid + NT * m, own[m]);
     drain_stores();
     __syncthreads();
     unsigned& wlast = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 10);
@@ -256,17 +308,35 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     }
     __syncthreads();
     if (!wlast) return;
-    for (int e = tid; e < 1024; e += NT) {
-      const int a = e >> 6, jl = e & 63;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int e = tid + NT * m;
       double t = 0.0;
       for (int64_t cc = 0; cc < nc; ++cc) t += ldx<true>(d.wpart + (u0 + cc) * 1024 + e);
-      stx<true>(&wv[(64 * jb + jl) * KINC + a], t);
+      stx<true>(&wv[64 * jb * KINC + e], t);
+      Wb[e] = t;
     }
   }
   drain_stores();
   __syncthreads();
   if (tid == 0) publish(d.wflag + jb, d.epoch);
   WTRACE(2);
+  // F's new rows for this block: F[n0 + a][j] = -sum_{b <= a} L22^-1[a][b] w[j][b]
+  wait_flag(d, d.sync + 2, d.epoch);
+  lat_l22inv(d, k, L22, Li);
+  for (int e = tid; e < 64 * k; e += NT) {
+    const int a = e >> 6, jl = e & 63;
+    const int64_t j = 64 * jb + jl;
+    if (j >= n0) continue;
+    double t = 0.0;
+    for (int b = 0; b <= a; ++b) t -= Li[a * KINC + b] * Wb[jl * KINC + b];
+    d.F[(n0 + a) * ld + j] = t;   // F row-major
+  }
+  if (jb == d.nwb - 1)
+    for (int e = tid; e < k * k; e += NT) {
+      const int a = e / k, b = e % k;
+      if (b <= a) d.F[(n0 + a) * ld + n0 + b] = Li[a * KINC + b];
+    }
 }
 
 // Geometry of one GEMM tile, and its buffer-descriptor LDS-DMA plan (as
@@ -403,6 +473,11 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   // barrier (an LDS read, not a memory round trip) and spin on memory only if it
   // was not yet set. Wave 0 issues nothing else, so the flags' round trips never
   // sit in front of a table load in any wave's vmcnt order.
+  // (descriptor fields the loop and the epilogue use, in registers: the raw
+  // barriers' memory clobbers and the global stores would make the compiler reload
+  // them from the descriptor, a scalar-memory round trip each time)
+  const unsigned epoch = d.epoch;
+  const unsigned* const wflag = d.wflag;
   const int cnt = w == 0 ? 1 : 4;   // vector-memory ops per issued stage
   unsigned* const fl = reinterpret_cast<unsigned*>(sm + LNST * LSTG);   // [LNST][64]
   const __amdgpu_buffer_rsrc_t rfl = make_rsrc(reinterpret_cast<const double*>(d.wflag),
@@ -424,9 +499,12 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   };
   constexpr int D = LNST - 1;   // stages in flight ahead of the one consumed
   static_assert(D * 4 <= 12, "vm_wait_bar covers the outstanding ops");
+#ifdef MFGP_DIAG_LATNOWAIT   // diagnostic build: the GEMM does not wait for w (timing only)
+  auto spin_wave = [](const GPDesc&, const unsigned*, unsigned) {};
+#endif
   if (lo < hi) {
     if (w == 3)
-      for (int64_t st = lo; st < lo + D && st < hi; ++st) spin_wave(d, d.wflag + blk(st), d.epoch);
+      for (int64_t st = lo; st < lo + D && st < hi; ++st) spin_wave(d, wflag + blk(st), epoch);
     WTRACE(1);
     for (int64_t st = lo; st < lo + D && st < hi; ++st) issue(st, st + D);
     // iteration t: stage t sits in slot (t - lo) % LNST, issued D iterations ago
@@ -435,18 +513,22 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
       const int64_t after = (hi - 1 - t) < (D - 1) ? (hi - 1 - t) : (D - 1);
       vm_wait_bar((int)after * cnt);
       if (t + D < hi) {
-        if (w == 3 && fl[((t + D - lo) % LNST) * 64] != d.epoch) spin_wave(d, d.wflag + blk(t + D), d.epoch);
+        if (w == 3 && fl[((t + D - lo) % LNST) * 64] != epoch) spin_wave(d, wflag + blk(t + D), epoch);
         issue(t + D, t + 2 * D);
       }
 #ifndef MFGP_DIAG_LATNOCOMP   // diagnostic build: the pipeline without its compute (timing only)
       lat_compute<KA>(sm + ((t - lo) % LNST) * LSTG, acc, r, q, ar, ixl0, ixl1);
 #endif
-      if (t == (lo + hi) / 2) WTRACE(5);
     }
   }
   vm_wait_all();
   __syncthreads();
   WTRACE(2);
+  // the L22 record's flag (sync[2], raised by the finish long before any K loop
+  // ends): read with the partial stores, so the reducer rarely waits for it
+  unsigned& l22_seen = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 11);
+  if (tid == 0)
+    l22_seen = __hip_atomic_load(d.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch ? 1u : 0u;
   // split-K: partials through memory, the last split reduces them in split order
   if (S > 1) {
     unsigned& lat_last = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 9);
@@ -484,53 +566,44 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
           }
     }
   }
-  // ---- epilogue: L22 / z2 (sync[2]), the new rows, L22^-1 (LDS: the ring is dead) ----
-  const int64_t n0 = d.n0, ld = d.ld;
+  if (!l22_seen) wait_flag(d, d.sync + 2, epoch);
+  WTRACE(3);
+  // ---- epilogue (LDS: the ring is dead) ----
+  const int64_t n0 = d.n0;
   const int k = (int)(d.N - n0);
-  double* L22 = sm;                              // [16][16] | z2 [16]
-  double* Li = L22 + KINC * KINC + KINC;         // L22^-1 [16][16]
-  double* Xn = Li + KINC * KINC;                 // new rows (x, y)
-  // psi(cell, new row a) = c_L exL[a][ix] eyL[a][iy] + c_H exH[a][ix] eyH[a][iy] for
-  // the tile's IXPT x 64 cells: the factors of the k new rows (c_L, c_H folded into
-  // ex), [KA][IXPT + 64] per kind (separable like the GEMM's terms)
-  double* Fn = Xn + 2 * KINC;
   constexpr int FW = IXPT + 64;
-  // the old posterior of the tile's cells, fetched while the epilogue waits for L22
-  double* Ro = Fn + 2 * KA * FW;   // [2][IXPT * 64]: var_old | mu_old
-  static_assert(560 + 2 * 16 * (8 + 64) + 2 * 8 * 64 <= LAT_LDS && 560 + 2 * 8 * 80 + 2 * 16 * 64 <= LAT_LDS,
+  constexpr int NBP = KA == 8 ? 2 : 1;      // 16-column blocks per cell pass
+  constexpr int TW = 16 * NBP;              // Ts row width
+  double* const L22 = sm;                   // [16][16] | z2 [16]
+  double* const Li = L22 + KINC * KINC + KINC;   // L22^-1 [16][16]
+  // psi(cell, new row a) = c_L exL[a][ix] eyL[a][iy] + c_H exH[a][ix] eyH[a][iy]:
+  // the new rows' separable tables (written through by the w units before their
+  // flags) for the tile's IXPT x 64 cells, [2 kinds][KA][IXPT | 64]
+  double* const Fn = Li + KINC * KINC;
+  double* const Ts = Fn + 2 * KA * FW;      // one cell pass of T: [4 waves][16 rows][TW]
+  static_assert(KINC * KINC + KINC + KINC * KINC + 2 * 8 * (16 + 64) + 4 * 16 * 32 <= LAT_LDS &&
+                    KINC * KINC + KINC + KINC * KINC + 2 * 16 * (8 + 64) + 4 * 16 * 16 <= LAT_LDS,
                 "the epilogue's LDS fits the ring's");
   __syncthreads();   // the ring's last reads are done
-  for (int u = tid; u < IXPT * 64; u += NT) {
-    const int64_t ix = G.ix0 + (u >> 6), iy = G.iy0 + (u & 63);
-    if (ix < lat.nx && iy < lat.ny) {
-      const int64_t c = ix * lat.sx + iy * lat.sy;
-      Ro[u] = d.rvar_in[c];
-      Ro[IXPT * 64 + u] = d.rmu_in[c];
+  {
+    // plain loads: no line of the record or of the new rows' tables is read in
+    // this launch before sync[2] / the w flags
+    for (int e = tid; e < KINC * KINC + KINC; e += NT) {
+      const double v = d.l22r[e];
+      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+      L22[e] = use ? v : 0.0;
+    }
+    const int64_t tstride = d.ld * d.tabw, tabw = d.tabw;
+    for (int e = tid; e < 2 * KA * FW; e += NT) {
+      const int kind2 = e / (KA * FW), rem = e % (KA * FW);
+      const int a = rem / FW, col = rem % FW;
+      const bool isx = col < IXPT;
+      const int t = 2 * kind2 + (isx ? 0 : 1);
+      const int64_t idx = isx ? G.ix0 + col : G.iy0 + (col - IXPT);
+      Fn[e] = a < k ? d.tab[t * tstride + (n0 + a) * tabw + idx] : 0.0;
     }
   }
-  wait_flag(d, d.sync + 2, d.epoch);
-  WTRACE(3);
-  for (int e = tid; e < KINC * KINC + KINC; e += NT) {
-    // plain loads: no line of the record is read in this launch before sync[2]
-    const double v = d.l22r[e];
-    const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
-    L22[e] = use ? v : 0.0;
-  }
-  if (tid >= NT - KINC) {
-    const int a = tid - (NT - KINC);
-    const double* p = row_pt(d, n0 + (a < k ? a : 0));
-    Xn[2 * a] = p[0];
-    Xn[2 * a + 1] = p[1];
-  }
   __syncthreads();
-  for (int e = tid; e < 2 * k * FW; e += NT) {
-    const int kind2 = e / (k * FW), rem = e % (k * FW);
-    const int a = rem / FW, col = rem % FW;
-    const bool isx = col < IXPT;
-    const int t = 2 * kind2 + (isx ? 0 : 1);
-    const int64_t idx = isx ? G.ix0 + col : G.iy0 + (col - IXPT);
-    Fn[(kind2 * KA + a) * FW + col] = lat_tab_value(d, t, n0 + a, idx, Xn[2 * a], Xn[2 * a + 1]);
-  }
   if (tid < KINC) {
     // column c of L22^-1 by forward substitution
     const int c = tid;
@@ -544,91 +617,100 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
       Li[i * KINC + c] = x[i];
     }
   }
-  __syncthreads();
-  // ---- cells, block by block from the accumulators: block (m, n) holds rows
-  // 32 w + 16 m + (g + 4v) and columns 16 n + r. KA = 8: a 16-row block is two
-  // lattice columns x (h = 0, 1) of 8 rows a, the value of a for x h in lane
-  // (r, a % 4), register 2 h + a / 4; lanes (r, h < 2) finish cell (x h, column r).
-  // KA = 16: one x per block, register a / 4; lanes (r, 0) finish the cells. ----
+  WTRACE(5);
+  // ---- cells: one pass per (m, group of NBP column blocks); the waves put
+  // their blocks' T into Ts (row rho = g + 4 v of block (m, n) is, for KA = 8,
+  // lattice column h = rho / 8 of the wave's pair and new row a = rho % 8; for
+  // KA = 16 new row a = rho), then thread tid finishes one cell: source wave
+  // cw = tid / 64, (h, column) from the rest. ----
   double bv = -__builtin_inf();
   int64_t bi = INT64_MAX;
   VT* const Vr = const_cast<VT*>(vres_ptr<VT>(d));
-  const bool elane = KA == 8 ? q < 2 : q == 0;
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      double tt[KA];
-#pragma unroll
-      for (int a = 0; a < KA; ++a) {
-        if (KA == 8) {
-          const double t0 = lane_get(acc[m][n][a / 4], r + 16 * (a % 4));
-          const double t1 = lane_get(acc[m][n][2 + a / 4], r + 16 * (a % 4));
-          tt[a] = (q & 1) ? t1 : t0;
-        } else {
-          tt[a] = lane_get(acc[m][n][a / 4], r + 16 * (a % 4));
-        }
-      }
-      const int64_t ix = G.ix0 + (KA == 8 ? 4 * w + 2 * m + (q & 1) : 2 * w + m);
-      const int64_t iy = G.iy0 + 16 * n + r;
-      if (!(elane && ix < lat.nx && iy < lat.ny)) continue;
+  const int64_t vld = d.vld;
+  double* const omu = d.mu;
+  double* const ovar = d.var;
+  double* const rmu = d.rmu;
+  double* const rvar = d.rvar;
+  const double* const rmu_in = d.rmu_in;
+  const double* const rvar_in = d.rvar_in;
+  const int cw = tid >> 6, cl = tid & 63;
+  const int ch = KA == 8 ? cl >> 5 : 0;
+  const int cyl = KA == 8 ? cl & 31 : cl & 15;
+  const bool cact = KA == 8 || cl < 16;
+  constexpr int NPASS = 2 * (4 / NBP);
+  auto cell_of = [&](int p, int64_t& ix, int64_t& iy) {
+    const int m = p / (4 / NBP), nf = NBP * (p % (4 / NBP));
+    ix = G.ix0 + (KA == 8 ? 4 * cw + 2 * m + ch : 2 * cw + m);
+    iy = G.iy0 + 16 * nf + cyl;
+  };
+  auto cell_ok = [&](int64_t ix, int64_t iy) { return cact && ix < lat.nx && iy < lat.ny; };
+  // the old posterior of this thread's cell of the next pass, one pass ahead
+  double ov = 0.0, om = 0.0;
+  {
+    int64_t ix, iy;
+    cell_of(0, ix, iy);
+    if (cell_ok(ix, iy)) {
       const int64_t c = ix * lat.sx + iy * lat.sy;
-      const int ixc = (int)(ix - G.ix0), iyc = IXPT + (int)(iy - G.iy0);
-      double vn[KA];
-      double vs = 0.0, ms = 0.0;
-#pragma unroll
-      for (int a = 0; a < KA; ++a) {
-        vn[a] = 0.0;
-        if (a < k) {
-          const double* fL = Fn + a * FW;
-          const double* fH = Fn + (KA + a) * FW;
-          const double pn = fL[ixc] * fL[iyc] + fH[ixc] * fH[iyc];
-          double t = pn - tt[a];
-#pragma unroll
-          for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
-          vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
-          vs += vn[a] * vn[a];
-          ms += vn[a] * L22[KINC * KINC + a];
-        }
-      }
-      const int uc = (ixc << 6) + (int)(iy - G.iy0);
-      const double vc = Ro[uc] - vs;
-      const double mc = Ro[IXPT * 64 + uc] + ms;
-      VT* vt = Vr + (c / PBM) * d.vld * PBM + (c % PBM);
-#pragma unroll
-      for (int a = 0; a < KA; ++a)
-        if (a < k) vt[(n0 + a) * PBM] = (VT)vn[a];
-      d.mu[c] = mc;
-      d.var[c] = vc;
-      if (d.rmu) {
-        d.rmu[c] = mc;
-        d.rvar[c] = vc;
-      }
-      argmax_pair(bv, bi, vc, c);
-    }
-  // ---- F's new rows: -L22^-1 w^T for this tile's column blocks, L22^-1 (tile 0) ----
-  const int64_t tiles = d.lat_tiles;
-  // (every block's flag was seen by one of this tile's splits before the tile's
-  // last split arrived; w is read with L2-bypassing loads all the same)
-  double* Wb = Fn;   // the block's w [64][16] (the cells are done with Fn)
-  for (int64_t jb = tile; jb < d.nwb; jb += tiles) {
-    __syncthreads();
-    for (int e = tid; e < 64 * KINC; e += NT) Wb[e] = ldx<true>(&d.wv[64 * jb * KINC + e]);   // all in flight
-    __syncthreads();
-    for (int e = tid; e < 64 * k; e += NT) {
-      const int a = e >> 6, jl = e & 63;
-      const int64_t j = 64 * jb + jl;
-      if (j >= n0) continue;
-      double t = 0.0;
-      for (int b = 0; b <= a; ++b) t -= Li[a * KINC + b] * Wb[jl * KINC + b];
-      d.F[(n0 + a) * ld + j] = t;   // F row-major
+      ov = rvar_in[c];
+      om = rmu_in[c];
     }
   }
-  if (tile == 0)
-    for (int e = tid; e < k * k; e += NT) {
-      const int a = e / k, b = e % k;
-      if (b <= a) d.F[(n0 + a) * ld + n0 + b] = Li[a * KINC + b];
+#pragma unroll
+  for (int p = 0; p < NPASS; ++p) {
+    const int m = p / (4 / NBP), nf = NBP * (p % (4 / NBP));
+    __syncthreads();   // the previous pass's Ts reads (and Li) are done
+#pragma unroll
+    for (int nb = 0; nb < NBP; ++nb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) Ts[(w * 16 + q + 4 * v) * TW + 16 * nb + r] = acc[m][nf + nb][v];
+    __syncthreads();
+    int64_t ix, iy;
+    cell_of(p, ix, iy);
+    const double cov = ov, com = om;
+    if (p + 1 < NPASS) {
+      int64_t ix2, iy2;
+      cell_of(p + 1, ix2, iy2);
+      if (cell_ok(ix2, iy2)) {
+        const int64_t c2 = ix2 * lat.sx + iy2 * lat.sy;
+        ov = rvar_in[c2];
+        om = rmu_in[c2];
+      }
     }
+    if (!cell_ok(ix, iy)) continue;
+    const int64_t c = ix * lat.sx + iy * lat.sy;
+    const int ixc = (int)(ix - G.ix0), iyc = IXPT + (int)(iy - G.iy0);
+    const double* const Tc = Ts + (cw * 16 + (KA == 8 ? 8 * ch : 0)) * TW + cyl;
+    VT* const vt = Vr + (c / PBM) * vld * PBM + (c % PBM);
+    double vn[KA];
+    double vs = 0.0, ms = 0.0;
+#pragma unroll
+    for (int a = 0; a < KA; ++a) {
+      vn[a] = 0.0;
+      if (a < k) {
+        const double* fL = Fn + a * FW;
+        const double* fH = Fn + (KA + a) * FW;
+        const double pn = fL[ixc] * fL[iyc] + fH[ixc] * fH[iyc];
+        double t = pn - Tc[a * TW];
+#pragma unroll
+        for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+        vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
+        vs += vn[a] * vn[a];
+        ms += vn[a] * L22[KINC * KINC + a];
+        vt[(n0 + a) * PBM] = (VT)vn[a];
+      }
+    }
+    const double vc = cov - vs;
+    const double mc = com + ms;
+    omu[c] = mc;
+    ovar[c] = vc;
+    if (rmu) {
+      rmu[c] = mc;
+      rvar[c] = vc;
+    }
+    argmax_pair(bv, bi, vc, c);
+  }
+  const int64_t tiles = d.lat_tiles;
+  WTRACE(6);
   if (d.vmax || d.vargmax || d.status_host)
     var_argmax_group(d, bv, bi, tile * 4 + w, tiles * 4);
   WTRACE(4);

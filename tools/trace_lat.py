@@ -1,7 +1,7 @@
 """Diagnostic: per-workgroup timeline of k_inc_lat (a -DMFGP_STAMPS build, argv[1]).
-Slots: producers 0 start / 1 arrival / 4 end; w blocks 0 start / 1 past the L21 wait /
+Slots: producers 0 start / 1 arrival / 4 end; w blocks 0 start / 1 past the L21 wait / 3 F loop done /
 2 published; GEMM 0 start / 1 past the first w waits / 2 K loop done / 3 past the
-L22 wait (reducers) / 4 end. Launches back to back; the trace is the last launch's."""
+L22 wait (reducers) / 5 new-row factors and L22^-1 done / 6 cells done / 4 end. Launches back to back; the trace is the last launch's."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["MFGP_LIB"] = sys.argv[1]
@@ -46,7 +46,7 @@ for s in range(T):
 ctx.synchronize()
 assert models[0].stats()["lattice"] == T, models[0].stats()
 raw = st.cpu().numpy()[64:64 + 8 * NWG].reshape(NWG, 8)
-tr = raw[:, :6].astype(np.float64)
+tr = raw[:, :7].astype(np.float64)
 used = tr[:, 0] > 0
 t0 = tr[used, 0].min()
 tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)   # us (100 MHz realtime counter)
@@ -57,7 +57,7 @@ role = np.arange(NWG) // B
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
 print(f"B={B}: percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
 for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w unit", (role >= nprod) & (role < nprod + nwu), (0, 1, 3, 2)),
-                         ("gemm", (role >= nprod + nwu) & used, (0, 1, 2, 3, 4))):
+                         ("gemm", (role >= nprod + nwu) & used, (0, 1, 2, 3, 5, 6, 4))):
     for sl in slots:
         print(f"  {name:9s} slot {sl}: {q(tr[sel, sl])}")
 gm = (role >= nprod + nwu) & used
@@ -65,10 +65,30 @@ w = tr[(role >= nprod) & (role < nprod + nwu)]
 print(f"  w units published (slot 2, last arrivers): {q(w[:, 2])}")
 print(f"  w unit F loop (slot 3 - slot 1): {q(w[:, 3] - w[:, 1])}; reduce+publish (2 - 3): {q(w[:, 2] - w[:, 3])}")
 print(f"  gemm K-loop durations (slot2 - slot1): {q(tr[gm, 2] - tr[gm, 1])}")
+red = gm & np.isfinite(tr[:, 3])
+print(f"  reducers: reduce+L22 wait (3 - 2) {q(tr[red, 3] - tr[red, 2])}; Fn/Li (5 - 3) {q(tr[red, 5] - tr[red, 3])}; "
+      f"cells (6 - 5) {q(tr[red, 6] - tr[red, 5])}; argmax (4 - 6) {q(tr[red, 4] - tr[red, 6])}")
 S = int(os.environ.get("MFGP_LAT_KSPLIT", "0")) or None
 if S:
     g = role - nprod - nwu
     tiles = 16
     for sp in range(S):
         sel = gm & (g // tiles == sp)
-        print(f"  split {sp}: start {q(tr[sel, 1])} | mid {q(tr[sel, 5])} | loop end {q(tr[sel, 2])}")
+        print(f"  split {sp}: start {q(tr[sel, 1])} | loop end {q(tr[sel, 2])}")
+# placement: GEMM workgroups per CU (XCC, SE, SH, CU from the HW_ID / XCC_ID
+# registers) and the K-loop duration against that count
+hw = raw[:, 7]
+cu = ((hw >> 32) & 0xF) * 1024 + ((hw >> 13) & 0x7) * 64 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xF)
+gcu = cu[gm]
+ucu, cnt = np.unique(gcu, return_counts=True)
+print("  GEMM WGs per CU: histogram", dict(zip(*np.unique(cnt, return_counts=True))), "over", len(ucu), "CUs")
+per = dict(zip(ucu, cnt))
+ncnt = np.array([per[c] for c in gcu])
+dur = tr[gm, 2] - tr[gm, 1]
+for n in sorted(set(ncnt)):
+    print(f"    CUs with {n} GEMM WGs: K-loop {q(dur[ncnt == n])}")
+wsel = (role >= nprod) & (role < nprod + nwu)
+wcu = dict(zip(*np.unique(cu[wsel], return_counts=True)))
+nw = np.array([wcu.get(c, 0) for c in gcu])
+for n in sorted(set(nw)):
+    print(f"    GEMM WGs sharing their CU with {n} w units: K-loop {q(dur[nw == n])}")
