@@ -179,11 +179,22 @@ struct mfgp_model {
   int64_t wv_ld = 0;
   unsigned* wflag = nullptr;  // [wv_ld / 64 + 2]
   unsigned* wcnt = nullptr;   // [wv_ld / 64 + 2]
-  double* wpart = nullptr;    // [lat_wunits(wv_ld)][1024]
+  double* wpart = nullptr;    // [lat_wunits(wv_ld, LAT_WCH_MIN)][1024]
   double* gpart = nullptr;    // split-K partials
   size_t gpart_n = 0;
   unsigned* gcnt = nullptr;   // per GEMM tile
   int64_t gcnt_n = 0;
+  int* lidx = nullptr;        // lattice indices per training row [tab_ld], rows [0, tab_n) (with the tables)
+  double* axt = nullptr;      // axis tables [4][tabw + 1][tabw], current for generation axt_gen
+  int64_t axt_w = 0;
+  uint64_t axt_gen = 0;
+  double* zb = nullptr;       // Z rows [P][zrows][tabw][zb_ka]
+  int64_t zb_rows = 0, zb_w = 0;
+  int zb_ka = 0;
+  unsigned* zflag = nullptr;  // [zflag_n]
+  int64_t zflag_n = 0;
+  unsigned* ldone = nullptr;  // [4] lattice phase hand-offs (arrivals | flag, twice)
+  int* zvl = nullptr;         // [2][zb_rows + 1]
 };
 
 namespace {
@@ -330,11 +341,13 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   }
   // the lattice step's F and tables move to the new leading dimension too
   double *F = nullptr, *tab = nullptr;
+  int* lidx = nullptr;
   if (keep && m->F && m->F_n > 0) {
-    HIP_TRY(hipMalloc(&F, sizeof(double) * ld * ld));
-    HIP_TRY(hipMemsetAsync(F, 0, sizeof(double) * ld * ld, c->stream));
-    HIP_TRY(hipMemcpy2DAsync(F, sizeof(double) * ld, m->F, sizeof(double) * m->F_ld, sizeof(double) * m->F_ld,
-                             m->F_ld, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMalloc(&F, sizeof(double) * fblk_size(ld)));
+    HIP_TRY(hipMemsetAsync(F, 0, sizeof(double) * fblk_size(ld), c->stream));
+    for (int64_t jb = 0; 64 * jb < m->F_n; ++jb)   // each column block's rows [64 jb, F_n)
+      HIP_TRY(hipMemcpyAsync(F + fblk_off(jb, ld), m->F + fblk_off(jb, m->F_ld),
+                             sizeof(double) * 64 * (m->F_n - 64 * jb), hipMemcpyDeviceToDevice, c->stream));
   }
   if (m->tab && m->tab_n > 0) {
     HIP_TRY(hipMalloc(&tab, sizeof(double) * 4 * ld * m->tabw));
@@ -342,10 +355,14 @@ int ensure_cap(mfgp_model* m, int64_t need) {
     for (int t = 0; t < 4; ++t)
       HIP_TRY(hipMemcpyAsync(tab + (size_t)t * ld * m->tabw, m->tab + (size_t)t * m->tab_ld * m->tabw,
                              sizeof(double) * m->tab_n * m->tabw, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMalloc(&lidx, sizeof(int) * ld));
+    HIP_TRY(hipMemcpyAsync(lidx, m->lidx, sizeof(int) * m->tab_n, hipMemcpyDeviceToDevice, c->stream));
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (m->F) HIP_TRY(hipFree(m->F));
   if (m->tab) HIP_TRY(hipFree(m->tab));
+  if (m->lidx) HIP_TRY(hipFree(m->lidx));
+  m->lidx = lidx;
   m->F = F;
   m->F_ld = F ? ld : 0;
   if (!F) m->F_n = 0;
@@ -561,25 +578,32 @@ int64_t lat_tabw(const mfgp_model* m) { return round_up(std::max<int64_t>(m->lat
 int64_t lat_tiles(const mfgp_model* m, int ka) {
   return ((m->lat.nx + 128 / ka - 1) / (128 / ka)) * ((m->lat.ny + 63) / 64);
 }
+// Z units of the lattice-axis form: parts x ceil(ny / zq), zq lattice y-rows each
+// (two per thread group of tabw threads)
+int lat_zq(const mfgp_model* m) { return (int)(2 * NT / lat_tabw(m)); }
+int64_t lat_nzu(const mfgp_model* m) {
+  return (m->kind == MFGP_SF ? 1 : 2) * ((m->lat.ny + lat_zq(m) - 1) / lat_zq(m));
+}
 // Can the bordered append of rows [n0, N) and its predict take k_inc_lat?
 bool lat_eligible(const mfgp_model* m, int64_t n0) {
   const int64_t k = m->NL + m->NH - n0;
   if (!m->ctx->lattice || m->lat.nx <= 0 || m->M <= 0 || k < 1 || k > KINC || n0 < 1) return false;
+  if (lat_tabw(m) > NT) return false;   // a Z unit's thread per lattice column
   if (!lat_cond_ok(m)) return false;
   const int b = res_find(m, n0);
   return b >= 0 && m->res_depth[b] < LAT_MAXD;
 }
 // F, the tables, w and the flags at the model's leading dimension (contents kept
 // across capacity growth: ensure_cap moves them)
-int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit) {
+int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
   hipStream_t s = m->ctx->stream;
   const int64_t ld = m->ld, tabw = lat_tabw(m);
   if (!m->F || m->F_ld != ld) {
     HIP_TRY(hipStreamSynchronize(s));
     if (m->F) HIP_TRY(hipFree(m->F));
     m->F = nullptr;
-    HIP_TRY(hipMalloc(&m->F, sizeof(double) * ld * ld));
-    HIP_TRY(hipMemsetAsync(m->F, 0, sizeof(double) * ld * ld, s));   // F's upper triangle stays zero
+    HIP_TRY(hipMalloc(&m->F, sizeof(double) * fblk_size(ld)));
+    HIP_TRY(hipMemsetAsync(m->F, 0, sizeof(double) * fblk_size(ld), s));   // F's upper triangle stays zero
     m->F_ld = ld;
     m->F_n = 0;
   }
@@ -589,6 +613,9 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit) {
     m->tab = nullptr;
     HIP_TRY(hipMalloc(&m->tab, sizeof(double) * 4 * ld * tabw));
     HIP_TRY(hipMemsetAsync(m->tab, 0, sizeof(double) * 4 * ld * tabw, s));
+    if (m->lidx) HIP_TRY(hipFree(m->lidx));
+    m->lidx = nullptr;
+    HIP_TRY(hipMalloc(&m->lidx, sizeof(int) * ld));
     m->tab_ld = ld;
     m->tabw = tabw;
     m->tab_n = 0;
@@ -609,7 +636,7 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit) {
     HIP_TRY(hipMemsetAsync(m->wflag, 0, sizeof(unsigned) * (ld / 64 + 2), s));   // below every epoch
     HIP_TRY(hipMalloc(&m->wcnt, sizeof(unsigned) * (ld / 64 + 2)));
     HIP_TRY(hipMemsetAsync(m->wcnt, 0, sizeof(unsigned) * (ld / 64 + 2), s));
-    HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 1024 * lat_wunits(ld)));
+    HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 1024 * lat_wunits(ld, LAT_WCH_MIN)));
     m->wv_ld = ld;
   }
   if (m->gcnt_n < tiles) {
@@ -619,6 +646,44 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit) {
     HIP_TRY(hipMalloc(&m->gcnt, sizeof(unsigned) * tiles));
     HIP_TRY(hipMemsetAsync(m->gcnt, 0, sizeof(unsigned) * tiles, s));
     m->gcnt_n = tiles;
+  }
+  if (!m->axt || m->axt_w != tabw) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->axt) HIP_TRY(hipFree(m->axt));
+    m->axt = nullptr;
+    HIP_TRY(hipMalloc(&m->axt, sizeof(double) * 4 * (tabw + 1) * tabw));
+    m->axt_w = tabw;
+    m->axt_gen = UINT64_MAX;   // build before use
+  }
+  // Z rows: per part the lattice y-rows (padded to ZKS), then one per training row
+  // that could lie off the lattice; zeros where never written (padding rows)
+  const int64_t zrows = round_up(m->lat.ny, ZKS) + ld;
+  if (!m->zb || m->zb_rows != zrows || m->zb_w != tabw || m->zb_ka < ka) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->zb) HIP_TRY(hipFree(m->zb));
+    if (m->zvl) HIP_TRY(hipFree(m->zvl));
+    m->zb = nullptr;
+    m->zvl = nullptr;
+    const size_t zn = (size_t)2 * zrows * tabw * ka;
+    HIP_TRY(hipMalloc(&m->zb, sizeof(double) * zn));
+    HIP_TRY(hipMemsetAsync(m->zb, 0, sizeof(double) * zn, s));
+    HIP_TRY(hipMalloc(&m->zvl, sizeof(int) * 2 * (zrows + 1)));
+    HIP_TRY(hipMemsetAsync(m->zvl, 0, sizeof(int) * 2 * (zrows + 1), s));
+    m->zb_rows = zrows;
+    m->zb_w = tabw;
+    m->zb_ka = ka;
+  }
+  if (!m->ldone) {
+    HIP_TRY(hipMalloc(&m->ldone, sizeof(unsigned) * 4));
+    HIP_TRY(hipMemsetAsync(m->ldone, 0, sizeof(unsigned) * 4, s));   // no arrivals; flags below every epoch
+  }
+  if (m->zflag_n < nzu) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->zflag) HIP_TRY(hipFree(m->zflag));
+    m->zflag = nullptr;
+    HIP_TRY(hipMalloc(&m->zflag, sizeof(unsigned) * nzu));
+    HIP_TRY(hipMemsetAsync(m->zflag, 0, sizeof(unsigned) * nzu, s));   // below every epoch
+    m->zflag_n = nzu;
   }
   const size_t need = ksplit > 1 ? (size_t)tiles * ksplit * 8192 : 0;   // LAT_PART doubles per split tile
   if (need > m->gpart_n) {
@@ -640,6 +705,12 @@ void free_lat(mfgp_model* m) {
   if (m->gpart) (void)hipFree(m->gpart);
   if (m->gcnt) (void)hipFree(m->gcnt);
   if (m->res) (void)hipFree(m->res);
+  if (m->lidx) (void)hipFree(m->lidx);
+  if (m->axt) (void)hipFree(m->axt);
+  if (m->zb) (void)hipFree(m->zb);
+  if (m->zflag) (void)hipFree(m->zflag);
+  if (m->ldone) (void)hipFree(m->ldone);
+  if (m->zvl) (void)hipFree(m->zvl);
 }
 
 // Enqueue assembly + blocked Cholesky for `count` models (descriptors already uploaded).
@@ -831,14 +902,17 @@ int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
 // and the separable tables they need (k_trinv_f / k_lat_tables: only when a model
 // enters the mode with a new factor, grid or hyperparameters).
 int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
-  int64_t max_blocks = 0, max_nbr = 0, max_rows = 0;
+  int64_t max_blocks = 0, max_nbr = 0, max_rows = 0, max_axw = 0;
   for (int i = 0; i < count; ++i) {
-    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + (int64_t)hd[i].lat_tiles * hd[i].ksplit);
+    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu +
+                                                   (int64_t)hd[i].lat_tiles * hd[i].ksplit);
     if (hd[i].lat_fbuild) max_nbr = std::max(max_nbr, nblocks_rows(hd[i].n0));
     max_rows = std::max(max_rows, hd[i].n0 - hd[i].tab_lo);
+    if (hd[i].lat_axbuild) max_axw = std::max(max_axw, hd[i].tabw);
   }
   if (max_nbr > 0) HIP_TRY(launch_trinv_f(dd, count, max_nbr, c->stream));
   if (max_rows > 0) HIP_TRY(launch_lat_tables(dd, count, max_rows, c->stream));
+  if (max_axw > 0) HIP_TRY(launch_lat_axes(dd, count, max_axw, c->stream));
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
@@ -1656,7 +1730,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     for (int i = 0; lat && i < ninc; ++i) lat = lat_eligible(order[i], hd[i].n0);
     res_depth.assign(ninc, 0);
     int ka = 8;
-    int64_t tiles_sum = 0, nwb_min = INT64_MAX;
+    int64_t tiles_sum = 0, nst_min = INT64_MAX;
     if (lat) {
       for (int i = 0; i < ninc; ++i) {
         if (order[i]->NL + order[i]->NH - hd[i].n0 > 8) ka = 16;
@@ -1664,8 +1738,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];
         tiles_sum += lat_tiles(m, ka);
-        const int64_t nwb = (hd[i].n0 + 63) / 64;
-        nwb_min = std::min(nwb_min, nwb);
+        // K stages of the axis rows (virtual rows add more)
+        const int64_t nst = (m->kind == MFGP_SF ? 1 : 2) * (round_up(m->lat.ny, ZKS) / ZKS);
+        nst_min = std::min(nst_min, nst);
       }
       // too few GEMM tiles to fill the chip (headline size: 16 tiles per GP): the w
       // pass and the split-K reductions cost more than the V stream they save.
@@ -1677,14 +1752,26 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     if (lat) {
       // split-K so that the GEMM tiles fill the chip about twice, >= 4 stages each
       int S = (int)std::min<int64_t>(8, std::max<int64_t>(1, (2 * c->ncu + tiles_sum - 1) / tiles_sum));
-      // (split s takes every S-th 64-row block of terms: at least one block each)
-      S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nwb_min));
-      if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, nwb_min));
+      // (split s takes every S-th stage: at least 4 each)
+      S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nst_min / 4));
+      if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, nst_min));
+      // rows of F per w unit: the largest chunk that still gives ~2 units per CU (w
+      // is latency-bound per unit: one round trip per 128 rows)
+      int64_t wch = LAT_WCH_MIN;
+      for (int64_t t = LAT_WCH_MAX; t > LAT_WCH_MIN; t /= 2) {
+        int64_t units = 0;
+        for (int i = 0; i < ninc; ++i) units += lat_wunits(hd[i].n0, t);
+        if (units >= 2 * c->ncu) {
+          wch = t;
+          break;
+        }
+      }
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
         const int64_t tiles = lat_tiles(m, ka);
-        if ((rc = ensure_lat(m, tiles, S))) return rc;
+        const int64_t nzu = lat_nzu(m);
+        if ((rc = ensure_lat(m, tiles, S, ka, nzu))) return rc;
         const int bin = res_find(m, fd.n0);
         fd.rmu_in = res_mu(m, bin);
         fd.rvar_in = res_var(m, bin);
@@ -1703,10 +1790,21 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.ksplit = S;
         fd.lat_tiles = (int)tiles;
         fd.nwb = (int)((fd.n0 + 63) / 64);
-        fd.nwu = (int)lat_wunits(fd.n0);
+        fd.wch = wch;
+        fd.nwu = (int)lat_wunits(fd.n0, wch);
         fd.wpart = m->wpart;
         fd.wcnt = m->wcnt;
         fd.lat_fbuild = (m->F_gen == m->gen && m->F_n >= fd.n0) ? 0 : 1;
+        fd.lidx = m->lidx;
+        fd.axt = m->axt;
+        fd.zb = m->zb;
+        fd.zrows = m->zb_rows;
+        fd.zflag = m->zflag;
+        fd.ldone = m->ldone;
+        fd.zvl = m->zvl;
+        fd.nzu = (int)nzu;
+        fd.zq = lat_zq(m);
+        fd.lat_axbuild = m->axt_gen == m->gen ? 0 : 1;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }
     }
@@ -1766,6 +1864,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         m->F_gen = m->gen;
         m->tab_n = m->v_n;
         m->tab_gen = m->gen;
+        m->axt_gen = m->gen;
       }
     }
   }

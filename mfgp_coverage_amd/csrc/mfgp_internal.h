@@ -99,7 +99,9 @@ struct GPDesc {
   int rsplit;          // one-pass predict: row splits per cell group (1, 2, 4; 128 / rsplit cells per workgroup)
   int vf32;            // 1 = the resident V is Vf (fp32; the one-pass predict streams 256 cells per workgroup)
   // lattice-separable step (k_inc_lat, mfgp_lattice.inl)
-  double* F;           // explicit L^-1, [ld][ld] ROW-major (F[i][j] at i * ld + j): lower triangle, zeros above
+  double* F;           // explicit L^-1, lower triangle in 64-column blocks: block jb holds rows
+                       // [64 jb, ld) x 64 columns contiguously (F[i][j] at fblk_off(j / 64, ld) +
+                       // (i - 64 (j / 64)) * 64 + j % 64); zeros above the diagonal
   double* tab;         // separable tables [4][ld][tabw]: c_L(j) ex_L, ey_L, c_H(j) ex_H, ey_H per training row j
   double* wv;          // w = L11^-T L21^T, [ld][KINC] (row j: w[j][0..KINC))
   unsigned* wflag;     // per 64-row block of w: the epoch of the launch that stored it
@@ -116,22 +118,42 @@ struct GPDesc {
   int lat_tiles;       // GEMM tiles per GP: ceil(nx / (64 / ka)) * ceil(ny / 64)
   int nwb;             // 64-row blocks of w: ceil(n0 / 64)
   int lat_fbuild;      // k_trinv_f: 1 = compute F for the n0 factor rows
-  int nwu;             // w work units: 64-column blocks x LAT_WCH-row chunks (lat_wunits(n0))
+  int nwu;             // w work units: 64-column blocks x wch-row chunks (lat_wunits(n0, wch))
+  int64_t wch;         // rows of F per w unit
   double* wpart;       // the units' partial w blocks [nwu][16 x 64]
   unsigned* wcnt;      // per 64-row block of w: arrivals of its units (zero between launches)
+  // lattice-axis form of the step (every term on the lattice's own axis values)
+  double* axt;         // axis tables [4][tabw + 1][tabw]: exp(-(a_p - a_col)^2 / 2 l^2) of the grid's
+                       // axis values, x then y, L then H lengthscale; row tabw: zeros
+  int* lidx;           // per training row: its lattice indices px | (py << 16), or -1 off the lattice
+  double* zb;          // Z rows [P][zrows][tabw][ka]: per part and lattice y-row q (then per
+                       // off-lattice "virtual" row), sum over the rows j on it of w[j][a] c_j ex_j(ix)
+  int64_t zrows;       // Z rows per part: round_up(ny, ZKS) + ld (room for every row off the lattice)
+  unsigned* zflag;     // per Z unit: the epoch once its rows are stored
+  unsigned* ldone;     // [4]: w blocks stored (arrivals, zero between launches) | epoch once all are |
+                       // Z units stored (arrivals) | epoch once all are
+  int* zvl;            // per part [zrows + 1]: the count of virtual rows, then their training rows
+  int nzu;             // Z units per GP: parts x ceil(ny / zq)
+  int zq;              // lattice y-rows per Z unit (2 NT / tabw)
+  int lat_axbuild;     // k_lat_axes: 1 = build axt (new grid or hyperparameters)
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
 
-// lattice step: w is computed in units of 64 columns x LAT_WCH rows of F's lower
-// triangle (column block jb: rows [64 jb, n0) in chunks), top block first
-constexpr int64_t LAT_WCH = 1024;
-inline __host__ __device__ int64_t lat_wunits_block(int64_t n0, int64_t jb) {
-  return (n0 - 64 * jb + LAT_WCH - 1) / LAT_WCH;
+// lattice step: w is computed in units of 64 columns x wch rows of F's lower
+// triangle (column block jb: rows [64 jb, n0) in chunks), top block first; wch is
+// one of LAT_WCH_MIN .. LAT_WCH_MAX (powers of two), chosen per launch by the host
+constexpr int64_t LAT_WCH_MIN = 256, LAT_WCH_MAX = 1024;
+constexpr int ZKS = 8;   // lattice-axis GEMM: K rows per pipeline stage (Z / axis-table rows)
+// F's column block jb starts at fblk_off(jb, ld): blocks b < jb hold ld - 64 b rows of 64
+inline __host__ __device__ int64_t fblk_off(int64_t jb, int64_t ld) { return 64 * jb * ld - 2048 * jb * (jb - 1); }
+inline __host__ __device__ int64_t fblk_size(int64_t ld) { return fblk_off(ld / 64, ld); }
+inline __host__ __device__ int64_t lat_wunits_block(int64_t n0, int64_t jb, int64_t wch) {
+  return (n0 - 64 * jb + wch - 1) / wch;
 }
-inline __host__ __device__ int64_t lat_wunits(int64_t n0) {
+inline __host__ __device__ int64_t lat_wunits(int64_t n0, int64_t wch) {
   int64_t u = 0;
-  for (int64_t jb = 0; jb * 64 < n0; ++jb) u += lat_wunits_block(n0, jb);
+  for (int64_t jb = 0; jb * 64 < n0; ++jb) u += lat_wunits_block(n0, jb, wch);
   return u;
 }
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
@@ -167,8 +189,10 @@ hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStre
 // lattice-separable append + predict (k_inc_lat); max_blocks = max over GPs of
 // nprod + nwu + lat_tiles * ksplit
 hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
-// separable tables of rows [tab_lo, n0); max_rows = max over GPs of n0 - tab_lo
+// separable tables and lattice indices of rows [tab_lo, n0); max_rows = max over GPs of n0 - tab_lo
 hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s);
+// axis tables (GPs with lat_axbuild); max_tabw = max over GPs of tabw
+hipError_t launch_lat_axes(const GPDesc* d, int count, int64_t max_tabw, hipStream_t s);
 // F = L^-1 of the n0 factor rows (block column per workgroup); max_nbr = max nblocks_rows(n0)
 hipError_t launch_trinv_f(const GPDesc* d, int count, int64_t max_nbr, hipStream_t s);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s);

@@ -2530,6 +2530,10 @@ hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka
   else hipLaunchKernelGGL((k_inc_lat<16, double>), g, dim3(NT), 0, s, d);
   return hipGetLastError();
 }
+hipError_t launch_lat_axes(const GPDesc* d, int count, int64_t max_tabw, hipStream_t s) {
+  hipLaunchKernelGGL(k_lat_axes, dim3((unsigned)((4 * (max_tabw + 1) + 3) / 4), count), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
 hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s) {
   if (max_rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_lat_tables, dim3((unsigned)((max_rows + 3) / 4), count), dim3(NT), 0, s, d);

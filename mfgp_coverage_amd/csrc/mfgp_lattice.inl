@@ -29,7 +29,7 @@
 //
 // One launch per batch, grid (GPs, roles); per GP the roles are
 //   [0, nprod)                 producers + finish, exactly as k_inc_stream's
-//   [nprod, nprod + nwu)       w units (64 rows of w x LAT_WCH rows of F, top
+//   [nprod, nprod + nwu)       w units (64 rows of w x wch rows of F, top
 //                              block first): wait for the compact rows of their
 //                              rows, then w[j][a] = sum_{i >= j} F[i][j] L21c[i][a]
 //                              on MFMA; the block's last unit adds the chunks,
@@ -62,39 +62,6 @@ static_assert(LAT_LDS >= FIN_LDS, "the ring also holds the finish's LDS image");
 static_assert(LNST > 3 || LAT_LDS + 16 <= 5120, "four workgroups per CU (40 KB of LDS each)");
 constexpr int LAT_PART = 4 * 32 * 64;     // doubles of one split-K partial tile (4 waves x 32 acc x 64 lanes)
 
-// The term blocks of split sp of S: every S-th block from the top (jb = nwb - 1
-// - sp - m S, m = 0, 1, ..), so every split starts at the blocks whose w is ready
-// first and all of them move down together as w becomes ready. Blocks jb >= jh
-// have L and H parts (8 stages of 16 rows), blocks below jh the L part only (4).
-__device__ __forceinline__ int64_t lat_nblk(int64_t from, int64_t S) { return from >= 0 ? from / S + 1 : 0; }
-__device__ __forceinline__ void lat_stage(int64_t t, int64_t nwb, int64_t jh, int64_t sp, int64_t S, int64_t& jb,
-                                          int& part, int64_t& j0) {
-  const int64_t top = nwb - 1 - sp;
-  const int64_t nh = top >= jh ? (top - jh) / S + 1 : 0;   // this split's blocks with H parts
-  int64_t m;
-  if (t < 8 * nh) {
-    m = t / 8;
-    part = (int)((t % 8) / 4);
-  } else {
-    t -= 8 * nh;
-    m = nh + t / 4;
-    part = 0;
-  }
-  jb = top - m * S;
-  j0 = 64 * jb + 16 * (t % 4);
-}
-__device__ __forceinline__ int64_t lat_nstages(int64_t nwb, int64_t jh, int64_t sp, int64_t S) {
-  const int64_t top = nwb - 1 - sp;
-  const int64_t nb = lat_nblk(top, S);
-  const int64_t nh = top >= jh ? (top - jh) / S + 1 : 0;
-  return 8 * nh + 4 * (nb - nh);
-}
-__device__ __forceinline__ int64_t lat_jh(const GPDesc& d) {
-  const int64_t nwb = d.nwb;
-  if (d.hp.kind == 0) return nwb;
-  return d.NL / 64 < nwb ? d.NL / 64 : nwb;
-}
-
 // Separable table entry (t: 0 = c_L ex_L, 1 = ey_L, 2 = c_H ex_H, 3 = ey_H) of
 // training row `row` at (px, py) for lattice axis index `col`: the factor of
 // psi(cell, row) along one axis, each in the SE kernel's operation order
@@ -115,6 +82,55 @@ __device__ double lat_tab_value(const GPDesc& d, int t, int64_t row, int64_t col
   if (!isx) return e;
   const double c = hterm ? h.sH : (h.kind == 0 ? h.sL : (row < d.NL ? h.rho * h.sL : h.rho2 * h.sL));
   return c * e;
+}
+
+// Axis table entry (t as lat_tab_value, no coefficient) of lattice axis value p
+// against axis column col: the factor lat_tab_value gives a training row whose
+// coordinate is that axis value, bit for bit (same operations, same operands).
+__device__ double lat_axis_value(const GPDesc& d, int t, int64_t p, int64_t col) {
+#pragma clang fp contract(off)
+  const Hyp& h = d.hp;
+  const GridLattice& L = d.lat;
+  const bool isx = (t & 1) == 0;
+  const int64_t n = isx ? L.nx : L.ny;
+  if (col >= n || p >= n) return 0.0;
+  if (t >= 2 && h.kind == 0) return 0.0;
+  const double l = t >= 2 ? h.lH : h.lL;
+  const double ax = isx ? d.grid[2 * (col * L.sx)] : d.grid[2 * (col * L.sy) + 1];
+  const double ap = isx ? d.grid[2 * (p * L.sx)] : d.grid[2 * (p * L.sy) + 1];
+  const double dx = div_(ax, l) - div_(ap, l);
+  return exp(-0.5 * (dx * dx));
+}
+
+// Lattice indices of a point: px | (py << 16) when both coordinates are axis
+// values (exact equality; the rounded estimate and its neighbours), else -1.
+__device__ int lattice_xy(const GPDesc& d, double px, double py) {
+  const GridLattice& L = d.lat;
+  if (L.nx <= 0 || !(px == px) || !(py == py)) return -1;
+  const int ex = (int)rint(fmin(fmax((px - L.x0) * L.xinv, 0.0), (double)(L.nx - 1)));
+  const int ey = (int)rint(fmin(fmax((py - L.y0) * L.yinv, 0.0), (double)(L.ny - 1)));
+  int hx = -1, hy = -1;
+  for (int t = -1; t <= 1; ++t) {
+    const int cx = ex + t, cy = ey + t;
+    if (cx >= 0 && cx < L.nx && d.grid[2 * (cx * L.sx)] == px) hx = cx;
+    if (cy >= 0 && cy < L.ny && d.grid[2 * (cy * L.sy) + 1] == py) hy = cy;
+  }
+  return (hx >= 0 && hy >= 0) ? (hx | (hy << 16)) : -1;
+}
+
+// Phase hand-off: every unit of a phase counts its arrival (relaxed fetch_add,
+// after draining its stores); the last of the n resets the count for the next
+// launch and raises the phase flag (c[1] = epoch). Waiters poll that one word.
+__device__ __forceinline__ void arrive_phase(unsigned* c, unsigned epoch, int64_t n) {
+  const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == (unsigned)(n - 1)) {
+    __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    publish(c + 1, epoch);
+  }
+}
+// Wait (thread 0 polls, the workgroup joins at the barrier) for a phase flag.
+__device__ __forceinline__ void wait_phase(const GPDesc& d, const unsigned* c, unsigned epoch) {
+  wait_flag(d, c + 1, epoch);
 }
 
 // Rows [lo, n0) of the compact rows are stored: every producer chunk from lo / FCH
@@ -157,17 +173,17 @@ __device__ __forceinline__ double l21c_at(const double* l21c, int64_t i, int a) 
   else return (double)gp(reinterpret_cast<const float*>(l21c))[i * KINC + a];
 }
 
-// w unit u (in role order: column blocks from the top, chunks of LAT_WCH rows
+// w unit u (in role order: column blocks from the top, chunks of wch rows
 // within a block): its block jb, chunk c, the block's first unit u0 and units nc.
-__device__ __forceinline__ void lat_wunit(int64_t n0, int64_t nwb, int64_t u, int64_t& jb, int64_t& c,
-                                          int64_t& u0, int64_t& nc) {
+__device__ __forceinline__ void lat_wunit(int64_t n0, int64_t nwb, int64_t wch, int64_t u, int64_t& jb,
+                                          int64_t& c, int64_t& u0, int64_t& nc) {
   u0 = 0;
   for (jb = nwb - 1; jb > 0; --jb) {
-    nc = lat_wunits_block(n0, jb);
+    nc = lat_wunits_block(n0, jb, wch);
     if (u < u0 + nc) break;
     u0 += nc;
   }
-  nc = lat_wunits_block(n0, jb);
+  nc = lat_wunits_block(n0, jb, wch);
   c = u - u0;
 }
 
@@ -211,9 +227,10 @@ template <class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
   const int64_t n0 = d.n0, ld = d.ld;
   int64_t jb, c, u0, nc;
-  lat_wunit(n0, d.nwb, u, jb, c, u0, nc);
-  const int64_t i_lo = 64 * jb + LAT_WCH * c;
-  const int64_t i_hi = i_lo + LAT_WCH < n0 ? i_lo + LAT_WCH : n0;
+  const int64_t wch = d.wch;
+  lat_wunit(n0, d.nwb, wch, u, jb, c, u0, nc);
+  const int64_t i_lo = 64 * jb + wch * c;
+  const int64_t i_hi = i_lo + wch < n0 ? i_lo + wch : n0;
   const double* const l21c = d.l21c;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -235,9 +252,15 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     // the w flags, which follow the drain below)
     stx<true>(&d.tab[t * tstride + (n0 + a) * tabw + col], lat_tab_value(d, t, n0 + a, col, p[0], p[1]));
   }
+  // the new rows' lattice indices (read from the next launch on)
+  if (u == 0 && tid < k) {
+    const double* p = row_pt(d, n0 + tid);
+    d.lidx[n0 + tid] = lattice_xy(d, p[0], p[1]);
+  }
   wait_l21_from(d, i_lo);
   WTRACE(1);
-  const GLOBAL double* Fr = gp(d.F) + 64 * jb + r;   // F[i][64 jb + 16 cb + r] at Fr[i * ld + 16 cb]
+  // F[i][64 jb + 16 cb + r] at Fr[(i - 64 jb) * 64 + 16 cb]: the block's rows are contiguous
+  const GLOBAL double* Fr = gp(d.F) + fblk_off(jb, ld) + r;
   d4 acc[4];
 #pragma unroll
   for (int x = 0; x < 4; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
@@ -251,7 +274,7 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       const int64_t ii = i < i_hi ? i : i_lo;
       // F is read once per step and would evict the GEMM tiles' tables from L2
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) f[x][cb] = __builtin_nontemporal_load(Fr + ii * ld + 16 * cb);
+      for (int cb = 0; cb < 4; ++cb) f[x][cb] = __builtin_nontemporal_load(Fr + (ii - 64 * jb) * 64 + 16 * cb);
       a[x] = l21c_at<VT>(l21c, ii, r);
     }
 #pragma unroll
@@ -308,18 +331,33 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     }
     __syncthreads();
     if (!wlast) return;
+    // every chunk's partial, 4 chunks' loads in flight at a time, added in chunk order
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t c0 = 0; c0 < nc; c0 += 4) {
+      double x[4][4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          x[cc][m] = c0 + cc < nc ? ldx<true>(d.wpart + (u0 + c0 + cc) * 1024 + tid + NT * m) : 0.0;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) t[m] += x[cc][m];
+    }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int e = tid + NT * m;
-      double t = 0.0;
-      for (int64_t cc = 0; cc < nc; ++cc) t += ldx<true>(d.wpart + (u0 + cc) * 1024 + e);
-      stx<true>(&wv[64 * jb * KINC + e], t);
-      Wb[e] = t;
+      stx<true>(&wv[64 * jb * KINC + e], t[m]);
+      Wb[e] = t[m];
     }
   }
   drain_stores();
   __syncthreads();
-  if (tid == 0) publish(d.wflag + jb, d.epoch);
+  if (tid == 0) {
+    publish(d.wflag + jb, d.epoch);
+    arrive_phase(d.ldone, d.epoch, d.nwb);
+  }
   WTRACE(2);
   // F's new rows for this block: F[n0 + a][j] = -sum_{b <= a} L22^-1[a][b] w[j][b]
   wait_flag(d, d.sync + 2, d.epoch);
@@ -330,50 +368,272 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     if (j >= n0) continue;
     double t = 0.0;
     for (int b = 0; b <= a; ++b) t -= Li[a * KINC + b] * Wb[jl * KINC + b];
-    d.F[(n0 + a) * ld + j] = t;   // F row-major
+    d.F[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + jl] = t;
   }
   if (jb == d.nwb - 1)
     for (int e = tid; e < k * k; e += NT) {
       const int a = e / k, b = e % k;
-      if (b <= a) d.F[(n0 + a) * ld + n0 + b] = Li[a * KINC + b];
+      const int64_t j = n0 + b, jb2 = j / 64;
+      if (b <= a) d.F[fblk_off(jb2, ld) + (n0 + a - 64 * jb2) * 64 + j % 64] = Li[a * KINC + b];
     }
 }
 
-// Geometry of one GEMM tile, and its buffer-descriptor LDS-DMA plan (as
-// k_predict's: the lane part of each source offset is a VGPR fixed for the
-// kernel, the row part an SGPR).
-struct LatGeo {
-  __amdgpu_buffer_rsrc_t rtab, rw;   // the four tables; w
-  int64_t tstride, tabw;
-  int64_t nwb, jh, sp, S;
-  int64_t ix0, iy0;
-  unsigned vB, vW, vX;               // lane byte offsets: Bs, Ws, Xs
-};
-
-// Issue the DMAs of stage st into `slot` (waves 1..3; wave 0 only loads the w
-// flags, so its vmcnt never waits for a flag's memory round trip behind a table
-// load, nor theirs for a flag): Bs = 16 Ey rows x 64 iy (8 two-row DMAs, waves
-// 1 and 2, swizzled as swz), Ws = 16 w rows and Xs = 16 Ex rows x 16 ix (wave 3,
-// two 8-row DMAs each).
-__device__ __forceinline__ void lat_issue(const LatGeo& G, int64_t st, double* slot, int w) {
-  int64_t jb, j0;
-  int part;
-  lat_stage(st, G.nwb, G.jh, G.sp, G.S, jb, part, j0);
-  const int64_t tx = (2 * part) * G.tstride, ty = tx + G.tstride;
-  if (w < 3) {
-    const int p0 = 4 * (w - 1);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int p = p0 + u;
-      dma_buf(G.rtab, slot + 2 * p * 64, G.vB, (unsigned)(8 * (ty + (j0 + 2 * p) * G.tabw + G.iy0)));
-    }
-  } else {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      dma_buf(G.rw, slot + LBS + 8 * h * KINC, G.vW, (unsigned)(8 * (j0 + 8 * h) * KINC));
-      dma_buf(G.rtab, slot + LBS + LWS + 8 * h * 16, G.vX, (unsigned)(8 * (tx + (j0 + 8 * h) * G.tabw + G.ix0)));
+// Wait (wave 0 polls, the workgroup joins at the barrier) until flags f[0, n)
+// all hold the epoch; bounded like wait_flag.
+__device__ void wait_flags_all(const GPDesc& d, const unsigned* f, int64_t n, unsigned epoch) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int it = 0;
+    while (true) {
+      bool mine = true;
+      for (int64_t i = lane; i < n; i += 64)
+        mine = mine && __hip_atomic_load(f + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (__ballot(!mine) == 0) break;
+      __builtin_amdgcn_s_sleep(MFGP_SPIN_SLEEP);
+      if (++it == (1 << 22)) {
+        if (lane == 0) atomicMin(d.status, SYNC_FAIL);
+        break;
+      }
     }
   }
+  __syncthreads();
+}
+
+// Exclusive prefix over the workgroup of NV per-thread counts (in thread order),
+// and the totals. scr: 4 * NV ints of LDS.
+template <int NV>
+__device__ __forceinline__ void block_scan(int (&v)[NV], int (&tot)[NV], int* scr) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int inc[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) inc[i] = v[i];
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int o = __shfl_up(inc[i], off);
+      if (lane >= off) inc[i] += o;
+    }
+  __syncthreads();   // scr is free
+  if (lane == 63)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) scr[w * NV + i] = inc[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    int before = 0, all = 0;
+#pragma unroll
+    for (int ww = 0; ww < NT / 64; ++ww) {
+      const int x = scr[ww * NV + i];
+      before += ww < w ? x : 0;
+      all += x;
+    }
+    v[i] = before + inc[i] - v[i];
+    tot[i] = all;
+  }
+}
+
+// One Z unit: part `part`, lattice y-rows q in [c zq, c zq + zq) (zq = 2 NT /
+// tabw), and every virtual (off-lattice) row v of the part with v % units == c.
+// Rows j of the part on the lattice at (px, py):
+//   Z[part][py][ix][a] = sum_j w[j][a] c_j ex(px, ix)          (axis table ex)
+// and a virtual row j: Z[part][zq8 + v][ix][a] = w[j][a] (c_j ex_j(ix)) (its own
+// table row). Thread (ql, ix) owns rows q = c zq + ql and c zq + zq / 2 + ql,
+// column ix, all a. Rows are scanned in batches of ZR NT in row order (members
+// bucketed by row q, stable), so each sum runs in row order. The axis-table
+// loads of the first members go out before the wait for w. Ends with the rows
+// stored (write-through, drain) and zflag[zu] = epoch.
+constexpr int ZR = 8;      // rows per thread per scan batch
+template <int KA>
+__device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* sm) {
+  constexpr int ZMB = KA == 8 ? 14 : 6;   // members per row q per load batch
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Hyp& h = d.hp;
+  const int P = h.kind == 0 ? 1 : 2;
+  const int64_t tabw = d.tabw;   // 64, 128 or 256 (host)
+  const int ZQ = d.zq;           // 2 NT / tabw (<= 8)
+  const int ZH = ZQ / 2;         // rows q per thread group
+  const int64_t nu = d.nzu / P;
+  const int part = (int)(zu / nu);
+  const int64_t c = zu % nu;
+  const int64_t ny = d.lat.ny;
+  const int64_t n0 = d.n0, NL = d.NL;
+  const int64_t j_lo = part == 1 ? NL : 0;
+  const int ql = __builtin_amdgcn_readfirstlane((int)(tid / tabw));
+  const int64_t ix = tid % tabw;
+  const int64_t zq8 = (ny + ZKS - 1) / ZKS * ZKS;
+  const int64_t zrows = d.zrows, tstride = d.ld * tabw;
+  const unsigned epoch = d.epoch;
+  const double* const wv = d.wv;
+  const int* const lidx = d.lidx;
+  double* const zb = d.zb;
+  int* const zvl = d.zvl + part * (zrows + 1);
+  const double* const axr = d.axt + (2 * part) * (tabw + 1) * tabw + ix;   // ex(p, ix) at axr[p * tabw]
+  const double cL = h.kind == 0 ? h.sL : h.rho * h.sL, cLH = h.rho2 * h.sL;
+  auto coef = [&](int64_t j) { return part == 1 ? h.sH : (j < NL ? cL : cLH); };
+  // LDS: members [2048] (row), their px [2048], this unit's virtual rows [2048],
+  // the waves' coefficient batches [4][2][ZMB][KA], scan scratch
+  int* const mrow = reinterpret_cast<int*>(sm);
+  int* const mpx = mrow + ZR * NT;
+  int* const vrow = mpx + ZR * NT;
+  double* const cw = sm + 3 * ZR * NT / 2 + w * 2 * ZMB * KA;
+  int* const scr = reinterpret_cast<int*>(sm + 3 * ZR * NT / 2 + 4 * 2 * ZMB * KA);
+  static_assert(3 * ZR * NT / 2 + 4 * 2 * ZMB * KA + 24 <= LAT_LDS, "the Z unit's LDS fits");
+  WTRACE(0);
+  double acc[2][KA];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int a = 0; a < KA; ++a) acc[hh][a] = 0.0;
+  int64_t vbase = 0;   // virtual rows of the part before this batch
+  bool waited = false;
+  auto wait_w = [&]() {
+    if (!waited) {
+      WTRACE(1);
+      wait_phase(d, d.ldone, epoch);   // w of every block
+      WTRACE(3);
+      waited = true;
+    }
+  };
+  for (int64_t b0 = j_lo; b0 < n0; b0 += ZR * NT) {
+    // per-thread counts of members of rows c zq + 0..7 (4-bit fields: <= ZR each)
+    // and of virtual rows; no dynamically indexed arrays (they would live in scratch)
+    int li[ZR];
+    unsigned pk = 0;
+    int nvirt = 0;
+#pragma unroll
+    for (int e = 0; e < ZR; ++e) {
+      const int64_t j = b0 + (int64_t)tid * ZR + e;
+      li[e] = j < n0 ? lidx[j] : -2;
+      if (li[e] >= 0) {
+        const int64_t b = (int64_t)(li[e] >> 16) - c * ZQ;
+        if (b >= 0 && b < ZQ) pk += 1u << (4 * b);
+      } else if (li[e] == -1) {
+        nvirt += 1;
+      }
+    }
+    int cnt[9], tot[9];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) cnt[b] = (int)((pk >> (4 * b)) & 15u);
+    cnt[8] = nvirt;
+    block_scan<9>(cnt, tot, scr);
+    int base[8];
+    base[0] = 0;
+#pragma unroll
+    for (int b = 1; b < 8; ++b) base[b] = base[b - 1] + tot[b - 1];
+    // this unit's first virtual row at or after vbase
+    const int64_t vfirst = vbase + ((c - vbase % nu) % nu + nu) % nu;
+    unsigned run = 0;   // members placed so far per bucket (4-bit fields)
+    int vrun = 0;
+#pragma unroll
+    for (int e = 0; e < ZR; ++e) {
+      const int64_t j = b0 + (int64_t)tid * ZR + e;
+      if (li[e] >= 0) {
+        const int64_t b = (int64_t)(li[e] >> 16) - c * ZQ;
+        if (b >= 0 && b < ZQ) {
+          int pos = 0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (i == b) pos = base[i] + cnt[i] + (int)((run >> (4 * i)) & 15u);
+          run += 1u << (4 * b);
+          mrow[pos] = (int)j;
+          mpx[pos] = li[e] & 0xffff;
+        }
+      } else if (li[e] == -1) {
+        const int64_t v = vbase + cnt[8] + vrun++;
+        if (v % nu == c) vrow[(v - vfirst) / nu] = (int)j;
+      }
+    }
+    __syncthreads();
+    // members of this thread group's two rows, ZMB of each at a time: ex(px, ix)
+    // for each (before the first wait for w), the coefficients w[j][a] c_j into the
+    // wave's LDS, then the FMAs (row order)
+    int lo[2] = {0, 0}, nm_all[2] = {0, 0};
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int b = ql + hh * ZH;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (i == b) {
+          lo[hh] = base[i];
+          nm_all[hh] = (c * ZQ + b < ny) ? tot[i] : 0;
+        }
+    }
+    const int mmax = nm_all[0] > nm_all[1] ? nm_all[0] : nm_all[1];
+    double ex[2][ZMB];
+    auto load_ex = [&](int m0) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int m = 0; m < ZMB; ++m)
+          ex[hh][m] = m0 + m < nm_all[hh] ? axr[(int64_t)mpx[lo[hh] + m0 + m] * tabw] : 0.0;
+    };
+    load_ex(0);
+    wait_w();   // every wave (a barrier): members or not
+    for (int m0 = 0; m0 < mmax; m0 += ZMB) {
+      if (m0 > 0) load_ex(m0);
+      for (int e = lane; e < 2 * ZMB * KA; e += 64) {
+        const int hh = e / (ZMB * KA), m = (e / KA) % ZMB, a = e % KA;
+        double v = 0.0;
+        if (m0 + m < nm_all[hh]) {
+          const int64_t j = mrow[lo[hh] + m0 + m];
+          v = wv[j * KINC + a] * coef(j);   // (no line of w is read before its flag)
+        }
+        cw[e] = v;
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int m = 0; m < ZMB; ++m)
+          if (m0 + m < nm_all[hh]) {
+#pragma unroll
+            for (int a = 0; a < KA; ++a) acc[hh][a] += cw[(hh * ZMB + m) * KA + a] * ex[hh][m];
+          }
+    }
+    WTRACE(4);
+    // this unit's virtual rows of the batch: Z row = w[j][a] (c_j ex_j(ix)), group ql == 0
+    const int64_t nvb = tot[8];
+    const int64_t nmine = vfirst < vbase + nvb ? (vbase + nvb - 1 - vfirst) / nu + 1 : 0;
+    if (ql == 0)
+      for (int64_t i = 0; i < nmine; ++i) {
+        const int64_t v = vfirst + i * nu;
+        const int64_t j = vrow[i];
+        const double e = d.tab[(2 * part) * tstride + j * tabw + ix];
+        double* zr = zb + ((part * zrows + zq8 + v) * tabw + ix) * KA;
+#pragma unroll
+        for (int a = 0; a < KA; ++a) stx<true>(zr + a, ldx<true>(&wv[j * KINC + a]) * e);
+        if (ix == 0) __hip_atomic_store(zvl + 1 + v, (int)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    vbase += nvb;
+    __syncthreads();   // the lists are reused by the next batch
+  }
+  // the part's last virtual stage: rows [nv, round_up(nv, ZKS)) are zero (their
+  // table row: the part's first row, any finite row)
+  const int64_t nv = vbase, nv8 = (nv + ZKS - 1) / ZKS * ZKS;
+  if (ql == 0)
+    for (int64_t v = nv + ((c - nv % nu) % nu + nu) % nu; v < nv8; v += nu) {
+      double* zr = zb + ((part * zrows + zq8 + v) * tabw + ix) * KA;
+#pragma unroll
+      for (int a = 0; a < KA; ++a) stx<true>(zr + a, 0.0);
+      if (ix == 0) __hip_atomic_store(zvl + 1 + v, (int)j_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  if (c == 0 && tid == 0) __hip_atomic_store(zvl, (int)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  WTRACE(5);
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int64_t q = c * ZQ + ql + hh * ZH;
+    if (q < ny) {
+      double* zr = zb + ((part * zrows + q) * tabw + ix) * KA;
+#pragma unroll
+      for (int a = 0; a < KA; ++a) stx<true>(zr + a, acc[hh][a]);
+    }
+  }
+  drain_stores();
+  __syncthreads();
+  WTRACE(6);
+  if (tid == 0) arrive_phase(d.ldone + 2, epoch, d.nzu);
+  WTRACE(2);
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n in [0, 4], then the raw barrier (no
@@ -388,50 +648,44 @@ __device__ __forceinline__ void vm_wait_bar(int n) {
   }
 }
 
-// acc += A B over one stage: A[(a, ix)][j] = w[j][a] * Ex[j][ix] (formed from the
-// Ws / Xs rows), B[j][iy] = Ey[j][iy]. Wave w: rows 32 w + 16 m + r (m = 0, 1), all
-// 64 columns (blocks n = 0..3): per 4-row k-step 7 LDS reads, 2 products and 8
-// MFMAs. The reads of two k-steps are issued ahead of their MFMAs.
-template <int KA>
-__device__ __forceinline__ void lat_compute(const double* slot, d4 (&acc)[2][4], int r, int q, int ar, int ixl0,
-                                            int ixl1) {
-  const double* Bs = slot;
-  const double* Ws = slot + LBS;
-  const double* Xs = slot + LBS + LWS;
+// acc += A B over one stage of ZKS = 8 K rows: A[(a, ix)][k] = Z rows (As, [8][128],
+// swizzled by (k & 1) << 4), B[k][iy] = axis-table / table rows (Bs, [8][64], swz).
+// Wave w: rows 32 w + 16 m + r (m = 0, 1), all 64 columns: per 4-row k-step 6 LDS
+// reads and 8 MFMAs, the reads of both k-steps ahead of the MFMAs.
+__device__ __forceinline__ void lat_zcompute(const double* slot, d4 (&acc)[2][4], int w, int r, int q) {
+  const double* As = slot;
+  const double* Bs = slot + ZKS * 128;
+  double a[2][2], b[2][4];
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    double wa[2], x0[2], x1[2], b[2][4];
+  for (int e = 0; e < 2; ++e) {
+    const int k = 4 * e + q;
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = 4 * (2 * hh + e) + q;
-      wa[e] = Ws[j * KINC + ar];
-      x0[e] = Xs[j * 16 + ixl0];
-      x1[e] = Xs[j * 16 + ixl1];
+    for (int m = 0; m < 2; ++m) a[e][m] = As[k * 128 + ((32 * w + 16 * m + r) ^ ((k & 1) << 4))];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) b[e][n] = Bs[swz(j, 16 * n + r)];
-    }
-    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
+    for (int n = 0; n < 4; ++n) b[e][n] = Bs[swz(k, 16 * n + r)];
+  }
+  __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const double a0 = wa[e] * x0[e];
-      const double a1 = wa[e] * x1[e];
+  for (int e = 0; e < 2; ++e) {
 #ifdef MFGP_DIAG_LATNOMMA   // diagnostic build: the loop without its MFMAs (timing only)
-      acc[0][0][0] += a0 + b[e][0];
-      acc[1][1][0] += a1 + b[e][1];
-      continue;
+    acc[0][0][0] += a[e][0] + b[e][0];
+    acc[1][1][0] += a[e][1] + b[e][1];
+    continue;
 #endif
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        acc[0][n] = mfma(a0, b[e][n], acc[0][n]);
-        acc[1][n] = mfma(a1, b[e][n], acc[1][n]);
-      }
+    for (int n = 0; n < 4; ++n) {
+      acc[0][n] = mfma(a[e][0], b[e][n], acc[0][n]);
+      acc[1][n] = mfma(a[e][1], b[e][n], acc[1][n]);
     }
   }
 }
 
 // One GEMM tile (split s of ksplit): 128 (a, ix) rows x 64 iy columns, i.e.
-// (128 / KA) x 64 cells; and, for the last split to arrive, the cell epilogue,
-// F's new rows for its column blocks and the fused var max / argmax partials.
+// (128 / KA) x 64 cells, over the K rows of both parts: per part the lattice
+// y-rows q < round_up(ny, ZKS) (A = Z rows, B = axis-table rows ey(q, iy)), then
+// the part's virtual rows (A = Z rows, B = the row's own table row ey_j(iy)).
+// Split s takes stages s, s + S, ... For the last split to arrive: the cell
+// epilogue and the fused var max / argmax partials.
 template <int KA, class VT>
 __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t s, double* sm) {
   constexpr int IXPT = 128 / KA;   // lattice columns x per tile
@@ -442,84 +696,67 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   const int64_t ntiy = (lat.ny + 63) / 64;
   const int64_t tix = tile / ntiy, tiy = tile % ntiy;
   const int S = d.ksplit;
-  LatGeo G;
-  G.tabw = d.tabw;
-  G.tstride = d.ld * d.tabw;
-  G.rtab = make_rsrc(d.tab, (int64_t)8 * 4 * G.tstride);
-  G.rw = make_rsrc(d.wv, (int64_t)8 * d.ld * KINC);
-  G.vB = (unsigned)(8 * ((lane >> 5) * G.tabw + (((lane & 31) * 2) ^ ((lane >> 5) << 4))));
-  G.vW = (unsigned)(8 * ((lane >> 3) * KINC + 2 * (lane & 7)));
-  G.vX = (unsigned)(8 * ((lane >> 3) * G.tabw + 2 * (lane & 7)));
-  G.nwb = d.nwb;
-  G.jh = lat_jh(d);
-  G.ix0 = tix * IXPT;
-  G.iy0 = tiy * 64;
-  G.sp = s;
-  G.S = S;
-  const int64_t lo = 0, hi = lat_nstages(G.nwb, G.jh, s, S);
+  const int64_t tabw = d.tabw, zrows = d.zrows, tstride = d.ld * tabw;
+  const int64_t ix0 = tix * IXPT, iy0 = tiy * 64;
+  const int P = d.hp.kind == 0 ? 1 : 2;
+  const int64_t zq8 = (lat.ny + ZKS - 1) / ZKS * ZKS;
+  const unsigned epoch = d.epoch;
   WTRACE(0);
-  // this lane's A rows: a = row % KA, lattice column ixl = row / KA (rows 32 w + 16 m + r)
-  const int ar = KA == 8 ? (r & 7) : r;
-  const int ixl0 = KA == 8 ? 4 * w + (r >> 3) : 2 * w;
-  const int ixl1 = KA == 8 ? 4 * w + 2 + (r >> 3) : 2 * w + 1;
+  // every Z unit of the GP (they waited for all of w) -- one wait, then no flags
+  wait_phase(d, d.ldone + 2, epoch);
+  WTRACE(1);
+  // stages per part: the axis rows, then the virtual rows (counts from the Z units)
+  const int* const zvl = d.zvl;
+  int64_t nsp[2] = {0, 0};
+  for (int pt = 0; pt < P; ++pt) {
+    const int64_t nv = __hip_atomic_load(zvl + pt * (zrows + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nsp[pt] = (zq8 + (nv + ZKS - 1) / ZKS * ZKS) / ZKS;
+  }
+  const int64_t NS = nsp[0] + nsp[1];
+  const int64_t hi = s < NS ? (NS - s + S - 1) / S : 0;   // this split's stages
+  const __amdgpu_buffer_rsrc_t rZ = make_rsrc(d.zb, (int64_t)8 * P * zrows * tabw * KA);
+  const __amdgpu_buffer_rsrc_t rAx = make_rsrc(d.axt, (int64_t)8 * 4 * (tabw + 1) * tabw);
+  const __amdgpu_buffer_rsrc_t rTab = make_rsrc(d.tab, (int64_t)8 * 4 * tstride);
+  // lane byte offsets: A rows 2 w + h (swizzle by row parity h), B row pair w
+  const unsigned vA0 = (unsigned)(8 * (2 * lane)), vA1 = (unsigned)(8 * ((2 * lane) ^ 16));
+  const unsigned vBc = (unsigned)(8 * (((lane & 31) * 2) ^ ((lane >> 5) << 4)));
+  const unsigned vB = vBc + (unsigned)(8 * (lane >> 5) * tabw);
+  auto issue = [&](int64_t t) {   // stage t's DMAs: 3 per wave
+    const int64_t g = s + t * S;
+    const int pt = g < nsp[0] ? 0 : 1;
+    const int64_t q0 = (g - (pt ? nsp[0] : 0)) * ZKS;
+    double* slot = sm + (t % LNST) * LSTG;
+    const int64_t ar = (pt * zrows + q0 + 2 * w) * tabw + ix0;
+    dma_buf(rZ, slot + (2 * w) * 128, vA0, (unsigned)(8 * ar * KA));
+    dma_buf(rZ, slot + (2 * w + 1) * 128, vA1, (unsigned)(8 * (ar + tabw) * KA));
+    double* bdst = slot + ZKS * 128 + 2 * w * 64;
+    if (q0 < zq8) {
+      dma_buf(rAx, bdst, vB, (unsigned)(8 * (((2 * pt + 1) * (tabw + 1) + q0 + 2 * w) * tabw + iy0)));
+    } else {
+      // virtual rows: each half-wave its own training row's table row
+      const int* vl = zvl + pt * (zrows + 1) + 1 + (q0 - zq8) + 2 * w;
+      const int64_t ja = __hip_atomic_load(vl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t jb = __hip_atomic_load(vl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned vv = vBc + (unsigned)(8 * ((lane >> 5) ? jb : ja) * tabw);
+      dma_buf(rTab, bdst, vv, (unsigned)(8 * ((2 * pt + 1) * tstride + iy0)));
+    }
+  };
   d4 acc[2][4];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = d4{0.0, 0.0, 0.0, 0.0};
-  // w's readiness: wave 0 loads the flag word of each stage's block into LDS (an
-  // agent-scope 4-byte LDS-DMA) two iterations before that stage's DMAs are
-  // issued; waves 2 and 3, which stage the w rows, check it there after the
-  // barrier (an LDS read, not a memory round trip) and spin on memory only if it
-  // was not yet set. Wave 0 issues nothing else, so the flags' round trips never
-  // sit in front of a table load in any wave's vmcnt order.
-  // (descriptor fields the loop and the epilogue use, in registers: the raw
-  // barriers' memory clobbers and the global stores would make the compiler reload
-  // them from the descriptor, a scalar-memory round trip each time)
-  const unsigned epoch = d.epoch;
-  const unsigned* const wflag = d.wflag;
-  const int cnt = w == 0 ? 1 : 4;   // vector-memory ops per issued stage
-  unsigned* const fl = reinterpret_cast<unsigned*>(sm + LNST * LSTG);   // [LNST][64]
-  const __amdgpu_buffer_rsrc_t rfl = make_rsrc(reinterpret_cast<const double*>(d.wflag),
-                                               (int64_t)4 * (d.nwb + 1));
-  auto blk = [&](int64_t st) {
-    int64_t jb, j0;
-    int part;
-    lat_stage(st < hi ? st : hi - 1, G.nwb, G.jh, G.sp, G.S, jb, part, j0);
-    return jb;
-  };
-  auto issue = [&](int64_t st, int64_t fst) {   // stage st's DMAs (waves 1..3), flag of stage fst (wave 0)
-    if (w == 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rfl, (lds_vptr)(fl + ((fst - lo) % LNST) * 64), 4, 0u,
-                                               (unsigned)(4 * blk(fst)), 0, 16 /* sc1: agent scope */);
-#ifndef MFGP_DIAG_LATNODMA   // diagnostic build: no table / w DMAs (timing only)
-    else
-      lat_issue(G, st, sm + ((st - lo) % LNST) * LSTG, w);
-#endif
-  };
   constexpr int D = LNST - 1;   // stages in flight ahead of the one consumed
-  static_assert(D * 4 <= 12, "vm_wait_bar covers the outstanding ops");
-#ifdef MFGP_DIAG_LATNOWAIT   // diagnostic build: the GEMM does not wait for w (timing only)
-  auto spin_wave = [](const GPDesc&, const unsigned*, unsigned) {};
-#endif
-  if (lo < hi) {
-    if (w == 3)
-      for (int64_t st = lo; st < lo + D && st < hi; ++st) spin_wave(d, wflag + blk(st), epoch);
-    WTRACE(1);
-    for (int64_t st = lo; st < lo + D && st < hi; ++st) issue(st, st + D);
-    // iteration t: stage t sits in slot (t - lo) % LNST, issued D iterations ago
-    // with the flag of stage t + D, and followed by the ops of the stages after it
-    for (int64_t t = lo; t < hi; ++t) {
-      const int64_t after = (hi - 1 - t) < (D - 1) ? (hi - 1 - t) : (D - 1);
-      vm_wait_bar((int)after * cnt);
-      if (t + D < hi) {
-        if (w == 3 && fl[((t + D - lo) % LNST) * 64] != epoch) spin_wave(d, wflag + blk(t + D), epoch);
-        issue(t + D, t + 2 * D);
-      }
+  constexpr int CNT = 3;        // vector-memory ops per issued stage (every wave)
+  static_assert(D * CNT <= 12, "vm_wait_bar covers the outstanding ops");
+  for (int64_t t = 0; t < D && t < hi; ++t) issue(t);
+  for (int64_t t = 0; t < hi; ++t) {
+    const int64_t after = (hi - 1 - t) < (D - 1) ? (hi - 1 - t) : (D - 1);
+    vm_wait_bar((int)after * CNT);
+    if (t + D < hi) issue(t + D);
 #ifndef MFGP_DIAG_LATNOCOMP   // diagnostic build: the pipeline without its compute (timing only)
-      lat_compute<KA>(sm + ((t - lo) % LNST) * LSTG, acc, r, q, ar, ixl0, ixl1);
+    lat_zcompute(sm + (t % LNST) * LSTG, acc, w, r, q);
 #endif
-    }
   }
   vm_wait_all();
   __syncthreads();
@@ -599,7 +836,7 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
       const int a = rem / FW, col = rem % FW;
       const bool isx = col < IXPT;
       const int t = 2 * kind2 + (isx ? 0 : 1);
-      const int64_t idx = isx ? G.ix0 + col : G.iy0 + (col - IXPT);
+      const int64_t idx = isx ? ix0 + col : iy0 + (col - IXPT);
       Fn[e] = a < k ? d.tab[t * tstride + (n0 + a) * tabw + idx] : 0.0;
     }
   }
@@ -640,8 +877,8 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   constexpr int NPASS = 2 * (4 / NBP);
   auto cell_of = [&](int p, int64_t& ix, int64_t& iy) {
     const int m = p / (4 / NBP), nf = NBP * (p % (4 / NBP));
-    ix = G.ix0 + (KA == 8 ? 4 * cw + 2 * m + ch : 2 * cw + m);
-    iy = G.iy0 + 16 * nf + cyl;
+    ix = ix0 + (KA == 8 ? 4 * cw + 2 * m + ch : 2 * cw + m);
+    iy = iy0 + 16 * nf + cyl;
   };
   auto cell_ok = [&](int64_t ix, int64_t iy) { return cact && ix < lat.nx && iy < lat.ny; };
   // the old posterior of this thread's cell of the next pass, one pass ahead
@@ -678,7 +915,7 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     }
     if (!cell_ok(ix, iy)) continue;
     const int64_t c = ix * lat.sx + iy * lat.sy;
-    const int ixc = (int)(ix - G.ix0), iyc = IXPT + (int)(iy - G.iy0);
+    const int ixc = (int)(ix - ix0), iyc = IXPT + (int)(iy - iy0);
     const double* const Tc = Ts + (cw * 16 + (KA == 8 ? 8 * ch : 0)) * TW + cyl;
     VT* const vt = Vr + (c / PBM) * vld * PBM + (c % PBM);
     double vn[KA];
@@ -735,10 +972,14 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     lat_wblock<VT>(d, role - np, sm);
     return;
   }
-#ifdef MFGP_DIAG_LATNOGEMM   // diagnostic build: producers and w only (timing only)
+  if (role < np + d.nwu + d.nzu) {
+    lat_zunit<KA>(d, role - np - d.nwu, sm);
+    return;
+  }
+#ifdef MFGP_DIAG_LATNOGEMM   // diagnostic build: producers, w and Z only (timing only)
   return;
 #endif
-  const int64_t g = role - np - d.nwu;
+  const int64_t g = role - np - d.nwu - d.nzu;
   if (g >= (int64_t)d.lat_tiles * d.ksplit) return;
   const int64_t tile = g % d.lat_tiles, s = g / d.lat_tiles;
   lat_gemm<KA, VT>(d, tile, s, sm);
@@ -765,5 +1006,24 @@ __global__ __launch_bounds__(NT) void k_lat_tables(const GPDesc* __restrict__ de
     const int64_t col = e % tabw;
     if (row >= hi) continue;
     d.tab[t * tstride + row * tabw + col] = lat_tab_value(d, t, row, col, d.X[2 * row], d.X[2 * row + 1]);
+  }
+  if (threadIdx.x < 4 && r0 + threadIdx.x < hi) {
+    const int64_t row = r0 + threadIdx.x;
+    d.lidx[row] = lattice_xy(d, d.X[2 * row], d.X[2 * row + 1]);
+  }
+}
+
+// The axis tables of GPs with lat_axbuild: axt[t][p][col] for p, col < tabw (row
+// tabw: zeros). Grid (GPs, 4 tables x (tabw + 1) rows / 4 rows per workgroup).
+__global__ __launch_bounds__(NT) void k_lat_axes(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  if (!d.lat_axbuild) return;
+  const int64_t tabw = d.tabw, rows = 4 * (tabw + 1);
+  for (int64_t e = threadIdx.x; e < 4 * tabw; e += NT) {
+    const int64_t rr = 4 * (int64_t)blockIdx.x + e / tabw, col = e % tabw;
+    if (rr >= rows) continue;
+    const int t = (int)(rr / (tabw + 1));
+    const int64_t p = rr % (tabw + 1);
+    d.axt[rr * tabw + col] = p < tabw ? lat_axis_value(d, t, p, col) : 0.0;
   }
 }

@@ -123,9 +123,10 @@ __global__ __launch_bounds__(NT) void k_trinv(const GPDesc* __restrict__ descs, 
 }
 
 // The same for a batch (grid (block columns, GPs)): F = L^-1 of the n0 leading
-// factor rows into each GP's resident F, stored ROW-major (F[i][j] at i * ld + j:
-// the lattice step reads F's rows i over 64 consecutive columns j, one cache line
-// per 16 columns; k_inc_lat then appends its rows).
+// factor rows into each GP's resident F, stored by 64-column blocks, each block's
+// rows contiguous (fblk_off: the lattice step streams a block's rows i >= 64 jb as
+// one contiguous range; k_inc_lat then appends its rows). Within block J the tile
+// X_KJ is a row-major 64 x 64 tile with row stride 64.
 __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs) {
   const GPDesc& d = descs[blockIdx.y];
   const int64_t ld = d.ld, nbr = nblocks_rows(d.n0);
@@ -134,13 +135,14 @@ __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs
   __shared__ double As[TILE], Bs[TILE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int r = lane & 15, q = lane >> 4;
-  double* Xt = d.F;
+  // block J as a row-major matrix of absolute rows, row stride 64
+  double* Xt = d.F + fblk_off(J, ld) - 64 * J * NB;
   for (int64_t I = J; I < nbr; ++I) {
     Acc acc;
     acc_zero(acc);
     for (int64_t K = J; K < I; ++K) {
       load_tile_cm(As, d.A, ld, I * NB, K * NB, tid);          // As[k][i] = L_IK[i][k]
-      load_tile_cm(Bs, Xt, ld, J * NB, K * NB, tid);           // Bs[k][j] = X_KJ[k][j] (row-major X)
+      load_tile_cm(Bs, Xt, NB, 0, K * NB, tid);                // Bs[k][j] = X_KJ[k][j] (row-major block)
       __syncthreads();
       tile_mma<true>(As, Bs, acc, wm, wn, lane);               // acc -= L_IK X_KJ
       __syncthreads();
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int v = 0; v < 4; ++v)
-          Xt[(I * NB + acc_row(wm, mt, q, v)) * ld + J * NB + acc_col(wn, nt, r)] = o.c[mt][nt][v];
+          Xt[(I * NB + acc_row(wm, mt, q, v)) * NB + acc_col(wn, nt, r)] = o.c[mt][nt][v];
     __threadfence_block();
     __syncthreads();
   }

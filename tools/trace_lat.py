@@ -1,6 +1,7 @@
 """Diagnostic: per-workgroup timeline of k_inc_lat (a -DMFGP_STAMPS build, argv[1]).
 Slots: producers 0 start / 1 arrival / 4 end; w blocks 0 start / 1 past the L21 wait / 3 F loop done /
-2 published; GEMM 0 start / 1 past the first w waits / 2 K loop done / 3 past the
+2 published; Z units 0 start / 1 scanned / 3 past the w wait / 2 published; GEMM 0 start / 1 past
+the Z wait / 2 K loop done / 3 past the
 L22 wait (reducers) / 5 new-row factors and L22^-1 done / 6 cells done / 4 end. Launches back to back; the trace is the last launch's."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -52,15 +53,21 @@ t0 = tr[used, 0].min()
 tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)   # us (100 MHz realtime counter)
 nprod, nwb = 16, 32
 import math
-nwu = sum(math.ceil((2040 - 64 * j) / 1024) for j in range(32))
+def _units(t):
+    return sum(math.ceil((2040 - 64 * j) / t) for j in range(32))
+wch = next((t for t in (1024, 512) if B * _units(t) >= 2 * 256), 256)   # the host's rule
+nwu = _units(wch)
+_zq = 2 * 256 // (((G + 63) // 64) * 64)
+nzu = 2 * ((G + _zq - 1) // _zq)
 role = np.arange(NWG) // B
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
-print(f"B={B}: percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
+print(f"B={B} (w chunk {wch}, {nwu} w units, {nzu} Z units per GP): percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
 for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w unit", (role >= nprod) & (role < nprod + nwu), (0, 1, 3, 2)),
-                         ("gemm", (role >= nprod + nwu) & used, (0, 1, 2, 3, 5, 6, 4))):
+                         ("Z unit", (role >= nprod + nwu) & (role < nprod + nwu + nzu), (0, 1, 3, 4, 5, 6, 2)),
+                         ("gemm", (role >= nprod + nwu + nzu) & used, (0, 1, 2, 3, 5, 6, 4))):
     for sl in slots:
         print(f"  {name:9s} slot {sl}: {q(tr[sel, sl])}")
-gm = (role >= nprod + nwu) & used
+gm = (role >= nprod + nwu + nzu) & used
 w = tr[(role >= nprod) & (role < nprod + nwu)]
 print(f"  w units published (slot 2, last arrivers): {q(w[:, 2])}")
 print(f"  w unit F loop (slot 3 - slot 1): {q(w[:, 3] - w[:, 1])}; reduce+publish (2 - 3): {q(w[:, 2] - w[:, 3])}")
@@ -70,7 +77,7 @@ print(f"  reducers: reduce+L22 wait (3 - 2) {q(tr[red, 3] - tr[red, 2])}; Fn/Li 
       f"cells (6 - 5) {q(tr[red, 6] - tr[red, 5])}; argmax (4 - 6) {q(tr[red, 4] - tr[red, 6])}")
 S = int(os.environ.get("MFGP_LAT_KSPLIT", "0")) or None
 if S:
-    g = role - nprod - nwu
+    g = role - nprod - nwu - nzu
     tiles = 16
     for sp in range(S):
         sel = gm & (g // tiles == sp)
