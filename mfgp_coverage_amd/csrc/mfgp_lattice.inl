@@ -257,17 +257,14 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     const double* p = row_pt(d, n0 + tid);
     d.lidx[n0 + tid] = lattice_xy(d, p[0], p[1]);
   }
-  wait_l21_from(d, i_lo);
-  WTRACE(1);
   // F[i][64 jb + 16 cb + r] at Fr[(i - 64 jb) * 64 + 16 cb]: the block's rows are contiguous
   const GLOBAL double* Fr = gp(d.F) + fblk_off(jb, ld) + r;
   d4 acc[4];
 #pragma unroll
   for (int x = 0; x < 4; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
-#ifndef MFGP_DIAG_LATNOW
   constexpr int RG = 8;   // 4-row groups per wave per batch (128 rows per batch)
-  for (int64_t i0 = i_lo + 32 * w; i0 < i_hi; i0 += 128) {
-    double f[RG][4], a[RG];
+  double f[RG][4];
+  auto load_f = [&](int64_t i0) {
 #pragma unroll
     for (int x = 0; x < RG; ++x) {
       const int64_t i = i0 + 4 * x + q;
@@ -275,7 +272,21 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       // F is read once per step and would evict the GEMM tiles' tables from L2
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) f[x][cb] = __builtin_nontemporal_load(Fr + (ii - 64 * jb) * 64 + 16 * cb);
-      a[x] = l21c_at<VT>(l21c, ii, r);
+    }
+  };
+  // (loading the first batch of F before the wait for the compact rows was
+  // tried: f and a live together spill ~85 VGPRs, 144 vs 119 us per launch)
+  const int64_t i_first = i_lo + 32 * w;
+  wait_l21_from(d, i_lo);
+  WTRACE(1);
+#ifndef MFGP_DIAG_LATNOW
+  for (int64_t i0 = i_first; i0 < i_hi; i0 += 128) {
+    load_f(i0);
+    double a[RG];
+#pragma unroll
+    for (int x = 0; x < RG; ++x) {
+      const int64_t i = i0 + 4 * x + q;
+      a[x] = l21c_at<VT>(l21c, i < i_hi ? i : i_lo, r);
     }
 #pragma unroll
     for (int x = 0; x < RG; ++x) {
@@ -446,7 +457,7 @@ __device__ __forceinline__ void block_scan(int (&v)[NV], int (&tot)[NV], int* sc
 constexpr int ZR = 8;      // rows per thread per scan batch
 template <int KA>
 __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* sm) {
-  constexpr int ZMB = KA == 8 ? 14 : 6;   // members per row q per load batch
+  constexpr int ZMB = KA == 8 ? 16 : 6;   // members per row q per load batch
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Hyp& h = d.hp;
@@ -573,14 +584,23 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
     wait_w();   // every wave (a barrier): members or not
     for (int m0 = 0; m0 < mmax; m0 += ZMB) {
       if (m0 > 0) load_ex(m0);
-      for (int e = lane; e < 2 * ZMB * KA; e += 64) {
-        const int hh = e / (ZMB * KA), m = (e / KA) % ZMB, a = e % KA;
-        double v = 0.0;
-        if (m0 + m < nm_all[hh]) {
-          const int64_t j = mrow[lo[hh] + m0 + m];
-          v = wv[j * KINC + a] * coef(j);   // (no line of w is read before its flag)
+      {
+        // all of the batch's coefficient loads in flight, then into LDS
+        constexpr int NE = (2 * ZMB * KA + 63) / 64;
+        double v[NE];
+#pragma unroll
+        for (int i = 0; i < NE; ++i) {
+          const int e = lane + 64 * i;
+          const int hh = e / (ZMB * KA), m = (e / KA) % ZMB, a = e % KA;
+          v[i] = 0.0;
+          if (e < 2 * ZMB * KA && m0 + m < nm_all[hh]) {
+            const int64_t j = mrow[lo[hh] + m0 + m];
+            v[i] = wv[j * KINC + a] * coef(j);   // (no line of w is read before its flag)
+          }
         }
-        cw[e] = v;
+#pragma unroll
+        for (int i = 0; i < NE; ++i)
+          if (lane + 64 * i < 2 * ZMB * KA) cw[lane + 64 * i] = v[i];
       }
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
@@ -620,14 +640,20 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
     }
   if (c == 0 && tid == 0) __hip_atomic_store(zvl, (int)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   WTRACE(5);
+  // the rows through LDS, so that every store instruction writes 512 contiguous
+  // bytes (write-through stores of scattered 8-byte pieces cost ~10 us here)
+  double* const zst = sm;   // [ZH][tabw][KA] (the lists are dead)
+  static_assert(4096 + 16 <= LAT_LDS, "the Z rows' staging fits");
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
-    const int64_t q = c * ZQ + ql + hh * ZH;
-    if (q < ny) {
-      double* zr = zb + ((part * zrows + q) * tabw + ix) * KA;
+    __syncthreads();
 #pragma unroll
-      for (int a = 0; a < KA; ++a) stx<true>(zr + a, acc[hh][a]);
-    }
+    for (int a = 0; a < KA; ++a) zst[(ql * tabw + ix) * KA + a] = acc[hh][a];
+    __syncthreads();
+    const int64_t q0 = c * ZQ + hh * ZH;   // rows q0 .. q0 + ZH - 1, contiguous in zb
+    const int64_t nrow = ny - q0 < ZH ? ny - q0 : ZH;
+    double* const zr = zb + (part * zrows + q0) * tabw * KA;
+    for (int64_t e = tid; e < nrow * tabw * KA; e += NT) stx<true>(zr + e, zst[e]);
   }
   drain_stores();
   __syncthreads();
@@ -767,6 +793,7 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   if (tid == 0)
     l22_seen = __hip_atomic_load(d.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch ? 1u : 0u;
   // split-K: partials through memory, the last split reduces them in split order
+  const double* p0 = d.gpart + tile * S * LAT_PART + (int64_t)w * 32 * 64 + lane;
   if (S > 1) {
     unsigned& lat_last = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 9);
     double* part = d.gpart + (tile * S + s) * LAT_PART + (int64_t)w * 32 * 64 + lane;
@@ -785,23 +812,6 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     }
     __syncthreads();
     if (!lat_last) return;
-    // every split's partial (this one's too) from memory, added in split order
-    // (p0 + p1) + p2 ...: the same bits whichever split arrives last
-    const double* p0 = d.gpart + tile * S * LAT_PART + (int64_t)w * 32 * 64 + lane;
-    for (int s2 = 0; s2 < S; ++s2) {
-      double x[32];
-#pragma unroll
-      for (int e = 0; e < 32; ++e) x[e] = ldx<true>(p0 + s2 * LAT_PART + e * 64);
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const double xv = x[(m * 4 + n) * 4 + v];
-            acc[m][n][v] = s2 == 0 ? xv : acc[m][n][v] + xv;
-          }
-    }
   }
   if (!l22_seen) wait_flag(d, d.sync + 2, epoch);
   WTRACE(3);
@@ -821,28 +831,50 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   static_assert(KINC * KINC + KINC + KINC * KINC + 2 * 8 * (16 + 64) + 4 * 16 * 32 <= LAT_LDS &&
                     KINC * KINC + KINC + KINC * KINC + 2 * 16 * (8 + 64) + 4 * 16 * 16 <= LAT_LDS,
                 "the epilogue's LDS fits the ring's");
-  __syncthreads();   // the ring's last reads are done
   {
-    // plain loads: no line of the record or of the new rows' tables is read in
-    // this launch before sync[2] / the w flags
-    for (int e = tid; e < KINC * KINC + KINC; e += NT) {
-      const double v = d.l22r[e];
-      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
-      L22[e] = use ? v : 0.0;
+    // the record and the new rows' tables (plain loads: no line of them is read in
+    // this launch before sync[2] / the w flags), in flight with the first partial
+    constexpr int NR = (KINC * KINC + KINC + NT - 1) / NT;
+    constexpr int NF = (2 * KA * FW + NT - 1) / NT;
+    double rv[NR], fv[NF];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int e = tid + NT * i;
+      rv[i] = e < KINC * KINC + KINC ? d.l22r[e] : 0.0;
     }
     const int64_t tstride = d.ld * d.tabw, tabw = d.tabw;
-    for (int e = tid; e < 2 * KA * FW; e += NT) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = tid + NT * i;
       const int kind2 = e / (KA * FW), rem = e % (KA * FW);
       const int a = rem / FW, col = rem % FW;
       const bool isx = col < IXPT;
       const int t = 2 * kind2 + (isx ? 0 : 1);
       const int64_t idx = isx ? ix0 + col : iy0 + (col - IXPT);
-      Fn[e] = a < k ? d.tab[t * tstride + (n0 + a) * tabw + idx] : 0.0;
+      fv[i] = (e < 2 * KA * FW && a < k) ? d.tab[t * tstride + (n0 + a) * tabw + idx] : 0.0;
     }
+    if (S > 1) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[m][n][v] = ldx<true>(p0 + ((m * 4 + n) * 4 + v) * 64);
+    }
+    __syncthreads();   // the ring's last reads are done
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int e = tid + NT * i;
+      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+      if (e < KINC * KINC + KINC) L22[e] = use ? rv[i] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+      if (tid + NT * i < 2 * KA * FW) Fn[tid + NT * i] = fv[i];
   }
   __syncthreads();
   if (tid < KINC) {
-    // column c of L22^-1 by forward substitution
+    // column c of L22^-1 by forward substitution (while the partials arrive)
     const int c = tid;
     double x[KINC];
 #pragma unroll
@@ -854,6 +886,20 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
       Li[i * KINC + c] = x[i];
     }
   }
+  // every split's partial (this one's too) from memory, added in split order
+  // (p0 + p1) + p2 ...: the same bits whichever split arrives last
+  for (int s2 = 1; s2 < S; ++s2) {
+    double x[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) x[e] = ldx<true>(p0 + s2 * LAT_PART + e * 64);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[m][n][v] += x[(m * 4 + n) * 4 + v];
+  }
+  __syncthreads();
   WTRACE(5);
   // ---- cells: one pass per (m, group of NBP column blocks); the waves put
   // their blocks' T into Ts (row rho = g + 4 v of block (m, n) is, for KA = 8,
