@@ -325,12 +325,15 @@ def main():
         _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
         varmax = torch.zeros(total, B, dtype=torch.float64, device=dev)
 
+        batch = _lib.Batch(models, ks)
+        xp0, yp0, vp0 = Xnew.data_ptr(), ynew.data_ptr(), varmax.data_ptr()
+        mup, varp = mu.data_ptr(), var.data_ptr()
+
         def step(s):
-            for mdl in models:
-                mdl.truncate(NH0)
+            batch.truncate(NH0)
             # VarMax of every seed (np.amax(cov), simulator.py:1014) fused into the predict epilogue
-            _lib.batch_append_predict(models, Xnew[s].data_ptr(), ynew[s].data_ptr(), ks, mu.data_ptr(),
-                                      var.data_ptr(), asynchronous=True, vmax_ptr=varmax[s].data_ptr())
+            batch.append_predict(xp0 + s * (B * k * 2 * 8), yp0 + s * (B * k * 8), mup, varp, asynchronous=True,
+                                 vmax_ptr=vp0 + s * (B * 8))
 
         def aggregate(traj):
             if backend != "nccl":
@@ -409,14 +412,20 @@ def main():
             vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (3 * k + 1))
         v_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
         v_gbs = vbytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
-        # the lattice-separable step (k_inc_lat): its work is
-        # the GEMM over the separable terms, 2 KA M n_terms flop per GP (KA = 8 rows
-        # of new points, n_terms = n0 + the hifi rows' second term), plus the w pass
-        # over F's lower triangle (MFMA, 16 rows: 16 n0^2 flop) -- f64 MFMA-bound
+        # the lattice step in axis form (k_inc_lat). Bytes: F's
+        # lower triangle read once by the w pass (the dominant stream), the resident
+        # posterior in and out plus the caller's mu / var, the new V rows, the Z rows
+        # written once and read by every 64-column tile row; flops: the w pass (16 n0^2),
+        # the Z sums (2 KA nx n_t) and the K = parts x ny GEMM (2 KA M parts ny8)
         ka = 8 if k <= 8 else 16
-        n_terms = n0 + (n0 - NL)
-        lat_flops = B * (2 * ka * M * n_terms + 16 * n0 * n0)
-        lat_bytes = B * 8 * (n0 * n0 / 2 + M * (k + 4) + n_terms * G * 2 + 3 * n0 * k)
+        parts = 2
+        n_t = n0 + (n0 - NL)
+        ny8 = -(-G // 8) * 8
+        fbytes = 8 * sum((n0 - 64 * jb) * 64 for jb in range(-(-n0 // 64)))
+        zbytes = 8 * parts * ny8 * G * ka * (1 + -(-G // 64))
+        lat_bytes = B * (fbytes + 8 * 6 * M + es * M * k + zbytes)
+        lat_flops = B * (16 * n0 * n0 + 2 * ka * G * n_t + 2 * ka * M * parts * ny8)
+        lat_gbs = lat_bytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
         lat_tf = lat_flops / (v_ms * 1e-3) / 1e12 if v_ms > 0 else float("nan")
         value = world * B * K / elapsed
         # SURVEY.md section 8d's algorithmic cost of one update as the reference
@@ -435,18 +444,17 @@ def main():
             else (None, None)
         if lattice:
             update = ("incremental, lattice-separable, one launch per step (k_inc_lat): bordered-Cholesky append, "
-                      "w = K11^-1 K12 from the resident L^-1, the SE kernel's separability over the grid axes turns "
-                      "L21 V_old into an f64 MFMA GEMM over the training terms (no pass over V), mean / variance "
-                      "updated from the previous posterior")
-            roof = {"bound": "mfma", "achieved": lat_tf, "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
-                    "frac": lat_tf / PEAK_F64_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel": kern, "flops_per_launch": lat_flops, "bytes_per_launch": lat_bytes,
-                    "hbm_gbs": lat_bytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan"),
-                    "avg_launch_ms": v_ms, "launches_timed": tm["predict_launches"],
+                      "w = K11^-1 K12 from the resident L^-1; every training term lies on the grid's lattice, so "
+                      "L21 V_old = sum over lattice rows of Z (w c ex summed per row) times axis-table rows: a "
+                      "K = 2 ny f64 MFMA GEMM, no pass over V; mean / variance updated from the previous posterior")
+            roof = {"bound": "hbm", "achieved": lat_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": lat_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": kern, "bytes_per_launch": lat_bytes, "flops_per_launch": lat_flops,
+                    "mfma_tflops": lat_tf, "avg_launch_ms": v_ms, "launches_timed": tm["predict_launches"],
                     "timing": f"HIP events around every {inc['stride']}th launch of the timed region",
-                    "design_note": f"flops_per_launch = B x (2 KA M n_terms + 16 n0^2): the separable GEMM (KA={ka}, "
-                                   f"n_terms={n_terms}) and the w pass; bytes = F's lower triangle, the outputs and "
-                                   "new V rows, the tables (DESIGN.md section 2.4)"}
+                    "design_note": "bytes = F's lower triangle (the w pass), the posterior in / out, the new V rows "
+                                   "and the Z rows; the launch is a chain of dependent phases (producers -> w -> "
+                                   "Z -> GEMM -> cells), latency- not bandwidth-bound (DESIGN.md section 2.4)"}
         else:
             update = ("incremental, one launch per step (k_inc_stream): bordered-Cholesky append + one pass over "
                       "the resident V = L^-1 psi^T" if FUSED else

@@ -175,6 +175,8 @@ int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, 
 int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, double* points, int64_t* count);
 /* Keep only the first n_keep_hifi hifi rows (no refactor; benchmark reset). */
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi);
+/* mfgp_truncate of count models with one call (the benchmark's per-step reset). */
+int mfgp_batch_truncate(mfgp_model** models, int count, int64_t n_keep_hifi);
 
 /* likelihood (gp:81-106 SF / gp:344-385 MF): the negative log-marginal
  * likelihood of the model's training data under the log-scaled hyperparameters

@@ -69,6 +69,7 @@ SIGNATURES = {
     "mfgp_batch_predict": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int]),
     "mfgp_truncate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "mfgp_batch_truncate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
     "mfgp_last_error": (ctypes.c_char_p, []),
     "mfgp_version": (ctypes.c_char_p, []),
 }
@@ -331,6 +332,27 @@ def batch_append_predict(models, X, y, k, mu_ptr, var_ptr, asynchronous=False, v
                                                 ctypes.c_void_p(vmax_ptr), ctypes.c_void_p(vargmax_ptr),
                                                 ASYNC if asynchronous else 0)
     check(rc)
+
+
+class Batch:
+    """A fixed list of models with its handle / row-count arrays built once: the
+    per-step calls of a seed ensemble without rebuilding ctypes arrays."""
+
+    def __init__(self, models, k):
+        self.models = list(models)
+        n = len(self.models)
+        self.n = n
+        self.arr = (ctypes.c_void_p * n)(*[m.handle.value for m in self.models])
+        self.ks = (ctypes.c_int64 * n)(*[int(v) for v in k])
+
+    def truncate(self, n_keep_hifi):
+        check(lib().mfgp_batch_truncate(self.arr, self.n, int(n_keep_hifi)))
+
+    def append_predict(self, X, y, mu_ptr, var_ptr, asynchronous=False, vmax_ptr=None, vargmax_ptr=None):
+        check(lib().mfgp_batch_append_predict_ex(self.arr, self.n, ctypes.c_void_p(X), ctypes.c_void_p(y), self.ks,
+                                                 ctypes.c_void_p(mu_ptr), ctypes.c_void_p(var_ptr),
+                                                 ctypes.c_void_p(vmax_ptr), ctypes.c_void_p(vargmax_ptr),
+                                                 ASYNC if asynchronous else 0))
 
 
 def batch_append_factor(models, X, y, k, asynchronous=False):

@@ -1473,6 +1473,15 @@ int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
   return MFGP_OK;
 }
 
+int mfgp_batch_truncate(mfgp_model** models, int count, int64_t n_keep_hifi) {
+  if (count < 0 || (count > 0 && !models)) return set_err(MFGP_ERR_ARG, "bad batch");
+  for (int i = 0; i < count; ++i) {
+    const int rc = mfgp_truncate(models[i], n_keep_hifi);
+    if (rc) return rc;
+  }
+  return MFGP_OK;
+}
+
 static int batch_run(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                      double* mu, double* var, double* vmax, int64_t* vargmax, int flags, bool do_factor,
                      bool do_predict);
