@@ -77,12 +77,13 @@ int mfgp_ctx_set_deferred_appends(mfgp_ctx* ctx, int enable);
  * (smallest noise + jitter) <= 1e4 and the model holds the posterior of the old
  * rows, a bordered append + predict of k <= 16 rows runs as k_inc_lat: w =
  * K11^-1 K12 from the resident explicit inverse L^-1, then the SE kernel's
- * separability over the two lattice axes turns L21 V_old into a GEMM over the
- * training terms (f64 MFMA) -- no pass over V -- and var / mu are updated from the
- * previous posterior. Batches with too few GEMM tiles to fill the GPU (one GP
- * at the headline size) keep the V stream; 2 = take it for them too (tests).
- * 0 = always the V stream (k_inc_stream). Same numbers to rounding (DESIGN.md
- * section 2.4). */
+ * separability over the two lattice axes turns L21 V_old into Z rows (per lattice
+ * y-row, the sum of w c ex over the training rows on it) times axis-table rows,
+ * a GEMM over 2 ny terms (f64 MFMA; a training row off the lattice adds one term)
+ * -- no pass over V -- and var / mu are updated from the previous posterior.
+ * Batches whose V stream is estimated cheaper (one GP at the headline size) keep
+ * it; 2 = take the lattice step for them too (tests). 0 = always the V stream
+ * (k_inc_stream). Same numbers to rounding. */
 int mfgp_ctx_set_lattice(mfgp_ctx* ctx, int enable);
 /* Kernel timing with HIP events on the launch stream: enable = 1 times every
  * predict-kernel launch (fused predict or one-pass incremental predict) and

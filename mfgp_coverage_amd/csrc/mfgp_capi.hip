@@ -1751,12 +1751,19 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         const int64_t nst = (m->kind == MFGP_SF ? 1 : 2) * (round_up(m->lat.ny, ZKS) / ZKS);
         nst_min = std::min(nst_min, nst);
       }
-      // too few GEMM tiles to fill the chip (headline size: 16 tiles per GP): the w
-      // pass and the split-K reductions cost more than the V stream they save.
-      // Measured at 128x128, N = 2048 (tools/bench_lattice.py, us per launch,
-      // V stream / lattice): B = 1 60 / 107, B = 2 108 / 115, B = 4 184 / 141,
-      // B = 6 269 / 192, B = 8 345 / 220
-      if (tiles_sum * 4 < c->ncu && !c->lat_force) lat = false;
+      // the lattice step has a fixed cost (its chain of dependent phases, ~58 us)
+      // plus the F stream (~2 TB/s effective); the V stream reads 8 n0 M bytes per GP
+      // (~5.5 TB/s) -- measured at 128x128, N = 2048 (tools/bench_lattice.py, us per
+      // launch, V stream / lattice): B = 1 60 / 65, B = 2 107 / 72, B = 4 185 / 91,
+      // B = 8 345 / 119; configs[4] (32 GPs, 256x256, N = 8192, fp32 V) 11.2 / 2.4 ms
+      double vs_us = 10.0, lat_us = 58.0;
+      for (int i = 0; i < ninc; ++i) {
+        const mfgp_model* m = order[i];
+        const double n0 = (double)hd[i].n0, es = m->dtype == MFGP_F32 ? 4.0 : 8.0;
+        vs_us += (double)m->M * n0 * es / 5.5e6;
+        lat_us += 4.0 * n0 * n0 / 2.0e6;
+      }
+      if (lat_us >= vs_us && !c->lat_force) lat = false;
     }
     if (lat) {
       // split-K so that the GEMM tiles fill the chip about twice, >= 4 stages each
