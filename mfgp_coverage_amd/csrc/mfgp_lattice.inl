@@ -813,6 +813,7 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     __syncthreads();
     if (!lat_last) return;
   }
+  __syncthreads();   // l22_seen is thread 0's (S == 1 has no barrier above)
   if (!l22_seen) wait_flag(d, d.sync + 2, epoch);
   WTRACE(3);
   // ---- epilogue (LDS: the ring is dead) ----
