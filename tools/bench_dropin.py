@@ -1,6 +1,7 @@
 """Per-step latency of the drop-in Python API for one GP (the reference simulator's
 pattern, simulator.py:888-892): updt_hifi(k new samples) then predict(X*) returning
-host arrays. Headline sizes: 128x128 grid, N_L = 1024, N_H = 1016 + 8 per step."""
+host arrays. Headline sizes: 128x128 grid, N_L = 1024, N_H = 1016 + 8 per step;
+--size=G,NL,NH0,k for others. The GP grows by k rows per step (as in the simulator)."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -10,8 +11,12 @@ from mfgp_coverage_amd.synthetic import HYP, Workload
 
 T = 60
 DEFERRED = "--deferred" in sys.argv
+# --size G,NL,NH0,k (default the headline: 128x128, N_L = 1024, N_H = 1016 + 8 per step;
+# the reference's native size: --size 51,121,176,4, i.e. N ~ 300)
+SIZE = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--size=")), "128,1024,1016,8")
+G, NL, NH0, K = (int(v) for v in SIZE.split(","))
 set_deferred_appends(DEFERRED)
-w = Workload(128, 1024, 1016, 8, T, seed=0)
+w = Workload(G, NL, NH0, K, T, seed=0)
 gp = MFGP(w.XL, w.yL.reshape(-1, 1), w.XH, w.yH.reshape(-1, 1), 1, 1)
 gp.hyp = HYP["australia8_mf"].copy()
 gp.updt_info(gp.X_L, gp.y_L, gp.X_H, gp.y_H)
@@ -27,6 +32,6 @@ for s in range(T):
     t3 = time.perf_counter()
     ts["updt_hifi"].append(t1 - t0); ts["predict"].append(t2 - t1); ts["np.diag+amax"].append(t3 - t2)
 import json
-res = {"mode": "deferred" if DEFERRED else "eager", "grid": 128, "N_L": 1024, "N_H": 1024, "agents": 8,
+res = {"mode": "deferred" if DEFERRED else "eager", "grid": G, "N_L": NL, "N_H": NH0 + K, "agents": K,
        "steps_timed": T - 10, "us_median": {k: round(1e6 * float(np.median(v[10:])), 1) for k, v in ts.items()}}
 print(json.dumps(res))
