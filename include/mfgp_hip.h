@@ -66,11 +66,6 @@ int mfgp_ctx_set_incremental(mfgp_ctx* ctx, int enable);
  * 0 = two launches (k_inc_stream for the append alone, then k_vstream). Same
  * numbers either way. */
 int mfgp_ctx_set_fused(mfgp_ctx* ctx, int enable);
-/* Full factor (np.linalg.cholesky, gp:254 / gp:529): one launch per 64-column
- * step (k_fstep: the step's panel, the next diagonal block and the trailing
- * update, handed over inside the launch). Default on; 0 = three launches per step
- * (k_potrf_diag, k_panel, k_syrk). Same numbers either way. */
-int mfgp_ctx_set_fused_factor(mfgp_ctx* ctx, int enable);
 /* Deferred appends (default 0): mfgp_append of rows that a bordered append can
  * take only stages them; the next call that needs the factor runs the append --
  * mfgp_predict as one launch with the one-pass predict (the single-model form of

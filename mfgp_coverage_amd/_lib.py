@@ -31,7 +31,6 @@ SIGNATURES = {
     "mfgp_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "mfgp_ctx_set_incremental": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_fused": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "mfgp_ctx_set_fused_factor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_deferred_appends": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_lattice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_timing_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
@@ -154,11 +153,6 @@ class Context:
     def set_fused(self, on=True):
         """Bordered append + one-pass predict of a batch in one launch (default on)."""
         check(lib().mfgp_ctx_set_fused(self.handle, 1 if on else 0))
-
-    def set_fused_factor(self, on=True):
-        """Full factor in one launch per 64-column step (k_fstep, default on), or three
-        (diagonal block, panel, trailing update). Same numbers either way."""
-        check(lib().mfgp_ctx_set_fused_factor(self.handle, 1 if on else 0))
 
     def set_deferred_appends(self, on=True):
         """Stage appends and run them with the next predict, in one launch (default off:

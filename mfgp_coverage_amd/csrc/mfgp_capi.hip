@@ -96,10 +96,6 @@ struct mfgp_ctx {
   // refactor and recompute V from scratch, as the reference does
   bool incremental = true;
   bool fused = true;          // bordered append + one-pass predict in one launch (k_inc_stream)
-  bool fused_factor = true;   // full factor: one launch per 64-column step (k_fstep)
-  unsigned* fflags = nullptr; // k_fstep ready words [GPs][nb], zeroed when allocated
-  int64_t fflags_n = 0;
-  unsigned fepoch = 0;        // k_fstep: epoch of the last launch (unique per launch)
   bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
@@ -729,30 +725,8 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int rc = ev_begin(c, ev, 1);
   if (rc) return rc;
   HIP_TRY(launch_assemble(dd, count, max_tiles, c->stream));
-  // Blocked right-looking Cholesky. Fused: the first diagonal block, then one
-  // k_fstep launch per step (panel of kb, look-ahead diagonal block kb+1,
-  // trailing update of kb). Otherwise per step: diagonal factor + inverse
-  // (k_potrf_diag), panel (k_panel), trailing update (k_syrk).
-  if (c->fused_factor && max_nb > 1) {
-    const int64_t need = (int64_t)count * max_nb;
-    if (need > c->fflags_n) {
-      if (c->fflags) HIP_TRY(hipFree(c->fflags));
-      c->fflags = nullptr;
-      c->fflags_n = 0;
-      const int64_t n = std::max<int64_t>(need, 2 * c->fflags_n);
-      HIP_TRY(hipMalloc(&c->fflags, sizeof(unsigned) * n));
-      HIP_TRY(hipMemsetAsync(c->fflags, 0, sizeof(unsigned) * n, c->stream));
-      c->fflags_n = n;
-    }
-    HIP_TRY(launch_potrf_diag(dd, count, 0, 0, c->stream));
-    for (int kb = 0; kb + 1 < max_nb; ++kb) {
-      if (++c->fepoch == 0) {   // wrapped: no stale word may match a new epoch
-        HIP_TRY(hipMemsetAsync(c->fflags, 0, sizeof(unsigned) * c->fflags_n, c->stream));
-        c->fepoch = 1;
-      }
-      HIP_TRY(launch_fstep(dd, count, kb, max_nb - kb - 1, c->fflags, (int)max_nb, c->fepoch, c->stream));
-    }
-  } else
+  // Blocked right-looking Cholesky, per 64-column step: diagonal factor +
+  // inverse (k_potrf_diag), panel (k_panel), trailing update (k_syrk).
   for (int kb = 0; kb < max_nb; ++kb) {
     HIP_TRY(launch_potrf_diag(dd, count, kb, 0, c->stream));
     const int64_t below = max_nb - kb - 1;
@@ -1115,7 +1089,6 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
       c->ncu = ncu;
   }
   c->stream = c->own;
-  if (const char* e = std::getenv("MFGP_FUSED_FACTOR")) c->fused_factor = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
@@ -1142,7 +1115,6 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
   for (int i = 0; i < RING; ++i) (void)hipEventDestroy(c->ring_ev[i]);
   if (c->ws) (void)hipFree(c->ws);
   if (c->vscr) (void)hipFree(c->vscr);
-  if (c->fflags) (void)hipFree(c->fflags);
   if (c->d_ring) (void)hipFree(c->d_ring);
   if (c->h_status) (void)hipHostFree(c->h_status);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
@@ -1205,13 +1177,6 @@ int mfgp_ctx_set_fused(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->fused = enable != 0;
-  return MFGP_OK;
-}
-
-int mfgp_ctx_set_fused_factor(mfgp_ctx* c, int enable) {
-  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  c->fused_factor = enable != 0;
   return MFGP_OK;
 }
 

@@ -171,11 +171,6 @@ inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1)
 hipError_t launch_append(const GPDesc* d, int count, hipStream_t s);
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);
 hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStream_t s);
-// one step kb of the blocked Cholesky in one launch: panel of kb, look-ahead diagonal
-// block kb+1, trailing update of kb (k_fstep); below = max over GPs of nb - kb - 1;
-// flags: [count][fstride] ready words, epoch unique per launch (never 0)
-hipError_t launch_fstep(const GPDesc* d, int count, int kb, int64_t below, unsigned* flags, int fstride,
-                        unsigned epoch, hipStream_t s);
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s);
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);

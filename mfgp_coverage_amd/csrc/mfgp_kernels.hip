@@ -176,7 +176,7 @@ __device__ __forceinline__ d4 mfma16(const double* __restrict__ A, int ars, int 
 
 // S: 64x64 row-major (stride SP), lower triangle = the matrix. On exit S = L
 // (zeros above the diagonal) and R = L^-1 (row-major, zeros above).
-__device__ __forceinline__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R, double* __restrict__ T,
+__device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R, double* __restrict__ T,
                                  double* __restrict__ U, int64_t g0, int64_t N, int* status) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r16 = lane & 15, q16 = lane >> 4;
@@ -288,6 +288,75 @@ __device__ __forceinline__ void factor_invert_64(double* __restrict__ S, double*
     __syncthreads();
     STAMP(14 + I);
   }
+}
+
+// With `upd`, the tile first receives the last trailing update of the previous
+// step, A_kk -= L_k,k-1 L_k,k-1^T (f64 MFMA), so that the rest of that trailing
+// update can run concurrently on the side stream (look-ahead, see capi).
+__global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb, int upd) {
+  const GPDesc& d = descs[blockIdx.x];
+  const int64_t N = d.N, ld = d.ld;
+  if (kb >= nblocks_factor(N)) return;
+  // one LDS array: As/Bs of the update (2 x 32 KB) alias S/R/T/U of the factor
+  __shared__ double sh[2 * NB * SP + (NB / DB) * DB * DP + (NB / DB - 1) * DB * DP];
+  double* const S = sh;
+  double* const R = sh + NB * SP;
+  double* const T = R + NB * SP;
+  double* const U = T + (NB / DB) * DB * DP;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int64_t o = (int64_t)kb * NB;
+  double* __restrict__ A = d.A;
+  STAMP(0);
+  if (upd && kb > 0) {
+    double* As = sh;
+    load_tile_cm(As, A, ld, o, o - NB, tid);   // L_k,k-1 (A operand and, transposed, B operand)
+    const int r = lane & 15, q = lane >> 4;
+    Acc acc;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          acc.c[mt][nt][v] = A[(o + acc_col(wn, nt, r)) * ld + o + acc_row(wm, mt, q, v)];
+    __syncthreads();
+    tile_mma<true>(As, As, acc, wm, wn, lane);
+    __syncthreads();   // As is overwritten by S below
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int i = acc_row(wm, mt, q, v), j = acc_col(wn, nt, r);
+          S[i * SP + j] = (j <= i) ? acc.c[mt][nt][v] : 0.0;
+        }
+  } else {
+    // unconditional loads (the upper part of the tile is masked afterwards) keep
+    // all 16 loads per thread in flight
+    double v[NB * NB / NT];
+#pragma unroll
+    for (int t = 0; t < NB * NB / NT; ++t) {
+      const int e = tid + t * NT, i = e & 63, j = e >> 6;
+      v[t] = A[(o + j) * ld + o + i];
+    }
+#pragma unroll
+    for (int t = 0; t < NB * NB / NT; ++t) {
+      const int e = tid + t * NT, i = e & 63, j = e >> 6;
+      S[i * SP + j] = (j <= i) ? v[t] : 0.0;
+    }
+  }
+  __syncthreads();
+  STAMP(1);
+  factor_invert_64(S, R, T, U, o, N, d.status);
+  double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
+#pragma unroll 4
+  for (int e = tid; e < NB * NB; e += NT) {
+    const int i = e & 63, j = e >> 6;   // column-major: consecutive threads -> consecutive rows
+    A[(o + j) * ld + o + i] = S[i * SP + j];
+    Li[j * NB + i] = R[i * SP + j];
+  }
+  STAMP(18);
 }
 
 // Panel: L_ik = A_ik * Linv_kk^T for every row block i > kb.
@@ -821,210 +890,6 @@ __device__ void wait_l21(const GPDesc& d) {
     }
   }
   __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// Blocked Cholesky, one launch per 64-column step after the first diagonal
-// block (k_fstep; the per-step three-launch form k_potrf_diag / k_panel / k_syrk
-// stays for mfgp_ctx_set_fused_factor(0)). Launch kb holds, per GP:
-//   roles [0, below)        panel: L_ik = A_ik Linv_kk^T for row blocks i > kb;
-//                           stored write-through, then flag[i] = epoch
-//   role below              look-ahead diagonal block kb+1: waits for flag[kb+1],
-//                           applies the last trailing term A_k+1,k+1 -= L L^T itself,
-//                           then factor + inverse (the next launch's panel input)
-//   roles > below           trailing tiles (i, j) of step kb except (kb+1, kb+1):
-//                           prefetch A_ij, wait for flag[i] and flag[j], A_ij -= L_ik L_jk^T
-// so the diagonal chain of step kb+1 runs beside the trailing update of step kb
-// instead of after it, and the launch gaps of two kernels per step are gone.
-// Hand-off as in k_inc_stream (launch_inc_stream): write-through stores, a drain,
-// a relaxed agent-scope flag holding this launch's epoch (unique per launch, so
-// the flags need no reset); consumers read the handed tiles with agent-scope
-// loads (coherent across the XCDs' L2s and past the CU's L1). Grid (GPs, roles)
-// with the GP as x: every panel role of every GP precedes every waiter in the
-// linear dispatch order, and panels wait on nothing, so the waits always end
-// (they are bounded anyway: SYNC_FAIL after ~1 s).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void load_tile_cm_x(double* __restrict__ Ts, const double* __restrict__ G, int64_t ld,
-                                               int64_t r0, int64_t c0, int tid) {
-  double v[16];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int k = p * 8 + (tid >> 5);
-    const int i = (tid & 31) * 2;
-    const double* src = G + (c0 + k) * ld + r0 + i;
-    v[2 * p] = ldx<true>(src);
-    v[2 * p + 1] = ldx<true>(src + 1);
-  }
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int k = p * 8 + (tid >> 5);
-    const int i = (tid & 31) * 2;
-    dv2 t;
-    t[0] = v[2 * p];
-    t[1] = v[2 * p + 1];
-    *reinterpret_cast<dv2*>(Ts + swz(k, i)) = t;
-  }
-}
-
-constexpr int DIAG_LDS = 2 * NB * SP + (NB / DB) * DB * DP + (NB / DB - 1) * DB * DP;
-
-// Diagonal block kb: factor + inverse of the 64x64 tile (factor_invert_64).
-// With `upd`, the tile first receives the last trailing update of the previous
-// step, A_kk -= L_k,k-1 L_k,k-1^T (f64 MFMA): k_fstep's look-ahead role, where
-// L_k,k-1 was stored by a panel role of the same launch (XW: agent-scope loads).
-template <bool XW>
-__device__ __forceinline__ void potrf_diag_tile(const GPDesc& d, int kb, int upd, double* sh) {
-  const int64_t N = d.N, ld = d.ld;
-  // one LDS array: As of the update (32 KB) aliases S/R/T/U of the factor
-  double* const S = sh;
-  double* const R = sh + NB * SP;
-  double* const T = R + NB * SP;
-  double* const U = T + (NB / DB) * DB * DP;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
-  const int64_t o = (int64_t)kb * NB;
-  double* __restrict__ A = d.A;
-  STAMP(0);
-  if (upd && kb > 0) {
-    double* As = sh;
-    const int r = lane & 15, q = lane >> 4;
-    Acc acc;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          acc.c[mt][nt][v] = A[(o + acc_col(wn, nt, r)) * ld + o + acc_row(wm, mt, q, v)];
-    // L_k,k-1 (A operand and, transposed, B operand)
-    if constexpr (XW) load_tile_cm_x(As, A, ld, o, o - NB, tid);
-    else load_tile_cm(As, A, ld, o, o - NB, tid);
-    __syncthreads();
-    tile_mma<true>(As, As, acc, wm, wn, lane);
-    __syncthreads();   // As is overwritten by S below
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int i = acc_row(wm, mt, q, v), j = acc_col(wn, nt, r);
-          S[i * SP + j] = (j <= i) ? acc.c[mt][nt][v] : 0.0;
-        }
-  } else {
-    // unconditional loads (the upper part of the tile is masked afterwards) keep
-    // all 16 loads per thread in flight
-    double v[NB * NB / NT];
-#pragma unroll
-    for (int t = 0; t < NB * NB / NT; ++t) {
-      const int e = tid + t * NT, i = e & 63, j = e >> 6;
-      v[t] = A[(o + j) * ld + o + i];
-    }
-#pragma unroll
-    for (int t = 0; t < NB * NB / NT; ++t) {
-      const int e = tid + t * NT, i = e & 63, j = e >> 6;
-      S[i * SP + j] = (j <= i) ? v[t] : 0.0;
-    }
-  }
-  __syncthreads();
-  STAMP(1);
-  factor_invert_64(S, R, T, U, o, N, d.status);
-  double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
-#pragma unroll 4
-  for (int e = tid; e < NB * NB; e += NT) {
-    const int i = e & 63, j = e >> 6;   // column-major: consecutive threads -> consecutive rows
-    A[(o + j) * ld + o + i] = S[i * SP + j];
-    Li[j * NB + i] = R[i * SP + j];
-  }
-  STAMP(18);
-}
-
-__global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb, int upd) {
-  const GPDesc& d = descs[blockIdx.x];
-  if (kb >= nblocks_factor(d.N)) return;
-  __shared__ double sh[DIAG_LDS];
-  potrf_diag_tile<false>(d, kb, upd, sh);
-}
-
-#ifndef MFGP_FSTEP_PRIO
-#define MFGP_FSTEP_PRIO 1   // k_fstep: panel and diagonal roles at wave priority 3
-#endif
-#ifndef MFGP_FSTEP_WAVES
-#define MFGP_FSTEP_WAVES 2   // k_fstep waves per SIMD: two workgroups per CU (LDS 2 x 80 KB)
-#endif
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_FSTEP_WAVES, MFGP_FSTEP_WAVES))) void k_fstep(const GPDesc* __restrict__ descs, int kb, int below,
-                                              unsigned* __restrict__ flags, int fstride, unsigned epoch) {
-  const GPDesc& d = descs[blockIdx.x];
-  const int64_t T = nblocks_factor(d.N) - kb - 1;   // this GP's row blocks below kb
-  const int role = blockIdx.y;
-  __shared__ double sh[DIAG_LDS];
-  unsigned* const fl = flags + (int64_t)blockIdx.x * fstride;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
-  const int r = lane & 15, q = lane >> 4;
-  double* __restrict__ A = d.A;
-  const int64_t ld = d.ld;
-  double* const As = sh;
-  double* const Bs = sh + TILE;
-  if (role < below) {   // panel tile of row block ib
-    if (role >= T) return;
-    if (MFGP_FSTEP_PRIO) __builtin_amdgcn_s_setprio(3);   // panels + diagonal block: the step's critical path
-    const int64_t ib = kb + 1 + role;
-    load_tile_cm(As, A, ld, ib * NB, (int64_t)kb * NB, tid);
-    load_tile_cm(Bs, d.Linv + (int64_t)kb * TILE, NB, 0, 0, tid);  // Bs[m][j] = Linv[j][m]
-    __syncthreads();
-    Acc acc;
-    acc_zero(acc);
-    tile_mma<false>(As, Bs, acc, wm, wn, lane);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
-          stx<true>(A + ((int64_t)kb * NB + col) * ld + ib * NB + row, acc.c[mt][nt][v]);
-        }
-    drain_stores();
-    __syncthreads();
-    if (tid == 0) publish(fl + ib, epoch);
-    return;
-  }
-  if (role == below) {   // look-ahead diagonal block kb+1
-    if (T <= 0) return;
-    if (MFGP_FSTEP_PRIO) __builtin_amdgcn_s_setprio(3);
-    wait_flag(d, fl + kb + 1, epoch);
-    potrf_diag_tile<true>(d, kb + 1, 1, sh);
-    return;
-  }
-  const int64_t t = (int64_t)(role - below);   // trailing tile t >= 1 (t = 0 is the look-ahead's)
-  if (t >= T * (T + 1) / 2) return;
-  int ii, jj;
-  tri_index(t, ii, jj);
-  const int64_t ib = kb + 1 + ii, jb = kb + 1 + jj;
-  Acc acc;   // A_ij is not written by any other role of this launch: load it before the wait
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
-        acc.c[mt][nt][v] = A[(jb * NB + col) * ld + ib * NB + row];
-      }
-  wait_flag(d, fl + ib, epoch);
-  if (jb != ib) wait_flag(d, fl + jb, epoch);
-  load_tile_cm_x(As, A, ld, ib * NB, (int64_t)kb * NB, tid);
-  load_tile_cm_x(Bs, A, ld, jb * NB, (int64_t)kb * NB, tid);
-  __syncthreads();
-  tile_mma<true>(As, Bs, acc, wm, wn, lane);
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
-        A[(jb * NB + col) * ld + ib * NB + row] = acc.c[mt][nt][v];
-      }
 }
 
 // Coordinates / observation of training row `row`: rows landing in this launch
@@ -2613,12 +2478,6 @@ hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStr
 }
 hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStream_t s) {
   hipLaunchKernelGGL(k_potrf_diag, dim3(count), dim3(NT), 0, s, d, kb, upd);
-  return hipGetLastError();
-}
-hipError_t launch_fstep(const GPDesc* d, int count, int kb, int64_t below, unsigned* flags, int fstride,
-                        unsigned epoch, hipStream_t s) {
-  const int64_t roles = below + below * (below + 1) / 2;
-  hipLaunchKernelGGL(k_fstep, dim3(count, (unsigned)roles), dim3(NT), 0, s, d, kb, (int)below, flags, fstride, epoch);
   return hipGetLastError();
 }
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s) {

@@ -1,9 +1,9 @@
-"""Full-path factor at the headline size: the fused step (k_fstep, one launch
-per 64-column step) against the three-launch form (k_potrf_diag / k_panel /
-k_syrk), 8 MF GPs at 128x128, N = 2048, full refactor + predict per step
-(incremental off: what the reference does on every update, gp:493-529).
-Prints one JSON line: factor ms per step (HIP events around the factor
-stages) for both, and whether mu / var / L agree bit for bit.
+"""Full-path factor at the headline size: 8 MF GPs at 128x128, N = 2048, full
+refactor + predict per step (incremental off: what the reference does on every
+update, gp:493-529). Prints one JSON line: the median factor ms per step (HIP
+events around the factor stages: k_assemble, k_potrf_diag / k_panel / k_syrk per
+64-column step, k_extract_z). Round 2 used it for the A/B of a one-launch-per-step
+factor (commit 3c145a2, profiles/r02_fstep_ab.json; not kept).
 
 usage (GPU box): python tools/bench_factor.py [--steps 10] [--gp 8]
 """
@@ -19,10 +19,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mfgp_coverage_amd import _lib, synthetic  # noqa: E402
 
 
-def run(fused, wls, steps, k, NH0, hyp, dev):
+def run(wls, steps, k, NH0, hyp, dev):
     ctx = _lib.Context(0)
     ctx.set_incremental(False)
-    ctx.set_fused_factor(fused)
     B, M = len(wls), wls[0].xs.shape[0]
     models = []
     for wl in wls:
@@ -64,15 +63,9 @@ def main():
     NH0 = a.NH - k
     wls = [synthetic.Workload(a.G, a.NL, NH0, k, a.steps + 2, seed=s) for s in range(a.gp)]
     hyp = synthetic.HYP["australia8_mf"]
-    t3, mu3, var3, L3, st3 = run(False, wls, a.steps, k, NH0, hyp, dev)
-    t1, mu1, var1, L1, st1 = run(True, wls, a.steps, k, NH0, hyp, dev)
-    assert st1["full_factor"] > a.steps and st3["full_factor"] > a.steps, (st1, st3)
-    print(json.dumps({"gp": a.gp, "G": a.G, "N": a.NL + a.NH, "steps": a.steps,
-                      "factor_ms_three_launch": t3, "factor_ms_fused": t1, "speedup": t3 / t1,
-                      "mu_bit_equal": bool(np.array_equal(mu1, mu3)),
-                      "var_bit_equal": bool(np.array_equal(var1, var3)),
-                      "L_bit_equal": bool(np.array_equal(L1, L3)),
-                      "max_abs_dL": float(np.max(np.abs(L1 - L3)))}))
+    t, _, _, _, st = run(wls, a.steps, k, NH0, hyp, dev)
+    assert st["full_factor"] > a.steps, st
+    print(json.dumps({"gp": a.gp, "G": a.G, "N": a.NL + a.NH, "steps": a.steps, "factor_ms": t}))
 
 
 if __name__ == "__main__":
