@@ -100,6 +100,8 @@ struct mfgp_ctx {
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
+  bool lat_arg = true;        // a step that is one k_inc_lat launch passes its descriptors by value
+                              // (MFGP_LAT_ARG=0: upload them, diagnostics)
   // pinned host staging of the status words
   int* h_status = nullptr;
   size_t h_status_n = 0;
@@ -920,6 +922,28 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   return ev_end(c, ev);
 }
 
+// The lattice step alone from host descriptors passed by value (k_inc_lat_arg):
+// for a batch step that needs nothing else on the device -- no F / table / axis
+// builds, no other appends or predicts -- so the descriptor array is not uploaded.
+bool lat_arg_ok(const mfgp_ctx* c, const GPDesc* hd, int count) {
+  if (!c->lat_arg || count < 1 || count > LAT_ARG_MAX) return false;
+  for (int i = 0; i < count; ++i)
+    if (hd[i].lat_fbuild || hd[i].n0 > hd[i].tab_lo || hd[i].lat_axbuild) return false;
+  return true;
+}
+
+int enqueue_inc_lat_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
+  int64_t max_blocks = 0;
+  for (int i = 0; i < count; ++i)
+    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu +
+                                                   (int64_t)hd[i].lat_tiles * hd[i].ksplit);
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 0);
+  if (rc) return rc;
+  HIP_TRY(launch_inc_lat_arg(hd, count, max_blocks, hd[0].ka, hd[0].vf32, c->stream));
+  return ev_end(c, ev);
+}
+
 // Row splits of the one-pass predict for a launch over these descriptors: 128-cell
 // workgroups while they fill the chip (~4 per CU), else 64 or 32 cells with the
 // rows split 2 or 4 ways (the drop-in simulator predicts one GP at a time).
@@ -1089,6 +1113,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
       c->ncu = ncu;
   }
   c->stream = c->own;
+  if (const char* e = std::getenv("MFGP_LAT_ARG")) c->lat_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
@@ -1857,6 +1882,10 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       if (res_b[0] >= 0) res_tag(m, res_b[0], m->v_n, 0);
       continue;
     }
+    if (do_factor && lat && nfull == 0 && ninc == nb && np == nv && lat_arg_ok(c, hd, ninc)) {
+      // the whole step is one k_inc_lat launch: its descriptors go by value
+      if ((rc = enqueue_inc_lat_arg(c, hd, ninc))) return rc;
+    } else {
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
     if (do_factor) {
@@ -1868,6 +1897,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     }
     if (nv > 0 && !fuse && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
     if (np > nv && (rc = enqueue_predict(c, dd + nb + nv, hd + nb + nv, np - nv))) return rc;
+    }
     if ((rc = release_slot(c, slot))) return rc;
     for (int i = 0; i < np; ++i) {
       mfgp_model* m = porder[i];

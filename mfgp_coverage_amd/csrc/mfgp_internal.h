@@ -189,6 +189,13 @@ hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStre
 // lattice-separable append + predict (k_inc_lat); max_blocks = max over GPs of
 // nprod + nwu + lat_tiles * ksplit
 hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
+// the same with the `count` <= LAT_ARG_MAX host descriptors `h` passed by value as
+// the kernel argument (no device copy of the descriptor array)
+constexpr int LAT_ARG_MAX = 8;
+struct LatDescArg {
+  GPDesc d[LAT_ARG_MAX];
+};
+hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
 // separable tables and lattice indices of rows [tab_lo, n0); max_rows = max over GPs of n0 - tab_lo
 hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s);
 // axis tables (GPs with lat_axbuild); max_tabw = max over GPs of tabw

@@ -19,6 +19,7 @@
 //   A[i][k]: lane l holds A[l&15][l>>4];  B[k][j]: lane l holds B[l>>4][l&15];
 //   C/D:     lane l, reg v holds C[(l>>4) + 4v][l&15].
 #include <climits>
+#include <cstring>
 #include "mfgp_internal.h"
 #include "mfgp_device.h"
 
@@ -2528,6 +2529,17 @@ hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka
   else if (ka == 8) hipLaunchKernelGGL((k_inc_lat<8, double>), g, dim3(NT), 0, s, d);
   else if (vf32) hipLaunchKernelGGL((k_inc_lat<16, float>), g, dim3(NT), 0, s, d);
   else hipLaunchKernelGGL((k_inc_lat<16, double>), g, dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s) {
+  if (count < 1 || count > LAT_ARG_MAX) return hipErrorInvalidValue;
+  LatDescArg a;
+  std::memcpy(a.d, h, sizeof(GPDesc) * count);
+  const dim3 g(count, (unsigned)max_blocks);
+  if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat_arg<8, float>), g, dim3(NT), 0, s, a);
+  else if (ka == 8) hipLaunchKernelGGL((k_inc_lat_arg<8, double>), g, dim3(NT), 0, s, a);
+  else if (vf32) hipLaunchKernelGGL((k_inc_lat_arg<16, float>), g, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((k_inc_lat_arg<16, double>), g, dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_lat_axes(const GPDesc* d, int count, int64_t max_tabw, hipStream_t s) {

@@ -1040,6 +1040,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
   inc_lat_wg<KA, VT>(descs[blockIdx.x]);
 }
 
+// The same step with the batch's descriptors as a by-value kernel argument (up
+// to LAT_ARG_MAX of them, 9 KB): a step that needs no other kernel takes no
+// per-step upload of its descriptor array. That upload is a host-to-device copy
+// on the copy engine, and its hand-off back to the compute queue put ~16 us of
+// idle stream time between consecutive steps (kernel trace: k_inc_lat ->
+// k_inc_lat gaps of 21 us under rocprofv3).
+template <int KA, class VT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_lat_arg(
+    const LatDescArg a) {
+  // index the kernarg segment itself: a dynamic index into the by-value argument
+  // would copy all 9 KB of it to scratch
+  (void)a;
+  const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
+  inc_lat_wg<KA, VT>(descs[blockIdx.x]);
+}
+
 // The separable tables of rows [tab_lo, n0) (full-path refresh; the step itself
 // appends its new rows). Grid (GPs, row chunks of 4 rows x 4 tables x tabw).
 __global__ __launch_bounds__(NT) void k_lat_tables(const GPDesc* __restrict__ descs) {

@@ -256,3 +256,53 @@ def test_lattice_after_hyp_change_rebuilds():
     assert _err(hyp2, mu, var, mu_r, var_r) < TOL
     st = m.stats()
     assert st["lattice"] == 2 and st["full_factor"] == 2, st
+
+
+def test_lattice_descriptors_by_value_equal_upload(monkeypatch):
+    """A batch step that is one k_inc_lat launch passes its descriptors as the
+    kernel argument (k_inc_lat_arg, no descriptor upload); MFGP_LAT_ARG=0 makes
+    a context upload them instead. Same kernel body, so the same bits; ragged
+    batch of 1, 3 and 8 GPs (LAT_ARG_MAX) over several steps, fused argmax."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    hyp = _hyp("australia8_mf")
+    G = 48
+
+    def run(ctx, B):
+        models, data = [], []
+        for i in range(B):
+            nl, nh = 100 + 17 * i, 150 - 9 * i
+            Xs, X, y = _data(G, nl + nh + 40, seed=70 + i)
+            models.append(_model(ctx, hyp, X[:nl + nh], y[:nl + nh], nl, Xs))
+            data.append((X, y, nl + nh))
+        M = Xs.shape[0]
+        mu = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        var = torch.empty_like(mu)
+        vmax = torch.empty(B, dtype=torch.float64, device="cuda")
+        vam = torch.empty(B, dtype=torch.int64, device="cuda")
+        _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
+        out = []
+        for step, k in enumerate((8, 3, 8, 8)):
+            Xn = np.concatenate([X[n:n + k] for X, _, n in data])
+            yn = np.concatenate([y[n:n + k] for _, y, n in data])
+            Xt = torch.from_numpy(np.ascontiguousarray(Xn)).cuda()
+            yt = torch.from_numpy(np.ascontiguousarray(yn)).cuda()
+            _lib.batch_append_predict(models, Xt.data_ptr(), yt.data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
+                                      vmax_ptr=vmax.data_ptr(), vargmax_ptr=vam.data_ptr())
+            data = [(X, y, n + k) for X, y, n in data]
+            out.append((mu.cpu().numpy(), var.cpu().numpy(), vmax.cpu().numpy(), vam.cpu().numpy()))
+        assert all(m.stats()["lattice"] == 4 for m in models), [m.stats() for m in models]
+        ctx.synchronize()
+        return out
+
+    for B in (1, 3, 8):
+        a = _lib.Context(0)
+        a.set_lattice("force")
+        monkeypatch.setenv("MFGP_LAT_ARG", "0")
+        b = _lib.Context(0)
+        monkeypatch.delenv("MFGP_LAT_ARG")
+        b.set_lattice("force")
+        ra, rb = run(a, B), run(b, B)
+        for sa, sb in zip(ra, rb):
+            for xa, xb in zip(sa, sb):
+                assert np.array_equal(xa, xb), B
