@@ -440,8 +440,16 @@ def main():
                                                                          "australia8_mf", "f64")
         c4_cfg = (G, NL, NH, B, a.hyp, a.dtype) == (256, 4096, 4096, 32, "australia9_mf", "f32")
         kern = "k_inc_lat" if lattice else ("k_inc_stream" if FUSED else "k_vstream")
-        traffic, traffic_src = pmc_traffic(kern, "configs4" if c4_cfg else None) if (default_cfg or c4_cfg) \
-            else (None, None)
+        traffic, traffic_src = None, None
+        if default_cfg or c4_cfg:
+            # batches of <= 8 GPs run the step with its descriptors as the kernel argument
+            # (k_inc_lat_arg); larger ones upload them (k_inc_lat)
+            if lattice and B <= 8:
+                traffic, traffic_src = pmc_traffic("k_inc_lat_arg", "configs4" if c4_cfg else None)
+                if traffic is not None:
+                    kern = "k_inc_lat_arg"
+            if traffic is None:
+                traffic, traffic_src = pmc_traffic(kern, "configs4" if c4_cfg else None)
         if lattice:
             update = ("incremental, lattice-separable, one launch per step (k_inc_lat): bordered-Cholesky append, "
                       "w = K11^-1 K12 from the resident L^-1; every training term lies on the grid's lattice, so "

@@ -544,3 +544,74 @@ def test_speculative_append_not_pd_raises_at_append():
     m.predict()
     with pytest.raises(np.linalg.LinAlgError):
         m.append(X[20:21], y[20:21])       # speculative form (after a predict): raises here
+
+
+def _bad_and_good(ctx, Xs, X, y):
+    """A model whose next append is not positive definite (negative jitter, as in
+    test_speculative_append_not_pd_raises_at_append) and a well-posed one."""
+    from mfgp_coverage_amd import _lib
+    hyp = np.array([0.0, 0.0, -1.0, 0.0, -3.0, -1.0, -1.0, 2.0, -20.0])
+    bad = _lib.Model(ctx, _lib.MF, hyp, -1.0)
+    bad.set_grid(Xs)
+    bad.set_data(X[:20], y[:20], np.empty((0, 2)), np.empty(0))
+    good, hyp_g = _model(ctx, "mf", X[:20], y[:20], 10, Xs)
+    return bad, good, hyp_g
+
+
+def test_batch_async_not_pd_is_traced_to_its_model():
+    """a non-PD factor inside an asynchronous batch is reported at
+    mfgp_ctx_synchronize and dropped from ITS model, so that model's next predict
+    refactors (and raises again) instead of serving the failed factor; the other
+    model of the batch is unaffected."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    ctx = _lib.Context(0)
+    Xs, X, y = _points(24, 30, seed=2, ongrid=True)
+    bad, good, hyp_g = _bad_and_good(ctx, Xs, X, y)
+    M = Xs.shape[0]
+    mu = torch.empty(2 * M, dtype=torch.float64, device="cuda")
+    var = torch.empty_like(mu)
+    _lib.batch_predict([bad, good], mu.data_ptr(), var.data_ptr())
+    ctx.synchronize()
+    Xn = torch.from_numpy(np.ascontiguousarray(np.concatenate([X[20:21], X[21:22]]))).cuda()
+    yn = torch.from_numpy(np.ascontiguousarray(np.concatenate([y[20:21], y[21:22]]))).cuda()
+    _lib.batch_append_predict([bad, good], Xn.data_ptr(), yn.data_ptr(), [1, 1], mu.data_ptr(), var.data_ptr(),
+                              asynchronous=True)
+    with pytest.raises(np.linalg.LinAlgError):
+        ctx.synchronize()
+    with pytest.raises(np.linalg.LinAlgError):
+        bad.predict()
+    mu_g, var_g = good.predict()
+    Xg = np.concatenate([X[:20], X[21:22]])
+    yg = np.concatenate([y[:20], y[21:22]])
+    mu_r, var_r = _ref("mf", Xg, yg, 10, Xs, hyp_g)
+    assert _err(mu_g, var_g, mu_r, var_r, hyp_g) < TOL
+
+
+def test_destroy_before_synchronize():
+    """a model destroyed (Python GC) while its asynchronous batch is
+    pending leaves no dangling status word behind: the context synchronises
+    cleanly and the surviving model's result is right."""
+    import gc
+
+    import torch
+    from mfgp_coverage_amd import _lib
+    ctx = _lib.Context(0)
+    Xs, X, y = _points(24, 60, seed=5, ongrid=True)
+    a, hyp = _model(ctx, "mf", X[:40], y[:40], 20, Xs)
+    b, _ = _model(ctx, "mf", X[:40], y[:40], 20, Xs)
+    M = Xs.shape[0]
+    mu = torch.empty(2 * M, dtype=torch.float64, device="cuda")
+    var = torch.empty_like(mu)
+    _lib.batch_predict([a, b], mu.data_ptr(), var.data_ptr())
+    ctx.synchronize()
+    Xn = torch.from_numpy(np.ascontiguousarray(np.concatenate([X[40:44], X[44:48]]))).cuda()
+    yn = torch.from_numpy(np.ascontiguousarray(np.concatenate([y[40:44], y[44:48]]))).cuda()
+    _lib.batch_append_predict([a, b], Xn.data_ptr(), yn.data_ptr(), [4, 4], mu.data_ptr(), var.data_ptr(),
+                              asynchronous=True)
+    del b
+    gc.collect()
+    ctx.synchronize()
+    mu_a, var_a = a.predict()
+    mu_r, var_r = _ref("mf", X[:44], y[:44], 20, Xs, hyp)
+    assert _err(mu_a, var_a, mu_r, var_r, hyp) < TOL
