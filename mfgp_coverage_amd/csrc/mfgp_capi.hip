@@ -100,8 +100,9 @@ struct mfgp_ctx {
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
-  bool lat_arg = true;        // a step that is one k_inc_lat launch passes its descriptors by value
-                              // (MFGP_LAT_ARG=0: upload them, diagnostics)
+  bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
+                              // descriptors by value
+                              // (MFGP_DESC_ARG=0: upload them, diagnostics)
   // pinned host staging of the status words
   int* h_status = nullptr;
   size_t h_status_n = 0;
@@ -922,14 +923,26 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   return ev_end(c, ev);
 }
 
-// The lattice step alone from host descriptors passed by value (k_inc_lat_arg):
+// A batch step that is one launch takes its host descriptors by value
+// (k_inc_stream_arg, k_inc_lat_arg). The lattice step alone (k_inc_lat_arg):
 // for a batch step that needs nothing else on the device -- no F / table / axis
 // builds, no other appends or predicts -- so the descriptor array is not uploaded.
-bool lat_arg_ok(const mfgp_ctx* c, const GPDesc* hd, int count) {
-  if (!c->lat_arg || count < 1 || count > LAT_ARG_MAX) return false;
+bool desc_arg_ok(const mfgp_ctx* c, const GPDesc* hd, int count) {
+  if (!c->desc_arg || count < 1 || count > DESC_ARG_MAX) return false;
   for (int i = 0; i < count; ++i)
     if (hd[i].lat_fbuild || hd[i].n0 > hd[i].tab_lo || hd[i].lat_axbuild) return false;
   return true;
+}
+
+int enqueue_inc_stream_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
+  int64_t max_blocks = 0;
+  for (int i = 0; i < count; ++i)
+    max_blocks = std::max(max_blocks, hd[i].nprod + ntiles_wg(hd[i].M, hd[i].rsplit, hd[i].vf32));
+  EvPair ev{};
+  int rc = ev_begin(c, ev, 0);
+  if (rc) return rc;
+  HIP_TRY(launch_inc_stream_arg(hd, count, max_blocks, hd[0].vf32, c->stream));
+  return ev_end(c, ev);
 }
 
 int enqueue_inc_lat_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
@@ -1113,7 +1126,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
       c->ncu = ncu;
   }
   c->stream = c->own;
-  if (const char* e = std::getenv("MFGP_LAT_ARG")) c->lat_arg = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
@@ -1882,9 +1895,13 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       if (res_b[0] >= 0) res_tag(m, res_b[0], m->v_n, 0);
       continue;
     }
-    if (do_factor && lat && nfull == 0 && ninc == nb && np == nv && lat_arg_ok(c, hd, ninc)) {
+    if (do_factor && lat && nfull == 0 && ninc == nb && np == nv && desc_arg_ok(c, hd, ninc)) {
       // the whole step is one k_inc_lat launch: its descriptors go by value
       if ((rc = enqueue_inc_lat_arg(c, hd, ninc))) return rc;
+    } else if (do_factor && fuse && !lat && nfull == 0 && ninc == nb && np == nv && c->desc_arg &&
+               ninc <= DESC_ARG_MAX) {
+      // the whole step is one k_inc_stream launch (append + one-pass predict)
+      if ((rc = enqueue_inc_stream_arg(c, hd, ninc))) return rc;
     } else {
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;

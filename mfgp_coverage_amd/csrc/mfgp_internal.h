@@ -181,20 +181,24 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
 // bordered append (k_inc_stream without cell tiles); max_nprod = max over GPs of nprod
 // vf32: the batch's models store V in fp32 (GPDesc::Vf); a batch is of one V precision
 hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, int vf32, hipStream_t s);
+// Descriptors of a batch passed by value as the kernel argument (k_inc_stream_arg,
+// k_inc_lat_arg): a batch step that is one launch then uploads nothing
+constexpr int DESC_ARG_MAX = 8;
+struct DescArg {
+  GPDesc d[DESC_ARG_MAX];
+};
 // bordered append + one-pass predict in one launch; max_blocks = max over GPs of nprod + cell tiles
 hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int vf32, hipStream_t s);
 // the same for ONE GP with its descriptor passed by value (kernel argument): no
 // descriptor upload, and with rows_inline no row copies either
 hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s);
+// the same for count <= DESC_ARG_MAX GPs from host descriptors passed by value
+hipError_t launch_inc_stream_arg(const GPDesc* h, int count, int64_t max_blocks, int vf32, hipStream_t s);
 // lattice-separable append + predict (k_inc_lat); max_blocks = max over GPs of
 // nprod + nwu + lat_tiles * ksplit
 hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
-// the same with the `count` <= LAT_ARG_MAX host descriptors `h` passed by value as
-// the kernel argument (no device copy of the descriptor array)
-constexpr int LAT_ARG_MAX = 8;
-struct LatDescArg {
-  GPDesc d[LAT_ARG_MAX];
-};
+// the same with the `count` <= DESC_ARG_MAX host descriptors `h` passed by value as
+// the kernel argument (DescArg: no device copy of the descriptor array)
 hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
 // separable tables and lattice indices of rows [tab_lo, n0); max_rows = max over GPs of n0 - tab_lo
 hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s);

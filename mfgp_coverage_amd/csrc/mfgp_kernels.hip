@@ -2402,6 +2402,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
   inc_stream_wg<VT>(d);
 }
 
+// A batch of <= DESC_ARG_MAX GPs with the descriptors as the kernel argument
+// (k_inc_lat_arg's reason: no per-step upload through the copy engine); the
+// kernarg segment is indexed directly, a dynamic index into the by-value
+// parameter would copy it to scratch.
+template <class VT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_stream_arg(
+    const DescArg a) {
+  (void)a;
+  const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
+  inc_stream_wg<VT>(descs[blockIdx.x]);
+}
+
 #include "mfgp_lattice.inl"
 
 // MFGP_F32 full predict: k_predict computed V in fp64 into the scratch d.V (the
@@ -2513,6 +2525,14 @@ hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int
   else hipLaunchKernelGGL(k_inc_stream<double>, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
+hipError_t launch_inc_stream_arg(const GPDesc* h, int count, int64_t max_blocks, int vf32, hipStream_t s) {
+  if (count < 1 || count > DESC_ARG_MAX) return hipErrorInvalidValue;
+  DescArg a;
+  std::memcpy(a.d, h, sizeof(GPDesc) * count);
+  if (vf32) hipLaunchKernelGGL(k_inc_stream_arg<float>, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(k_inc_stream_arg<double>, dim3(count, (unsigned)max_blocks), dim3(NT), 0, s, a);
+  return hipGetLastError();
+}
 hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s) {
   if (vf32) hipLaunchKernelGGL(k_inc_stream1<float>, dim3(1, (unsigned)blocks), dim3(NT), 0, s, d);
   else hipLaunchKernelGGL(k_inc_stream1<double>, dim3(1, (unsigned)blocks), dim3(NT), 0, s, d);
@@ -2532,8 +2552,8 @@ hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka
   return hipGetLastError();
 }
 hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s) {
-  if (count < 1 || count > LAT_ARG_MAX) return hipErrorInvalidValue;
-  LatDescArg a;
+  if (count < 1 || count > DESC_ARG_MAX) return hipErrorInvalidValue;
+  DescArg a;
   std::memcpy(a.d, h, sizeof(GPDesc) * count);
   const dim3 g(count, (unsigned)max_blocks);
   if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat_arg<8, float>), g, dim3(NT), 0, s, a);

@@ -1041,14 +1041,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
 }
 
 // The same step with the batch's descriptors as a by-value kernel argument (up
-// to LAT_ARG_MAX of them, 9 KB): a step that needs no other kernel takes no
+// to DESC_ARG_MAX of them, 9 KB): a step that needs no other kernel takes no
 // per-step upload of its descriptor array. That upload is a host-to-device copy
 // on the copy engine, and its hand-off back to the compute queue put ~16 us of
 // idle stream time between consecutive steps (kernel trace: k_inc_lat ->
 // k_inc_lat gaps of 21 us under rocprofv3).
 template <int KA, class VT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_lat_arg(
-    const LatDescArg a) {
+    const DescArg a) {
   // index the kernarg segment itself: a dynamic index into the by-value argument
   // would copy all 9 KB of it to scratch
   (void)a;

@@ -30,7 +30,7 @@ def report():
 
 def _stream(rep):
     ks = {n: r for n, r in rep.items() if any(s in n for s in STREAM)}
-    assert len(ks) == 6, sorted(rep)   # <double> and <float> of each (k_inc_stream, k_inc_stream1, k_vstream)
+    assert len(ks) == 8, sorted(rep)   # <double> and <float> of k_inc_stream, k_inc_stream1, k_inc_stream_arg, k_vstream
     return ks
 
 

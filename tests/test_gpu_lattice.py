@@ -258,11 +258,13 @@ def test_lattice_after_hyp_change_rebuilds():
     assert st["lattice"] == 2 and st["full_factor"] == 2, st
 
 
-def test_lattice_descriptors_by_value_equal_upload(monkeypatch):
-    """A batch step that is one k_inc_lat launch passes its descriptors as the
-    kernel argument (k_inc_lat_arg, no descriptor upload); MFGP_LAT_ARG=0 makes
-    a context upload them instead. Same kernel body, so the same bits; ragged
-    batch of 1, 3 and 8 GPs (LAT_ARG_MAX) over several steps, fused argmax."""
+@pytest.mark.parametrize("lattice", ["force", False])
+def test_lattice_descriptors_by_value_equal_upload(monkeypatch, lattice):
+    """A batch step that is one k_inc_lat (or, lattice off, k_inc_stream) launch
+    passes its descriptors as the kernel argument (k_inc_lat_arg /
+    k_inc_stream_arg, no descriptor upload); MFGP_DESC_ARG=0 makes a context
+    upload them instead. Same kernel body, so the same bits; ragged batches of
+    1, 3 and 8 GPs (DESC_ARG_MAX) over several steps, fused argmax."""
     import torch
     from mfgp_coverage_amd import _lib
     hyp = _hyp("australia8_mf")
@@ -291,17 +293,20 @@ def test_lattice_descriptors_by_value_equal_upload(monkeypatch):
                                       vmax_ptr=vmax.data_ptr(), vargmax_ptr=vam.data_ptr())
             data = [(X, y, n + k) for X, y, n in data]
             out.append((mu.cpu().numpy(), var.cpu().numpy(), vmax.cpu().numpy(), vam.cpu().numpy()))
-        assert all(m.stats()["lattice"] == 4 for m in models), [m.stats() for m in models]
+        key = "lattice" if lattice else "vstream"
+        assert all(m.stats()[key] >= 4 for m in models), [m.stats() for m in models]
+        if not lattice:
+            assert all(m.stats()["lattice"] == 0 for m in models)
         ctx.synchronize()
         return out
 
     for B in (1, 3, 8):
         a = _lib.Context(0)
-        a.set_lattice("force")
-        monkeypatch.setenv("MFGP_LAT_ARG", "0")
+        a.set_lattice(lattice)
+        monkeypatch.setenv("MFGP_DESC_ARG", "0")
         b = _lib.Context(0)
-        monkeypatch.delenv("MFGP_LAT_ARG")
-        b.set_lattice("force")
+        monkeypatch.delenv("MFGP_DESC_ARG")
+        b.set_lattice(lattice)
         ra, rb = run(a, B), run(b, B)
         for sa, sb in zip(ra, rb):
             for xa, xb in zip(sa, sb):
