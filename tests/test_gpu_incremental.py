@@ -615,3 +615,33 @@ def test_destroy_before_synchronize():
     mu_a, var_a = a.predict()
     mu_r, var_r = _ref("mf", X[:44], y[:44], 20, Xs, hyp)
     assert _err(mu_a, var_a, mu_r, var_r, hyp) < TOL
+
+
+def test_capacity_growth_clamped_to_full_predict_limit():
+    """capacity grows by 1.5x on appends; from N ~ 13,000 that would pass
+    the full predict's limit (ld <= 16383, include/mfgp_hip.h) and a later full
+    predict (here: after a grid change) would fail although N fits. The growth is
+    clamped to that limit, so the full predict after the appends runs and agrees
+    with a model built from the same rows in one set_data."""
+    from mfgp_coverage_amd import _lib
+    rng = np.random.default_rng(21)
+    N0, k = 13000, 16
+    X = rng.random((N0 + 3 * k, 2))
+    y = np.sin(4 * X[:, 0]) * np.cos(3 * X[:, 1]) + 0.1 * rng.standard_normal(X.shape[0])
+    hyp = HYP_SF
+    ctx = _lib.context()
+    m = _lib.Model(ctx, _lib.SF, hyp, 1e-8)
+    m.set_grid(_grid(16))
+    m.set_data(np.empty((0, 2)), np.empty(0), X[:N0], y[:N0])
+    m.predict()
+    for s in range(3):
+        m.append(X[N0 + s * k:N0 + (s + 1) * k], y[N0 + s * k:N0 + (s + 1) * k])
+    Xs2 = _grid(12)
+    m.set_grid(Xs2)
+    mu, var = m.predict()             # full predict at N = 13,048
+    ref = _lib.Model(ctx, _lib.SF, hyp, 1e-8)
+    ref.set_grid(Xs2)
+    ref.set_data(np.empty((0, 2)), np.empty(0), X, y)
+    mu_r, var_r = ref.predict()
+    assert np.all(np.isfinite(mu)) and np.all(np.isfinite(var))
+    assert _err(mu, var, mu_r, var_r, hyp) < 1e-8
