@@ -11,12 +11,14 @@ per-seed max-variance trajectory (the VarMax log, simulator.py:925) is
 all-gathered over RCCL for the loss/variance aggregation of runner.py:144-147.
 
 Two update paths are timed back to back on the same workload, with identical
-results (tests/test_gpu_incremental.py):
-  value          -- the library's default path: ONE launch per step
-                    (k_inc_stream): producer workgroups append the k rows to the
-                    factor (bordered Cholesky; L21 gathered from the resident
-                    V = L^-1 psi^T), the cell tiles stream V once for mean and
-                    variance at every cell, picking L21 / L22 up in-kernel;
+results (tests/test_gpu_incremental.py, tests/test_gpu_lattice*.py):
+  value          -- the library's default path: ONE launch per step. On the
+                    headline's lattice grid that is the lattice-separable step
+                    (k_inc_lat_arg): bordered-Cholesky
+                    append, w = K11^-1 K12 from the resident L^-1, the separable
+                    SE kernel turns L21 V_old into a K = 2 ny GEMM, and mean /
+                    variance are updated from the resident posterior; elsewhere
+                    the one-pass V stream (k_inc_stream);
   full_recompute -- what the reference does per update: full refactor
                     (k_assemble/potrf/panel/syrk) and V recomputed from scratch
                     (k_predict).
@@ -31,12 +33,14 @@ headline (configs[3] sizes, fp64).
 --gpus N without a torch.distributed launcher: the process starts N ranks itself
 (python -m torch.distributed.run as a child; this process never touches the GPU)
 and exits with their status. Under a launcher WORLD_SIZE must equal N.
-roofline (value): k_inc_stream, HBM-bound; algorithmic bytes per launch =
-  B x 8 x [M (n0 + k + 4) + n0 (3k + 1)] (V_old read once; V_new, mu, var
-  written; grid read; L21 gathered from V, written to A and read back; z once)
-  over its average duration from HIP events on the launch stream, every 8th
-  step of the timed region sampled (an event pair costs a few microseconds of
-  stream time); peak = MI355X HBM3E 8 TB/s.
+The timed region holds exactly the K steps (a barrier + device synchronisation
+on both sides, no HIP events inside); the trajectory gather runs after it and is
+reported on its own (gather_ms).
+roofline (value): the step's kernel, HBM-bound (k_inc_lat: F's lower triangle
+  streamed once, the posterior in / out, the new V rows, the Z rows; k_inc_stream:
+  the resident V read once) over its average launch time from HIP events on the
+  launch stream around each launch of an untimed pass after the timed region;
+  peak = MI355X HBM3E 8 TB/s.
 roofline (full_recompute): k_predict, MFMA-bound; B x (M N^2 + 4 M N) f64 flops
   per launch; peak = MI355X f64 MFMA spec.
 cpu_baseline: the oracle's diag-only NumPy restatement (Cholesky, triangular
@@ -61,12 +65,6 @@ PEAK_F64_TFLOPS = 78.6   # MI355X f64 matrix (= vector) spec
 PEAK_HBM_GBS = 8000.0    # MI355X HBM3E
 FUSED = os.environ.get("MFGP_FUSED", "1") != "0"
 F32_RTOL = 1e-4          # oracle.gp_oracle.F32_TOL: incremental vs full VarMax in the fp32 mode
-
-
-def timing_stride(steps):
-    """Events bracket every stride-th launch of the timed region (an event pair
-    costs a few microseconds of stream time), at least 8 launches sampled."""
-    return max(1, min(8, steps // 8))
 
 
 def launch_plan(gpus, env):
@@ -170,17 +168,19 @@ def cpu_baseline(wl, hyp, s, NL, NH0, k, reps=5):
     """Time the oracle on one seed's update (same inputs as step s): one untimed
     warm-up, then the median of `reps` updates."""
     from oracle import gp_oracle as O
-    threads = _blas_threads()
     XH = np.vstack([wl.XH[:NH0], wl.Xnew[s]])
     yH = np.concatenate([wl.yH[:NH0], wl.ynew[s]])
-    O.mf_diag(wl.XL, wl.yL, XH, yH, hyp, wl.xs)   # warm-up (BLAS threads, page faults)
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        O.mf_diag(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
-        ts.append(time.perf_counter() - t0)
+    with blas_all_cores():
+        threads = _blas_threads()
+        O.mf_diag(wl.XL, wl.yL, XH, yH, hyp, wl.xs)   # warm-up (BLAS threads, page faults)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            O.mf_diag(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
+            ts.append(time.perf_counter() - t0)
+    avail, aff, quota = host_cores()
     out = {"value": 1.0 / float(np.median(ts)), "unit": "GP-updates/s", "cores": int(threads), "kind": "port",
-           "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "nproc": os.cpu_count(), "affinity_cores": aff, "cgroup_cpu_quota": quota, "cpu_model": cpu_model(),
            "sample": f"oracle.mf_diag (Cholesky + triangular solves + row-sum, fp64 NumPy/BLAS, {threads} BLAS "
                      f"threads), 1 seed x {reps} updates after one warm-up at the full config "
                      f"(M={wl.xs.shape[0]}, N={NL + NH0 + k}), median"}
@@ -206,12 +206,13 @@ def cpu_baseline_sampled(wl, hyp, s, NL, NH0, k, cells=4096, reps=3):
     rest per cell). Median of `reps`."""
     import scipy.linalg as sla
     from oracle import gp_oracle as O
-    threads = _blas_threads()
     XH = np.vstack([wl.XH[:NH0], wl.Xnew[s]])
     yH = np.concatenate([wl.yH[:NH0], wl.ynew[s]])
     M = wl.xs.shape[0]
     sub = wl.xs[np.random.default_rng(0).choice(M, cells, replace=False)]
     tf, tc = [], []
+    lim = blas_all_cores()
+    threads = _blas_threads()
     for _ in range(reps + 1):
         t0 = time.perf_counter()
         K = O.mf_K(wl.XL, XH, hyp)
@@ -223,12 +224,29 @@ def cpu_baseline_sampled(wl, hyp, s, NL, NH0, k, cells=4096, reps=3):
         t2 = time.perf_counter()
         tf.append(t1 - t0)
         tc.append(t2 - t1)
+    lim.restore_original_limits()
     t = float(np.median(tf[1:])) + float(np.median(tc[1:])) * M / cells
     return {"value": 1.0 / t, "unit": "GP-updates/s", "cores": int(threads), "kind": "port",
             "nproc": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": f"oracle.mf_diag steps (fp64 NumPy/BLAS, {threads} BLAS threads) for 1 seed at N={NL + NH0 + k}: "
                       f"K + Cholesky at full N, psi / triangular solve / row-sums for {cells} of the M={M} cells, "
                       f"scaled to M; median of {reps} after one warm-up"}
+
+
+def host_cores():
+    """The host cores this process may run on: the scheduler affinity, capped by a
+    cgroup CPU quota when one is set (a GPU box shares its host: os.cpu_count()
+    reports every core of the machine, the quota what this job gets)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
 
 
 def _blas_threads():
@@ -239,14 +257,22 @@ def _blas_threads():
         return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
+def blas_all_cores():
+    """Context manager: BLAS threads = every host core available."""
+    from threadpoolctl import threadpool_limits
+    return threadpool_limits(limits=host_cores()[0], user_api="blas")
+
+
 def cpu_faithful(wl, hyp, XH, yH, reps=3):
     from oracle import gp_oracle as O
     ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        O.mf_faithful(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
-        ts.append(time.perf_counter() - t0)
-    return {"value": 1.0 / float(np.median(ts)), "unit": "GP-updates/s",
+    with blas_all_cores():
+        threads = _blas_threads()
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            O.mf_faithful(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
+            ts.append(time.perf_counter() - t0)
+    return {"value": 1.0 / float(np.median(ts)), "unit": "GP-updates/s", "cores": int(threads),
             "sample": "oracle.mf_faithful (the reference's op sequence: dense K(X*,X*), 4x np.linalg.solve, "
                       f"dense psi@beta), median of {reps} updates at the full config"}
 
@@ -345,11 +371,8 @@ def main():
             step(s)
         aggregate(varmax[:W].transpose(0, 1).contiguous())   # first-use kernel loads / communicator setup
         ctx.synchronize()
-        # HIP events around every stride-th predict launch inside the timed region
-        stride = timing_stride(K)
-        ctx.enable_timing(not os.environ.get("MFGP_NO_TIMING"), predict_only=True)
-        ctx.set_timing_stride(stride)
-        ctx.reset_timing()
+        # the timed region: exactly K steps, nothing else on the stream (no HIP events)
+        ctx.enable_timing(False)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -359,13 +382,27 @@ def main():
             th = time.perf_counter()
             step(s)
             host_t.append(time.perf_counter() - th)
-        traj = varmax[W:].transpose(0, 1).contiguous()           # [B, K] per-seed VarMax trajectory
-        agg = aggregate(traj)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
+        # the job's one exchange (the per-seed VarMax trajectories, runner.py:144-147),
+        # once per job: timed on its own, not part of the per-step rate
+        traj = varmax[W:].transpose(0, 1).contiguous()           # [B, K] per-seed VarMax trajectory
+        tg0 = time.perf_counter()
+        agg = aggregate(traj)
+        torch.cuda.synchronize(dev)
+        tg1 = time.perf_counter()
         ctx.synchronize()   # raises LinAlgError if any factor was not positive definite
+        # the kernel's launch time (roofline): R more untimed steps on the same
+        # inputs, HIP events around every launch on the launch stream
+        R = min(K, 50) if incremental else min(K, 3)
+        ctx.enable_timing(True, predict_only=True)
+        ctx.set_timing_stride(1)
+        ctx.reset_timing()
+        for s in range(W, W + R):
+            step(s)
+        ctx.synchronize()
         tm = ctx.timing()
         # per-stage breakdown: a few more (untimed) steps with every stage bracketed by events
         ctx.enable_timing(True)
@@ -377,15 +414,15 @@ def main():
         ctx.synchronize()
         tb = ctx.timing()
         ctx.enable_timing(False)
-        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        el = torch.tensor([t1 - t0, tg1 - tg0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         if not diag_lib:   # diagnostic library builds compute garbage on purpose
             assert torch.isfinite(agg).all()
         st = models[0].stats()
         del models
-        return {"elapsed": float(el.item()), "tm": tm, "host_ms": 1e3 * float(np.mean(host_t)), "stats": st,
-                "traj": traj.cpu().numpy(), "stride": stride,
+        return {"elapsed": float(el[0].item()), "gather_ms": 1e3 * float(el[1].item()), "tm": tm,
+                "host_ms": 1e3 * float(np.mean(host_t)), "stats": st, "traj": traj.cpu().numpy(), "R": R,
                 "breakdown": {"predict": tb["predict_ms"] / nb_steps, "factor": tb["factor_ms"] / nb_steps}}
 
     inc = run(True, W, K)
@@ -459,7 +496,8 @@ def main():
                     "frac": lat_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": kern, "bytes_per_launch": lat_bytes, "flops_per_launch": lat_flops,
                     "mfma_tflops": lat_tf, "avg_launch_ms": v_ms, "launches_timed": tm["predict_launches"],
-                    "timing": f"HIP events around every {inc['stride']}th launch of the timed region",
+                    "timing": f"HIP events around each of {inc['R']} launches of an untimed pass after the timed "
+                              "region (no events inside the timed region)",
                     "design_note": "bytes = F's lower triangle (the w pass), the posterior in / out, the new V rows "
                                    "and the Z rows; the launch is a chain of dependent phases (producers -> w -> "
                                    "Z -> GEMM -> cells), latency- not bandwidth-bound (DESIGN.md section 2.4)"}
@@ -472,7 +510,8 @@ def main():
                     "frac": v_gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": kern, "bytes_per_launch": vbytes, "avg_launch_ms": v_ms,
                     "launches_timed": tm["predict_launches"],
-                    "timing": f"HIP events around every {inc['stride']}th launch of the timed region",
+                    "timing": f"HIP events around each of {inc['R']} launches of an untimed pass after the timed "
+                              "region (no events inside the timed region)",
                     "design_bytes_note": f"{es}-byte V: bytes_per_launch = the resident V read once plus the new "
                                          "rows, grid, outputs and per-row L21 / z terms (DESIGN.md section 4)"}
         if default_cfg:
@@ -515,6 +554,7 @@ def main():
                         "peak by construction; the roofline above is the kernel's own work",
             },
             "host_enqueue_ms_per_step": inc["host_ms"],
+            "gather_ms": inc["gather_ms"],
             "breakdown_ms_per_step": inc["breakdown"],
         }
         if full is not None:

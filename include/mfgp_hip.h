@@ -48,6 +48,10 @@ typedef struct mfgp_model mfgp_model;
 /* One context per host thread: owns a HIP stream and a scratch workspace. */
 int mfgp_ctx_create(int device, mfgp_ctx** out);
 void mfgp_ctx_destroy(mfgp_ctx* ctx);
+/* Give back the context's scratch (the fp64 V scratch of MFGP_F32 full predicts,
+ * up to 16 GB, and the workspace) after synchronising; the next call that needs
+ * it allocates it again. Models keep their resident state. */
+int mfgp_ctx_trim(mfgp_ctx* ctx);
 /* Launch on a caller stream (hipStream_t) instead of the context's own. NULL restores it. */
 int mfgp_ctx_set_stream(mfgp_ctx* ctx, void* hip_stream);
 void* mfgp_ctx_get_stream(mfgp_ctx* ctx);
@@ -140,7 +144,10 @@ int64_t mfgp_model_m(const mfgp_model* m);
 /* Path introspection (tests / benchmarks): out[0..n) = {factor rows (-1 = none),
  * resident V rows, full refactors, bordered appends, full predicts, one-pass
  * predicts (V stream or lattice step), grid lattice axes nx, ny (0 = the grid is
- * not a lattice: appends locate new points by a scan), lattice steps}. */
+ * not a lattice: appends locate new points by a scan), lattice steps, off-lattice
+ * training rows of the last lattice step (read back from the device; synchronises
+ * the context's stream; only when n > 9), lattice steps launched with their
+ * descriptors as the kernel argument}. */
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n);
 /* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
 int mfgp_get_factor(mfgp_model* m, double* L_out);

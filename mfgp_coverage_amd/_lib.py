@@ -26,6 +26,7 @@ _c_int64_p = ctypes.POINTER(ctypes.c_int64)
 SIGNATURES = {
     "mfgp_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "mfgp_ctx_destroy": (None, [ctypes.c_void_p]),
+    "mfgp_ctx_trim": (ctypes.c_int, [ctypes.c_void_p]),
     "mfgp_ctx_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "mfgp_ctx_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "mfgp_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
@@ -141,6 +142,11 @@ class Context:
 
     def synchronize(self):
         check(lib().mfgp_ctx_synchronize(self.handle))
+
+    def trim(self):
+        """Free the context's scratch (the MFGP_F32 full predict's fp64 V scratch and
+        the workspace); models keep their state."""
+        check(lib().mfgp_ctx_trim(self.handle))
 
     def set_stream(self, stream_ptr):
         check(lib().mfgp_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
@@ -283,11 +289,14 @@ class Model:
         """{factor_rows, v_rows, full_factor, inc_factor, full_predict, vstream} (path
         counters; vstream counts every one-pass predict, lattice steps included), the
         grid's lattice axes {lattice_nx, lattice_ny} (0: not a lattice) and {lattice}:
-        the steps that took the lattice-separable path (k_inc_lat)."""
-        out = (ctypes.c_int64 * 9)()
-        check(lib().mfgp_model_stats(self.handle, out, 9))
+        the steps that took the lattice-separable path (k_inc_lat); {lattice_virtual}: the
+        off-lattice training rows (extra K rows) the last lattice step ran, as its
+        device counters hold them (MF: summed over both kernel parts); {lattice_arg}:
+        the lattice steps launched with their descriptors by value (k_inc_lat_arg)."""
+        out = (ctypes.c_int64 * 11)()
+        check(lib().mfgp_model_stats(self.handle, out, 11))
         keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream",
-                "lattice_nx", "lattice_ny", "lattice")
+                "lattice_nx", "lattice_ny", "lattice", "lattice_virtual", "lattice_arg")
         return dict(zip(keys, (int(v) for v in out)))
 
     def sample_points(self, threshold, max_points):

@@ -160,6 +160,7 @@ struct mfgp_model {
   bool pred_since_append = false;   // a predict came after the last append
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0, n_lattice = 0;
+  int64_t n_lattice_arg = 0;   // lattice steps launched with their descriptors by value (k_inc_lat_arg)
   // state generation: a new factor from scratch, a new grid or new hyperparameters
   // start a new one (the resident posterior, F and the tables belong to one)
   uint64_t gen = 1;
@@ -778,12 +779,17 @@ int assign_predict_scratch(mfgp_ctx* c, GPDesc* hd, int count) {
   for (int i = 0; i < count; ++i) per = std::max(per, v64_bytes(hd[i]));
   per = (per + 255) / 256 * 256;
   if (per == 0) return MFGP_OK;
-  const int g = (int)std::max<size_t>(1, std::min<size_t>((size_t)count, F32_SCRATCH / per));
+  int g = (int)std::max<size_t>(1, std::min<size_t>((size_t)count, F32_SCRATCH / per));
   if (per * g > c->vscr_bytes) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->vscr) HIP_TRY(hipFree(c->vscr));
     c->vscr = nullptr;
     c->vscr_bytes = 0;
+    // at most half of the free HBM (the resident state of the models comes first);
+    // mfgp_ctx_trim gives the scratch back
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && per * g > fr / 2)
+      g = (int)std::max<size_t>(1, std::min<size_t>((size_t)g, fr / 2 / per));
     HIP_TRY(hipMalloc(&c->vscr, per * g));
     c->vscr_bytes = per * g;
   }
@@ -1158,6 +1164,18 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
   if (c->h_ring) (void)hipHostFree(c->h_ring);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
+}
+
+int mfgp_ctx_trim(mfgp_ctx* c) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->vscr) HIP_TRY(hipFree(c->vscr));
+  c->vscr = nullptr;
+  c->vscr_bytes = 0;
+  if (c->ws) HIP_TRY(hipFree(c->ws));
+  c->ws = nullptr;
+  c->ws_bytes = 0;
+  return MFGP_OK;
 }
 
 int mfgp_ctx_set_stream(mfgp_ctx* c, void* s) {
@@ -1604,9 +1622,21 @@ int64_t mfgp_model_n(const mfgp_model* m) { return m ? m->NL + m->NH : -1; }
 
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
   if (!m || !out) return set_err(MFGP_ERR_ARG, "null model/out");
-  const int64_t v[9] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
-                        m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice};
-  for (int i = 0; i < n && i < 9; ++i) out[i] = v[i];
+  // off-lattice training rows the last lattice step's Z units found (lidx = -1,
+  // the step's "virtual" K rows): the counts they published, read back from the
+  // device (both parts; an MF hifi row off the lattice counts in each)
+  int64_t virt = 0;
+  if (n > 9 && m->zvl && m->n_lattice > 0) {
+    int nv[2] = {0, 0};
+    HIP_TRY(hipStreamSynchronize(m->ctx->stream));
+    HIP_TRY(hipMemcpy(&nv[0], m->zvl, sizeof(int), hipMemcpyDeviceToHost));
+    if (m->kind == MFGP_MF) HIP_TRY(hipMemcpy(&nv[1], m->zvl + m->zb_rows + 1, sizeof(int), hipMemcpyDeviceToHost));
+    virt = (int64_t)nv[0] + nv[1];
+  }
+  const int64_t v[11] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+                         m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice, virt,
+                         m->n_lattice_arg};
+  for (int i = 0; i < n && i < 11; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
@@ -1895,9 +1925,11 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       if (res_b[0] >= 0) res_tag(m, res_b[0], m->v_n, 0);
       continue;
     }
+    bool lat_arg = false;
     if (do_factor && lat && nfull == 0 && ninc == nb && np == nv && desc_arg_ok(c, hd, ninc)) {
       // the whole step is one k_inc_lat launch: its descriptors go by value
       if ((rc = enqueue_inc_lat_arg(c, hd, ninc))) return rc;
+      lat_arg = true;
     } else if (do_factor && fuse && !lat && nfull == 0 && ninc == nb && np == nv && c->desc_arg &&
                ninc <= DESC_ARG_MAX) {
       // the whole step is one k_inc_stream launch (append + one-pass predict)
@@ -1923,6 +1955,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       if (res_b[i] >= 0) res_tag(m, res_b[i], m->v_n, (lat && i < ninc) ? res_depth[i] : 0);
       if (lat && i < ninc) {
         m->n_lattice += 1;
+        if (lat_arg) m->n_lattice_arg += 1;
         m->F_n = m->v_n;   // F's new rows and the new rows' tables came with the step
         m->F_gen = m->gen;
         m->tab_n = m->v_n;

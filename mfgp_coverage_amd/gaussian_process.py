@@ -132,7 +132,6 @@ class _DeviceGP:
             self.__dict__["_model"] = m
             self.__dict__["_synced"] = None
             self.__dict__["_grid"] = None
-            self.__dict__["_grid_src"] = None
             self.__dict__["_hyp_pushed"] = None
         return m
 
@@ -147,29 +146,16 @@ class _DeviceGP:
         self._dev().set_hyp(h, self.jitter)
         self.__dict__["_hyp_pushed"] = key
 
-    @staticmethod
-    def _grid_sample(xs):
-        flat = xs.reshape(-1)
-        return flat[::max(1, flat.shape[0] // 256)].tobytes() + flat[-2:].tobytes()
-
     def _grid_to_device(self, X_star):
-        # the simulator passes the same x_star array to every predict (sim:671, 884):
-        # the same object with the same strided sample skips the exact compare of
-        # all M cells (an in-place edit of X_star that leaves every sampled value
-        # unchanged is not seen; a new or reshaped array always takes the compare)
+        # every predict compares all M cells of X_star with the grid the device
+        # holds (a private copy): an in-place edit of the caller's array, anywhere,
+        # moves the device to the new grid (the reference evaluates the kernel on
+        # whatever X_star holds at the call, gp:139 / gp:426-429); ~10-20 us at M = 16384
         g = self.__dict__.get("_grid")
-        last = self.__dict__.get("_grid_src")
-        if g is not None and last is not None and last[0] is X_star and isinstance(X_star, np.ndarray) \
-                and X_star.shape == last[1] and X_star.__array_interface__["data"][0] == last[2] \
-                and self._grid_sample(_as2(X_star)) == last[3]:
-            return
         xs = _as2(X_star)
         if g is None or g.shape != xs.shape or not np.array_equal(g, xs):
             self._dev().set_grid(xs)
             self.__dict__["_grid"] = xs.copy()
-        if isinstance(X_star, np.ndarray):
-            self.__dict__["_grid_src"] = (X_star, X_star.shape, X_star.__array_interface__["data"][0],
-                                          self._grid_sample(xs))
 
     def _predict_dev(self, X_star):
         self._sync_data()
@@ -220,9 +206,6 @@ class _DeviceGP:
         memo[id(self)] = new
         for k, v in self.__dict__.items():
             if k == "_model":
-                continue
-            if k == "_grid_src":   # the caller's X_star, held for the identity check only
-                new.__dict__[k] = None
                 continue
             new.__dict__[k] = copy.deepcopy(v, memo)
         m = self.__dict__.get("_model")

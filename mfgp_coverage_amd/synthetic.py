@@ -46,7 +46,12 @@ class Workload:
     """One Monte-Carlo seed: a grid, a lofi prior set, a hifi set and a stream of
     per-step agent samples (k new hifi points per update)."""
 
-    def __init__(self, G, NL, NH, k, steps, seed):
+    def __init__(self, G, NL, NH, k, steps, seed, revisit=0.0):
+        """revisit: the fraction of each step's k samples taken at cells sampled
+        before (the base hifi set or earlier steps, the same cell twice in one step
+        allowed), with fresh noise -- the reference's Todescato loop re-samples an
+        explorer's current cell (simulator.py:872-891), so its training sets hold
+        repeated rows. 0 (default) keeps every hifi cell distinct."""
         rng = np.random.default_rng(seed)
         self.xs = grid(G)
         M = self.xs.shape[0]
@@ -60,5 +65,19 @@ class Workload:
         self.XH = self.xs[ih[:NH]]
         self.yH = truth[ih[:NH]] + 0.1 * rng.standard_normal(NH)
         inew = ih[NH:]
+        if revisit > 0 and steps * k:
+            # a separate stream, so that revisit = 0 draws exactly the data above
+            rr = np.random.default_rng(seed + 7919)
+            inew = inew.reshape(steps, k).copy()
+            nrep = int(round(revisit * k))
+            for s in range(steps):
+                seen = np.concatenate([ih[:NH], inew[:s].reshape(-1)])
+                if seen.size == 0:
+                    continue
+                slots = rr.choice(k, nrep, replace=False)
+                inew[s, slots] = seen[rr.integers(0, seen.size, nrep)]
+                if nrep >= 2 and s % 3 == 0:
+                    inew[s, slots[1]] = inew[s, slots[0]]   # two agents in one cell
+            inew = inew.reshape(-1)
         self.Xnew = self.xs[inew].reshape(steps, k, 2)
         self.ynew = (truth[inew] + 0.1 * rng.standard_normal(inew.shape[0])).reshape(steps, k)

@@ -217,10 +217,13 @@ def parity_errors_f32(mu, var, mu_ref, var_ref, kss):
     stored and streamed in fp32, everything else fp64) against this fp64 oracle.
     Returns (mu_err, var_err):
 
-    mu:  max |d| / max(|ref|, 1e-2 * max|ref|) -- fp32 storage of V puts an
-         absolute error of ~1e-8 on mu (2^-24 per V entry times |V^T z|); the
+    mu:  max |d| / max(|ref|, 1e-2 * max|ref|, 1e-300) -- fp32 storage of V puts
+         an absolute error of ~1e-8 on mu (2^-24 per V entry times |V^T z|); the
          posterior mean of a [0, 1] field crosses zero, so the relative bound is
-         floored at 1 % of the field's largest |mu|;
+         floored at 1 % of the field's largest |mu|: where |ref| is below that
+         floor the gate F32_TOL is an ABSOLUTE bound of F32_TOL * 1e-2 * max|mu_ref|
+         (1e-6 * max|mu_ref|), elsewhere relative; an all-zero mu_ref is compared
+         against the 1e-300 floor (finite, never nan);
     var: max |d| / max(|ref|, 1e-6 * k**), the fp64 metric.
     Measured on australia9 (128x128, N = 2048, numpy emulation of the kernels'
     arithmetic): fp32 V alone 7e-7 / 3e-7; with the f32 accumulation of
@@ -232,7 +235,7 @@ def parity_errors_f32(mu, var, mu_ref, var_ref, kss):
     var_ref = np.asarray(var_ref, dtype=np.float64).reshape(-1)
     if not mu.size:
         return 0.0, 0.0
-    mden = np.maximum(np.abs(mu_ref), 1e-2 * np.max(np.abs(mu_ref)))
+    mden = np.maximum(np.maximum(np.abs(mu_ref), 1e-2 * np.max(np.abs(mu_ref))), 1e-300)
     vden = np.maximum(np.abs(var_ref), 1e-6 * kss)
     return float(np.max(np.abs(mu - mu_ref) / mden)), float(np.max(np.abs(var - var_ref) / vden))
 

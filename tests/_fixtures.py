@@ -10,6 +10,9 @@ REPLAY_RUNS = (
     "atc24_todescato_nsf", "atc24_todescato_hsf", "atc24_todescato_hmf",
     "atc24_choi_hmf", "atc248_todescato_hmf",
     "australia6_todescato_nsf", "australia6_todescato_hmf",
+    # priors partly off the grid's lattice, revisited cells (make_golden.py REPLAYS)
+    "australia2_todescato_hsf", "australia2_todescato_hmf",
+    "australia4_todescato_hsf", "australia4_todescato_hmf",
 )
 
 

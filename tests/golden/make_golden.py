@@ -129,6 +129,14 @@ REPLAYS = {
     "atc248_todescato_hmf": ("anti_two_corners", "anti_two_corners_mf_hyp.csv", "anti_two_corners_prior.csv", (3,)),
     "australia6_todescato_nsf": ("australia6", "australia6_sf_hyp.csv", None, (0,)),
     "australia6_todescato_hmf": ("australia6", "australia6_mf_hyp.csv", "australia6_prior.csv", (0,)),
+    # priors partly off the grid's lattice (distribution.py:112-113 builds them by
+    # float steps: australia2 has 17 of 81 rows 1 ulp off the grid's axis values,
+    # australia4 11 of 36) and revisited cells (australia4_todescato_hsf: 40 samples
+    # at 13 distinct cells; simulator.py:872-891 re-samples an explorer's cell)
+    "australia2_todescato_hsf": ("australia2", "australia2_sf_hyp.csv", "australia2_prior.csv", (0, 1)),
+    "australia2_todescato_hmf": ("australia2", "australia2_mf_hyp.csv", "australia2_prior.csv", (0, 1)),
+    "australia4_todescato_hsf": ("australia4", "australia4_sf_hyp.csv", "australia4_prior.csv", (0,)),
+    "australia4_todescato_hmf": ("australia4", "australia4_mf_hyp.csv", "australia4_prior.csv", (0,)),
 }
 
 
@@ -152,6 +160,26 @@ def make_replay_fixtures():
             out[f"s{sim}_sample_y"] = s.Sample.values.astype(np.float64)
         np.savez_compressed(os.path.join(OUT, f"replay_{run}.npz"), **out)
         print("wrote replay", run)
+
+
+def make_prior_fixtures():
+    """7. ``priors_offlattice.npz``: the reference's priors that lie partly off the
+    grid's lattice (distribution.py:112-113 steps the prior positions by float
+    additions, so some coordinates end 1 ulp away from the grid's axis values,
+    e.g. 0.6000000000000001 against 0.6), with the native 51x51 grid they come
+    with (``<name>_hifi.csv``) and the trained hyperparameters. CSV extraction."""
+    out = {}
+    for name in ("australia2", "australia3", "australia4", "australia9"):
+        out[name + "_prior"] = _csv(name + "_prior.csv")
+        out[name + "_grid"] = _csv(name + "_hifi.csv")[:, :2].copy()
+        out[name + "_hyp_sf"] = _csv(name + "_sf_hyp.csv")[0]
+        out[name + "_hyp_mf"] = _csv(name + "_mf_hyp.csv")[0]
+        g = out[name + "_grid"]
+        ax, ay = np.unique(g[:, 0]), np.unique(g[:, 1])
+        P = out[name + "_prior"]
+        off = ~(np.isin(P[:, 0], ax) & np.isin(P[:, 1], ay))
+        print(name, "prior rows", P.shape[0], "off the lattice", int(off.sum()))
+    np.savez_compressed(os.path.join(OUT, "priors_offlattice.npz"), **out)
 
 
 def _import_simulator():
@@ -328,6 +356,10 @@ def make_log_headers():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["replays"]:   # CSV extraction only (no reference code)
+        make_replay_fixtures()
+        make_prior_fixtures()
+        sys.exit(0)
     gp = _import_reference()
     make_reference_fixture(gp)
     make_replay_fixtures()

@@ -72,6 +72,43 @@ def test_no_cpu_fallback(lib):
         m.predict(np.zeros((4, 2)))
 
 
+@pytest.mark.gpu
+def test_inplace_grid_edit_is_seen(lib):
+    """The simulator passes the same x_star array to every predict (sim:671, 884);
+    an in-place edit of ONE cell of that same array, anywhere, must move the
+    next predict to the edited grid (gp:139 evaluates the kernel on X_star as it
+    is at the call) -- and back when the edit is undone."""
+    from oracle import gp_oracle as O
+    from mfgp_coverage_amd.gaussian_process import SFGP
+    from mfgp_coverage_amd.synthetic import HYP, grid
+    hyp = HYP["australia3_sf"]
+    xs = grid(64)
+    rng = np.random.default_rng(4)
+    X = xs[rng.choice(xs.shape[0], 150, replace=False)]
+    y = rng.standard_normal((150, 1))
+    m = SFGP(X.copy(), y.copy(), 1)
+    m.hyp = hyp.copy()
+    m.updt_info(m.X, m.y)
+    mu0, cov0 = m.predict(xs)
+    for cell in (1237, 4095, 0):   # cells no strided sample of the array would hit first
+        old = xs[cell].copy()
+        xs[cell] = (0.123456789, 0.987654321)   # the same array object, edited in place
+        mu, cov = m.predict(xs)
+        mu_r, var_r = O.sf_diag(X, y, hyp, xs)
+        assert max(O.parity_errors(mu[:, 0], np.diag(cov), mu_r, var_r, O.prior_variance(hyp))) < O.PARITY_TOL
+        assert mu[cell, 0] != mu0[cell, 0]
+        xs[cell] = old
+        mu, cov = m.predict(xs)
+        np.testing.assert_array_equal(mu, mu0)
+        np.testing.assert_array_equal(np.diag(cov), np.diag(cov0))
+    # an append between predicts (the simulator's step) still sees an edit
+    m.updt(xs[5:7], np.zeros((2, 1)))
+    xs[77] = (0.5, 0.55555)
+    mu, cov = m.predict(xs)
+    mu_r, var_r = O.sf_diag(np.vstack([X, grid(64)[5:7]]), np.vstack([y, np.zeros((2, 1))]), hyp, xs)
+    assert max(O.parity_errors(mu[:, 0], np.diag(cov), mu_r, var_r, O.prior_variance(hyp))) < O.PARITY_TOL
+
+
 def test_diagcov_semantics():
     from mfgp_coverage_amd.gaussian_process import DiagCov
     v = np.array([0.1, 0.5, 0.2])

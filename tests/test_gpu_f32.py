@@ -169,18 +169,21 @@ def test_f32_mirror_precision_attribute():
     _check(mu[:, 0], np.diag(cov), mu_r, var_r, hyp)
 
 
-def test_configs4_f32_batch_vs_oracle(L):
-    """BASELINE configs[4] sizes: 256x256 grid (M = 65536), N = 4096 lofi + 4096
-    hifi, australia9 MF, a batch of 8 GPs in fp32: the full factor + predict
-    (set_data, batch_predict), then three incremental steps of 8 new hifi rows
-    per GP (one k_inc_stream<float> launch each), with the fused var max. Two
-    GPs are checked against the oracle at every step on 2048 sampled cells plus
-    the new samples' cells and the device argmax; every GP's fused VarMax must
-    equal the max of its variance."""
+@pytest.mark.parametrize("B", [8, 32])
+def test_configs4_f32_batch_vs_oracle(L, B):
+    """BASELINE configs[4]: 256x256 grid (M = 65536), N = 4096 lofi + 4096 hifi,
+    australia9 MF, fp32 (MFGP_F32), at the config's own batch of 32 GPs per GPU
+    and at 8: the full factor + predict (set_data, batch_predict), then three
+    incremental steps of 8 new hifi rows per GP -- each ONE lattice-step launch
+    (gp:401-438 / 493-529 via DESIGN.md section 2.4): k_inc_lat_arg (descriptors
+    as the kernel argument) for 8 GPs, k_inc_lat (descriptors uploaded) for 32;
+    the path counters assert which ran. The fused var max of every GP must equal
+    the max of its variance; two GPs are checked against the oracle at every step
+    on 2048 sampled cells plus the new samples' cells and the device argmax."""
     import torch
     from mfgp_coverage_amd.synthetic import Workload
     hyp, _ = _hyp()
-    B, G, NL, NH0, k, steps = 8, 256, 4096, 4088, 8, 3
+    G, NL, NH0, k, steps = 256, 4096, 4088, 8, 3
     wls = [Workload(G, NL, NH0, k, steps, seed=100 + s) for s in range(B)]
     M = G * G
     ctx = L.context()
@@ -224,5 +227,9 @@ def test_configs4_f32_batch_vs_oracle(L):
             w = wls[i]
             mu_r, var_r = O.mf_diag(w.XL, w.yL, XH[i], yH[i], hyp, w.xs[pick])
             _check(mu[i, pick], var[i, pick], mu_r, var_r, hyp)
-    st = models[0].stats()
-    assert st["inc_factor"] == steps and st["vstream"] == steps and st["full_predict"] == 1, st
+    for m in models:
+        st = m.stats()
+        assert st["inc_factor"] == steps and st["vstream"] == steps and st["full_predict"] == 1, st
+        assert st["lattice"] == steps and st["lattice_arg"] == (steps if B <= 8 else 0), st
+    del models
+    ctx.trim()   # the fp64 scratch of the fp32 full predict (16 GB) is not kept

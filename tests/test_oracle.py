@@ -196,3 +196,16 @@ def test_oracle_nlml_vs_reference():
         fd = fx[c + "_fdgrad"]
         tol = 1e-3 if c.endswith("h0") else 1e-5
         assert np.all(np.abs(g - fd) <= tol * np.maximum(np.abs(fd), 1.0)), (c, g, fd)
+
+
+def test_parity_errors_f32_degenerate_reference():
+    """parity_errors_f32 stays finite for an all-zero reference mean (the 1 % floor
+    is then 0; the 1e-300 floor keeps the metric defined) and is an absolute bound
+    of 1e-2 * max|mu_ref| below that floor."""
+    z = np.zeros(5)
+    e = O.parity_errors_f32(z, np.full(5, 0.1), z, np.full(5, 0.1), 0.1)
+    assert np.isfinite(e).all() and e == (0.0, 0.0)
+    ref = np.array([1.0, 1e-6, -0.5])
+    got = ref + np.array([0.0, 1e-6, 0.0])            # |d| = 1e-6 where |ref| is below the 1e-2 floor
+    e_mu, _ = O.parity_errors_f32(got, np.ones(3), ref, np.ones(3), 1.0)
+    assert abs(e_mu - 1e-6 / 1e-2) < 1e-12
