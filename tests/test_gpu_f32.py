@@ -230,6 +230,8 @@ def test_configs4_f32_batch_vs_oracle(L, B):
     for m in models:
         st = m.stats()
         assert st["inc_factor"] == steps and st["vstream"] == steps and st["full_predict"] == 1, st
-        assert st["lattice"] == steps and st["lattice_arg"] == (steps if B <= 8 else 0), st
+        # the first step also builds F, the tables and the axis tables (uploaded
+        # descriptors); the next ones are single launches: by value for <= 8 GPs
+        assert st["lattice"] == steps and st["lattice_arg"] == (steps - 1 if B <= 8 else 0), st
     del models
     ctx.trim()   # the fp64 scratch of the fp32 full predict (16 GB) is not kept

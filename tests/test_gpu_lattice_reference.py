@@ -83,16 +83,19 @@ def test_lattice_replays_logged_runs(run):
         assert max(O.parity_errors(mu[:, 0], np.diag(cov), mu_r, var_r, O.prior_variance(hyp))) < TOL
         st = m._dev().stats()
         ks = np.array([np.sum(fx[f"s{sim}_sample_iter"] == it) for it in fx[f"s{sim}_iters"]])
+        # an append of >= 1 row is a lattice step once a predict has run on >= 1
+        # training row before it (the resident posterior of its old rows)
+        rows = (prior.shape[0] if prior is not None else 0) + np.cumsum(ks)
+        eligible = int(np.sum((ks[1:] > 0) & (rows[:-1] >= 1)))
         if _gate_ok(hyp):
-            # every append of >= 1 row after the first predict is a lattice step
-            assert st["lattice"] == int(np.sum(ks[1:] > 0)) > 0, (st, ks)
+            assert st["lattice"] == eligible > 0, (st, ks)
             X_all = m.X if hyp.shape[0] == 4 else np.vstack([m.X_L, m.X_H])
             off = _off_lattice(X_all, grid)
             assert off == (_off_lattice(prior[:, :2], grid) if prior is not None else 0)
             assert st["lattice_virtual"] == off, (st, off)
         else:
             assert st["lattice"] == 0, st   # anti_two_corners: refused, the V stream ran
-            assert st["vstream"] >= int(np.sum(ks[1:] > 0)), st
+            assert st["vstream"] >= eligible, st
 
 
 @pytest.mark.parametrize("name,kind", [("australia3", "sf"), ("australia3", "mf"), ("australia9", "mf")])
