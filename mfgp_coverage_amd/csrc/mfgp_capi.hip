@@ -99,6 +99,7 @@ struct mfgp_ctx {
   bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
+  int lat_wr = 0;             // row parts per block of its w units (0: chosen per launch; MFGP_LAT_WR, diagnostics)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
@@ -144,6 +145,7 @@ struct mfgp_model {
   void* V = nullptr;
   int64_t vld = 0, vtiles = 0, v_n = 0;
   double* tred = nullptr;     // [vtiles][2] per-tile (max, argmax) of var, then the tiles' arrival counter
+  int64_t tred_n = 0;         // doubles of tred
   unsigned* sync = nullptr;   // k_inc_stream hand-off words {arrivals, L21 ready, L22 ready} (zeroed)
   unsigned epoch = 0;         // last k_inc_stream epoch of this model
   // the compact bordered rows in iscr (inc_l21c_offset) hold rows [l21c_n0, l21c_N)
@@ -183,7 +185,7 @@ struct mfgp_model {
   int64_t wv_ld = 0;
   unsigned* wflag = nullptr;  // [wv_ld / 64 + 2]
   unsigned* wcnt = nullptr;   // [wv_ld / 64 + 2]
-  double* wpart = nullptr;    // [lat_wunits(wv_ld, LAT_WCH_MIN)][1024]
+  double* wpart = nullptr;    // [wv_ld / 64 + 1][2][LAT_WR_MAX][512]
   double* gpart = nullptr;    // split-K partials
   size_t gpart_n = 0;
   unsigned* gcnt = nullptr;   // per GEMM tile
@@ -427,6 +429,7 @@ int ensure_v(mfgp_model* m) {
     HIP_TRY(hipMalloc(&m->tred, sizeof(double) * (4 * tiles + 1)));
     HIP_TRY(hipMemsetAsync(m->tred, 0, sizeof(double) * (4 * tiles + 1), s));
     HIP_TRY(hipStreamSynchronize(s));
+    m->tred_n = 4 * tiles + 1;
   }
   m->vtiles = tiles;
   return MFGP_OK;
@@ -638,18 +641,29 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     HIP_TRY(hipMemsetAsync(m->wv, 0, sizeof(double) * ld * KINC, s));
     HIP_TRY(hipMalloc(&m->wflag, sizeof(unsigned) * (ld / 64 + 2)));
     HIP_TRY(hipMemsetAsync(m->wflag, 0, sizeof(unsigned) * (ld / 64 + 2), s));   // below every epoch
-    HIP_TRY(hipMalloc(&m->wcnt, sizeof(unsigned) * (ld / 64 + 2)));
-    HIP_TRY(hipMemsetAsync(m->wcnt, 0, sizeof(unsigned) * (ld / 64 + 2), s));
-    HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 1024 * lat_wunits(ld, LAT_WCH_MIN)));
+    HIP_TRY(hipMalloc(&m->wcnt, sizeof(unsigned) * 2 * (ld / 64 + 2)));
+    HIP_TRY(hipMemsetAsync(m->wcnt, 0, sizeof(unsigned) * 2 * (ld / 64 + 2), s));
+    HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 512 * 2 * LAT_WR_MAX * (ld / 64 + 1)));
     m->wv_ld = ld;
   }
-  if (m->gcnt_n < tiles) {
+  if (m->gcnt_n != tiles) {
+    // [tiles] arrival counters of the splits | [tiles] flags (the epoch once all arrived)
     HIP_TRY(hipStreamSynchronize(s));
     if (m->gcnt) HIP_TRY(hipFree(m->gcnt));
     m->gcnt = nullptr;
-    HIP_TRY(hipMalloc(&m->gcnt, sizeof(unsigned) * tiles));
-    HIP_TRY(hipMemsetAsync(m->gcnt, 0, sizeof(unsigned) * tiles, s));
+    HIP_TRY(hipMalloc(&m->gcnt, sizeof(unsigned) * 2 * tiles));
+    HIP_TRY(hipMemsetAsync(m->gcnt, 0, sizeof(unsigned) * 2 * tiles, s));   // flags below every epoch
     m->gcnt_n = tiles;
+  }
+  // the fused var max / argmax: one (max, argmax) slot per GEMM workgroup
+  if (m->tred && 2 * tiles * ksplit + 1 > m->tred_n) {
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipFree(m->tred));
+    m->tred = nullptr;
+    const int64_t nd = 2 * tiles * ksplit + 1;
+    HIP_TRY(hipMalloc(&m->tred, sizeof(double) * nd));
+    HIP_TRY(hipMemsetAsync(m->tred, 0, sizeof(double) * nd, s));
+    m->tred_n = nd;
   }
   if (!m->axt || m->axt_w != tabw) {
     HIP_TRY(hipStreamSynchronize(s));
@@ -1134,6 +1148,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
+  if (const char* e = std::getenv("MFGP_LAT_WR")) c->lat_wr = std::max(0, std::min(LAT_WR_MAX, std::atoi(e)));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
     const int v = std::atoi(e);
@@ -1839,16 +1854,23 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       // (split s takes every S-th stage: at least 4 each)
       S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nst_min / 4));
       if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, nst_min));
-      // rows of F per w unit: the largest chunk that still gives ~2 units per CU (w
-      // is latency-bound per unit: one round trip per 128 rows)
-      int64_t wch = LAT_WCH_MIN;
-      for (int64_t t = LAT_WCH_MAX; t > LAT_WCH_MIN; t /= 2) {
+      // a power of two (the splits share the tile's cell passes), and with S > 1 every
+      // GEMM workgroup of the launch resident at once (the splits of a tile wait for
+      // each other): tiles x S within two workgroups per CU
+      {
+        int p2 = 1;
+        while (2 * p2 <= S) p2 *= 2;
+        S = p2;
+        while (S > 1 && tiles_sum * S > 2 * (int64_t)c->ncu) S /= 2;
+      }
+      // row parts per block of F: one per w unit while the block pairs alone give a
+      // unit per CU (B >= 8 at the headline), more for smaller batches (partials)
+      int wr = 1;
+      {
         int64_t units = 0;
-        for (int i = 0; i < ninc; ++i) units += lat_wunits(hd[i].n0, t);
-        if (units >= 2 * c->ncu) {
-          wch = t;
-          break;
-        }
+        for (int i = 0; i < ninc; ++i) units += lat_wunits(hd[i].n0, 1);
+        while (wr < LAT_WR_MAX && units * wr < c->ncu) wr *= 2;
+        if (c->lat_wr > 0) wr = std::min(c->lat_wr, LAT_WR_MAX);
       }
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
@@ -1874,8 +1896,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.ksplit = S;
         fd.lat_tiles = (int)tiles;
         fd.nwb = (int)((fd.n0 + 63) / 64);
-        fd.wch = wch;
-        fd.nwu = (int)lat_wunits(fd.n0, wch);
+        fd.wr = wr;
+        fd.nwu = (int)lat_wunits(fd.n0, wr);
         fd.wpart = m->wpart;
         fd.wcnt = m->wcnt;
         fd.lat_fbuild = (m->F_gen == m->gen && m->F_n >= fd.n0) ? 0 : 1;

@@ -118,10 +118,10 @@ struct GPDesc {
   int lat_tiles;       // GEMM tiles per GP: ceil(nx / (64 / ka)) * ceil(ny / 64)
   int nwb;             // 64-row blocks of w: ceil(n0 / 64)
   int lat_fbuild;      // k_trinv_f: 1 = compute F for the n0 factor rows
-  int nwu;             // w work units: 64-column blocks x wch-row chunks (lat_wunits(n0, wch))
-  int64_t wch;         // rows of F per w unit
-  double* wpart;       // the units' partial w blocks [nwu][16 x 64]
-  unsigned* wcnt;      // per 64-row block of w: arrivals of its units (zero between launches)
+  int nwu;             // w work units: block pairs x 2 column halves x wr row parts (lat_wunits(n0, wr))
+  int wr;              // row parts per block of F (1: no partials; the host raises it for small batches)
+  double* wpart;       // the row parts' partial w halves [64-column blocks][2 halves][LAT_WR_MAX][32 x 16]
+  unsigned* wcnt;      // per (64-column block, half): arrivals of its row parts (zero between launches)
   // lattice-axis form of the step (every term on the lattice's own axis values)
   double* axt;         // axis tables [4][tabw + 1][tabw]: exp(-(a_p - a_col)^2 / 2 l^2) of the grid's
                        // axis values, x then y, L then H lengthscale; row tabw: zeros
@@ -140,22 +140,17 @@ struct GPDesc {
   Hyp hp;              // hyperparameters of predict (predict time)
 };
 
-// lattice step: w is computed in units of 64 columns x wch rows of F's lower
-// triangle (column block jb: rows [64 jb, n0) in chunks), top block first; wch is
-// one of LAT_WCH_MIN .. LAT_WCH_MAX (powers of two), chosen per launch by the host
-constexpr int64_t LAT_WCH_MIN = 256, LAT_WCH_MAX = 1024;
+// lattice step: w is computed by units of one PAIR of 64-column blocks of F's
+// lower triangle (block p and block nwb - 1 - p: rows [64 p, n0) and [64 (nwb - 1
+// - p), n0), about n0 + 64 rows together, so every pair streams the same number
+// of bytes) x one 32-column half x one of wr row parts of each block
+constexpr int LAT_WR_MAX = 8;
 constexpr int ZKS = 8;   // lattice-axis GEMM: K rows per pipeline stage (Z / axis-table rows)
 // F's column block jb starts at fblk_off(jb, ld): blocks b < jb hold ld - 64 b rows of 64
 inline __host__ __device__ int64_t fblk_off(int64_t jb, int64_t ld) { return 64 * jb * ld - 2048 * jb * (jb - 1); }
 inline __host__ __device__ int64_t fblk_size(int64_t ld) { return fblk_off(ld / 64, ld); }
-inline __host__ __device__ int64_t lat_wunits_block(int64_t n0, int64_t jb, int64_t wch) {
-  return (n0 - 64 * jb + wch - 1) / wch;
-}
-inline __host__ __device__ int64_t lat_wunits(int64_t n0, int64_t wch) {
-  int64_t u = 0;
-  for (int64_t jb = 0; jb * 64 < n0; ++jb) u += lat_wunits_block(n0, jb, wch);
-  return u;
-}
+inline __host__ __device__ int64_t lat_wpairs(int64_t n0) { return ((n0 + 63) / 64 + 1) / 2; }
+inline __host__ __device__ int64_t lat_wunits(int64_t n0, int64_t wr) { return lat_wpairs(n0) * 2 * wr; }
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
 inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
 inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1) / PBM; }

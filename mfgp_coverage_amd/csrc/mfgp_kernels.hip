@@ -468,6 +468,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const double* base, 
 __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, double* dst, unsigned voff, unsigned soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr)dst, 16, voff, soff, 0, 0);
 }
+// the same with the sc1 cache policy (aux 16): served by L2, never by a possibly
+// stale line of this CU's L1 -- for bytes another workgroup stored in this launch
+__device__ __forceinline__ void dma_buf_sc1(__amdgpu_buffer_rsrc_t rs, double* dst, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr)dst, 16, voff, soff, 0, 16);
+}
 
 
 // Main-loop accumulator: wave wm owns rows wm*32.. x all 64 cells.

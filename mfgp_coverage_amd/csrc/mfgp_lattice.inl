@@ -29,12 +29,15 @@
 //
 // One launch per batch, grid (GPs, roles); per GP the roles are
 //   [0, nprod)                 producers + finish, exactly as k_inc_stream's
-//   [nprod, nprod + nwu)       w units (64 rows of w x wch rows of F, top
-//                              block first): wait for the compact rows of their
-//                              rows, then w[j][a] = sum_{i >= j} F[i][j] L21c[i][a]
-//                              on MFMA; the block's last unit adds the chunks,
-//                              write-through + drain + wflag[jb] = epoch; then a
-//                              share of the new rows' separable tables
+//   [nprod, nprod + nwu)       w units (a pair of 64-column blocks of F, the
+//                              top block and the bottom one, x a 32-column half
+//                              x a row part): wait for the compact rows, then
+//                              w[j][a] = sum_{i >= j} F[i][j] L21c[i][a] on
+//                              MFMA; store w (or a partial: the last row part
+//                              adds them), count it into ldone; then F's new rows
+//                              and a share of the new rows' separable tables
+//   [.., + nzu)                Z units: wait for all of w, sum w c ex per lattice
+//                              row (the GEMM's A rows)
 //   [.., + tiles * ksplit)     GEMM tiles: 64 (a, ix) rows x 64 iy columns, the
 //                              term blocks in descending order (the order w
 //                              becomes ready), split ksplit ways over the terms;
@@ -173,27 +176,13 @@ __device__ __forceinline__ double l21c_at(const double* l21c, int64_t i, int a) 
   else return (double)gp(reinterpret_cast<const float*>(l21c))[i * KINC + a];
 }
 
-// w unit u (in role order: column blocks from the top, chunks of wch rows
-// within a block): its block jb, chunk c, the block's first unit u0 and units nc.
-__device__ __forceinline__ void lat_wunit(int64_t n0, int64_t nwb, int64_t wch, int64_t u, int64_t& jb,
-                                          int64_t& c, int64_t& u0, int64_t& nc) {
-  u0 = 0;
-  for (jb = nwb - 1; jb > 0; --jb) {
-    nc = lat_wunits_block(n0, jb, wch);
-    if (u < u0 + nc) break;
-    u0 += nc;
-  }
-  nc = lat_wunits_block(n0, jb, wch);
-  c = u - u0;
-}
-
 // L22^-1 (rows / columns >= k zero) into Li [16][16] from the L22 record (sync[2]
-// must have been seen; plain loads: no line of the record is read in this launch
-// before that flag). L22 is scratch [16][16 | 16].
+// must have been seen; L2-served loads: the finish stored it in this launch).
+// L22 is scratch [16][16 | 16].
 __device__ __forceinline__ void lat_l22inv(const GPDesc& d, int k, double* L22, double* Li) {
   const int tid = threadIdx.x;
   for (int e = tid; e < KINC * KINC; e += NT) {
-    const double v = d.l22r[e];
+    const double v = ldx<true>(d.l22r + e);
     L22[e] = (e / KINC < k && e % KINC <= e / KINC) ? v : 0.0;
   }
   __syncthreads();
@@ -213,180 +202,257 @@ __device__ __forceinline__ void lat_l22inv(const GPDesc& d, int k, double* L22, 
   __syncthreads();
 }
 
-// One w unit: columns j = 64 jb + [0, 64) of w = F11^T L21^T, rows i of chunk c
-// of [64 jb, n0) -- F's lower triangle below the block. Each wave takes 32 of
-// every 128 rows and all 64 columns: lane (r, q) loads F[i][64 jb + 16 cb + r]
-// (four 128-byte lines per load, F row-major) for cb = 0..3 and the compact row
-// entry L21c[i][r] once for all four (MFMA A = L21c, B = F), so 80 VGPRs hold
-// 16 KB of F per wave in flight. The waves' sums meet in LDS in wave order. A
-// block of one chunk stores w itself; otherwise each chunk stores its partial
-// and the last of the block to arrive adds them in chunk order. Either way the
-// block's flag is raised once w is stored; then the same workgroup writes F's
-// new rows for the block, -L22^-1 w^T (and the top block's unit L22^-1).
+// Row part rp of R of w's column block jb: rows [lo, hi) of [64 jb, n0), in parts
+// of a multiple of 16 rows (one MFMA step of the workgroup's four waves).
+__device__ __forceinline__ void lat_wpart_rows(int64_t n0, int64_t jb, int R, int rp, int64_t& lo, int64_t& hi) {
+  const int64_t L = n0 - 64 * jb;
+  const int64_t cs = ((L + R - 1) / R + 15) / 16 * 16;
+  lo = 64 * jb + rp * cs;
+  hi = lo + cs < n0 ? lo + cs : n0;
+  if (lo > hi) lo = hi;
+}
+
+// Compact row i, entry a (written by the producers in this launch: an L2-served
+// load of the agent scope, never a possibly stale L1 line).
+template <class VT>
+__device__ __forceinline__ double l21c_ld(const double* l21c, int64_t i, int a) {
+  if constexpr (sizeof(VT) == 8) {
+    return __hip_atomic_load(gp(l21c) + i * KINC + a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    return (double)__hip_atomic_load(gp(reinterpret_cast<const float*>(l21c)) + i * KINC + a, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// One w unit: w = F11^T L21^T, w[j][a] = sum_{i >= j} F[i][j] L21c[i][a], for the
+// 32-column half h of the PAIR of column blocks (p, nwb - 1 - p), row part rp of
+// each (the pair's two blocks hold ~n0 + 64 rows together, so every unit streams
+// the same bytes of F and they all end together). Per 16-row step each wave takes
+// 4 rows: lane (r, q) loads L21c[i][r] (the MFMA A operand, a = r) and F[i][32 h +
+// 2 r + c] for c = 0, 1 (B, one 16-byte load: the row's 256-byte half), RG steps per
+// batch, two batches in flight (registers, no LDS): the first batch of F is issued
+// before the wait for the compact rows. At the end of a block the waves' sums
+// meet in LDS in wave order; with one row part the unit stores its w half itself,
+// else each part stores a partial and the last of the block half's R parts adds
+// them in part order. Whoever stored a w half counts it into ldone[0] (the Z units
+// wait for all 2 nwb halves), then writes F's new rows for its columns,
+// -L22^-1 w^T (the top block's h = 0 unit also the L22^-1 entries).
 template <class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
+  constexpr int RG = 6;            // 16-row steps per batch
+  constexpr int WB = 16 * RG;      // rows per batch (the four waves)
   const int64_t n0 = d.n0, ld = d.ld;
-  int64_t jb, c, u0, nc;
-  const int64_t wch = d.wch;
-  lat_wunit(n0, d.nwb, wch, u, jb, c, u0, nc);
-  const int64_t i_lo = 64 * jb + wch * c;
-  const int64_t i_hi = i_lo + wch < n0 ? i_lo + wch : n0;
+  const int nwb = d.nwb, R = d.wr;
+  const int64_t p = u / (2 * R);
+  const int h = (int)((u / R) & 1), rp = (int)(u % R);
+  const int64_t blk0 = p, blk1 = nwb - 1 - p;
+  const int nblk = blk0 < blk1 ? 2 : 1;
   const double* const l21c = d.l21c;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, q = lane >> 4;
+  const unsigned epoch = d.epoch;
   WTRACE(0);
   // a share of the new rows' separable tables (read from the next launch on)
   const int k = (int)(d.N - n0);
-  const int64_t tabw = d.tabw, tstride = (d.ld) * tabw;
-  const int64_t tot = 4 * (int64_t)k * tabw;
-  const int64_t per = (tot + d.nwu - 1) / d.nwu, e0 = u * per;
-  const int64_t e1 = e0 + per < tot ? e0 + per : tot;
-  for (int64_t e = e0 + tid; e < e1; e += NT) {
-    const int t = (int)(e / (k * tabw));
-    const int64_t rem = e % (k * tabw);
-    const int a = (int)(rem / tabw);
-    const int64_t col = rem % tabw;
-    const double* p = row_pt(d, n0 + a);
-    // written through: the GEMM tiles' epilogues read them in this launch (after
-    // the w flags, which follow the drain below)
-    stx<true>(&d.tab[t * tstride + (n0 + a) * tabw + col], lat_tab_value(d, t, n0 + a, col, p[0], p[1]));
+  {
+    const int64_t tabw = d.tabw, tstride = (d.ld) * tabw;
+    const int64_t tot = 4 * (int64_t)k * tabw;
+    const int64_t per = (tot + d.nwu - 1) / d.nwu, e0 = u * per;
+    const int64_t e1 = e0 + per < tot ? e0 + per : tot;
+    for (int64_t e = e0 + tid; e < e1; e += NT) {
+      const int t = (int)(e / (k * tabw));
+      const int64_t rem = e % (k * tabw);
+      const int a = (int)(rem / tabw);
+      const int64_t col = rem % tabw;
+      const double* pt = row_pt(d, n0 + a);
+      // written through: the GEMM tiles' epilogues read them in this launch
+      stx<true>(&d.tab[t * tstride + (n0 + a) * tabw + col], lat_tab_value(d, t, n0 + a, col, pt[0], pt[1]));
+    }
+    // the new rows' lattice indices (read from the next launch on)
+    if (u == 0 && tid < k) {
+      const double* pt = row_pt(d, n0 + tid);
+      d.lidx[n0 + tid] = lattice_xy(d, pt[0], pt[1]);
+    }
   }
-  // the new rows' lattice indices (read from the next launch on)
-  if (u == 0 && tid < k) {
-    const double* p = row_pt(d, n0 + tid);
-    d.lidx[n0 + tid] = lattice_xy(d, p[0], p[1]);
-  }
-  // F[i][64 jb + 16 cb + r] at Fr[(i - 64 jb) * 64 + 16 cb]: the block's rows are contiguous
-  const GLOBAL double* Fr = gp(d.F) + fblk_off(jb, ld) + r;
-  d4 acc[4];
-#pragma unroll
-  for (int x = 0; x < 4; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
-  constexpr int RG = 8;   // 4-row groups per wave per batch (128 rows per batch)
-  double f[RG][4];
-  auto load_f = [&](int64_t i0) {
+  // (scalars, not arrays indexed by the segment: a dynamically indexed local array
+  // lives in scratch, and a scratch load in the loop drains every outstanding load)
+  int64_t lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+  lat_wpart_rows(n0, blk0, R, rp, lo0, hi0);
+  if (nblk == 2) lat_wpart_rows(n0, blk1, R, rp, lo1, hi1);
+  const int64_t nbt0 = (hi0 - lo0 + WB - 1) / WB, nbt1 = (hi1 - lo1 + WB - 1) / WB;
+  const int64_t T = nbt0 + nbt1;
+  // LDS: red [4 w][2 c][4 v][64] | the w halves this unit stored [2][32 jl][16 a] | L22 | Li
+  double* const red = sm;
+  double* const Wh = sm + 2048;
+  double* const L22 = Wh + 2 * 32 * KINC;
+  double* const Li = L22 + KINC * KINC + KINC;
+  static_assert(2048 + 2 * 32 * KINC + 2 * KINC * KINC + KINC <= LAT_LDS, "the w unit's LDS fits");
+  unsigned& wlast = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 10);
+  bool have0 = false, have1 = false;
+  // rows of batch t: segment b (block blk0, then blk1), i = lo + WB s + 16 x + 4 w + q
+  struct Seg {
+    int64_t jb, lo, hi, i0;
+  };
+  auto seg = [&](int64_t t) {
+    const bool b = t >= nbt0;
+    Seg g;
+    g.jb = b ? blk1 : blk0;
+    g.lo = b ? lo1 : lo0;
+    g.hi = b ? hi1 : hi0;
+    g.i0 = g.lo + WB * (t - (b ? nbt0 : 0)) + 4 * w + q;
+    return g;
+  };
+  // lane (r, q) loads columns 32 h + 2 r, 2 r + 1 of a row with ONE 16-byte load
+  // (16 lanes: the row's 256-byte half): MFMA c = 0 takes the even columns, c = 1
+  // the odd ones
+  auto load_f = [&](int64_t t, dv2 (&f)[RG]) {
+    const Seg g = seg(t);
+    const GLOBAL dv2* Fr = reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + fblk_off(g.jb, ld) + 32 * h + 2 * r);
 #pragma unroll
     for (int x = 0; x < RG; ++x) {
-      const int64_t i = i0 + 4 * x + q;
-      const int64_t ii = i < i_hi ? i : i_lo;
+      const int64_t i = g.i0 + 16 * x;
+      const int64_t ii = i < g.hi ? i : g.lo;
       // F is read once per step and would evict the GEMM tiles' tables from L2
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) f[x][cb] = __builtin_nontemporal_load(Fr + (ii - 64 * jb) * 64 + 16 * cb);
+      f[x] = __builtin_nontemporal_load(Fr + (ii - 64 * g.jb) * 32);
     }
   };
-  // (loading the first batch of F before the wait for the compact rows was
-  // tried: f and a live together spill ~85 VGPRs, 144 vs 119 us per launch)
-  const int64_t i_first = i_lo + 32 * w;
-  wait_l21_from(d, i_lo);
+  // (unconditional loads -- a row past the part reloads its first row -- and the
+  // row mask applied at the MFMA: a branch around a load makes the compiler drain
+  // every outstanding load, the next batch's too, before the current one's MFMAs)
+  auto load_a = [&](int64_t t, double (&a)[RG], unsigned& live) {
+    const Seg g = seg(t);
+    live = 0;
+#pragma unroll
+    for (int x = 0; x < RG; ++x) {
+      const int64_t i = g.i0 + 16 * x;
+      live |= (i < g.hi ? 1u : 0u) << x;
+      a[x] = l21c_ld<VT>(l21c, i < g.hi ? i : g.lo, r);
+    }
+  };
+  d4 acc[2];
+  acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+  auto compute = [&](const dv2 (&f)[RG], const double (&a)[RG], unsigned live) {
+#pragma unroll
+    for (int x = 0; x < RG; ++x) {
+      const double av = (live >> x) & 1u ? a[x] : 0.0;
+      acc[0] = mfma(av, f[x].x, acc[0]);
+      acc[1] = mfma(av, f[x].y, acc[1]);
+    }
+  };
+  // the end of block b's rows: the waves' sums in wave order, then w (or a partial)
+  auto block_done = [&](int b) {
+    const int64_t jb = b ? blk1 : blk0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) red[w * 512 + (c * 4 + v) * 64 + lane] = acc[c][v];
+    acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+    __syncthreads();
+    // thread tid: outputs e = tid + 256 m, (jl, a) = (e >> 4, e & 15); lane (rr, g)
+    // register v of acc[c] is w row a = g + 4 v, column jl = 2 rr + c
+    double own[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int e = tid + NT * m, jl = e >> 4, a = e & 15;
+      const int o = ((jl & 1) * 4 + (a >> 2)) * 64 + 16 * (a & 3) + (jl >> 1);
+      own[m] = (red[o] + red[512 + o]) + (red[1024 + o] + red[1536 + o]);
+    }
+    __syncthreads();
+    double* const wv = d.wv + (64 * jb + 32 * h) * KINC;
+    bool stored = true;
+    if (R > 1) {
+      double* const part = d.wpart + ((jb * 2 + h) * LAT_WR_MAX + rp) * 512;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) stx<true>(part + tid + NT * m, own[m]);
+      drain_stores();
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old =
+            __hip_atomic_fetch_add(d.wcnt + jb * 2 + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wlast = old == (unsigned)(R - 1) ? 1u : 0u;
+        if (wlast) __hip_atomic_store(d.wcnt + jb * 2 + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      stored = wlast != 0;
+      if (stored) {
+        // every part's partial, in part order: the same bits whichever arrives last
+        const double* const p0 = d.wpart + (jb * 2 + h) * LAT_WR_MAX * 512;
+        double x[LAT_WR_MAX][2];
+#pragma unroll
+        for (int rr = 0; rr < LAT_WR_MAX; ++rr)
+#pragma unroll
+          for (int m = 0; m < 2; ++m) x[rr][m] = rr < R ? ldx<true>(p0 + rr * 512 + tid + NT * m) : 0.0;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          double t = x[0][m];
+#pragma unroll
+          for (int rr = 1; rr < LAT_WR_MAX; ++rr)
+            if (rr < R) t += x[rr][m];
+          own[m] = t;
+        }
+      }
+    }
+    if (stored) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        stx<true>(wv + tid + NT * m, own[m]);
+        Wh[(b ? 512 : 0) + tid + NT * m] = own[m];
+      }
+      drain_stores();
+      __syncthreads();
+      if (tid == 0) arrive_phase(d.ldone, epoch, 2 * (int64_t)nwb);
+    }
+    if (b) have1 = stored;
+    else have0 = stored;
+  };
+  dv2 fA[RG], fB[RG];
+  double aA[RG], aB[RG];
+  unsigned mA = 0, mB = 0;
+  if (T > 0) load_f(0, fA);   // F does not depend on this launch: before the wait
+  wait_l21_from(d, nblk == 2 && lo1 < lo0 ? lo1 : lo0);
   WTRACE(1);
-#ifndef MFGP_DIAG_LATNOW
-  for (int64_t i0 = i_first; i0 < i_hi; i0 += 128) {
-    load_f(i0);
-    double a[RG];
-#pragma unroll
-    for (int x = 0; x < RG; ++x) {
-      const int64_t i = i0 + 4 * x + q;
-      a[x] = l21c_at<VT>(l21c, i < i_hi ? i : i_lo, r);
-    }
-#pragma unroll
-    for (int x = 0; x < RG; ++x) {
-      const int64_t i = i0 + 4 * x + q;
-      const double av = i < i_hi ? a[x] : 0.0;
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(av, f[x][cb], acc[cb]);
-    }
+  if (nbt0 == 0) block_done(0);
+  if (T > 0) load_a(0, aA, mA);
+  // the next batch's loads are issued unconditionally (past the end: the last batch
+  // again, unused): a branch around them would make the compiler's wait for the
+  // current batch also wait for the next one's loads
+  for (int64_t t = 0; t < T; t += 2) {
+    load_f(t + 1 < T ? t + 1 : T - 1, fB);
+    load_a(t + 1 < T ? t + 1 : T - 1, aB, mB);
+    compute(fA, aA, mA);
+    if (t == nbt0 - 1) block_done(0);
+    if (t + 1 >= T) break;
+    load_f(t + 2 < T ? t + 2 : T - 1, fA);
+    load_a(t + 2 < T ? t + 2 : T - 1, aA, mA);
+    compute(fB, aB, mB);
+    if (t + 1 == nbt0 - 1) block_done(0);
   }
-#endif
+  if (nblk == 2) block_done(1);
   WTRACE(3);
-  // the waves' sums in wave order: lane (r, g) register v of acc[cb] is w row
-  // a = g + 4 v, column jl = 16 cb + r; Wb [64 jl][16 a] after the sum
-  double* const red = sm;             // [4 w][4 cb][4 v][64 lanes]
-  double* const Wb = sm;              // [64][16], once the sums are read
-  double* const L22 = Wb + 64 * KINC;  // [16][16]
-  double* const Li = L22 + KINC * KINC;
-  static_assert(4096 <= LAT_LDS, "the w unit's LDS fits");
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) red[((w * 4 + cb) * 4 + v) * 64 + lane] = acc[cb][v];
-  __syncthreads();
-  double* const wv = d.wv;
-  // thread tid sums outputs e = tid + 256 m: (jl, a) = (e >> 4, e & 15)
-  double own[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int e = tid + NT * m, jl = e >> 4, a = e & 15;
-    const int cb = jl >> 4, rr = jl & 15, v = a >> 2, g = a & 3;
-    const int o = (cb * 4 + v) * 64 + 16 * g + rr;
-    own[m] = (red[o] + red[1024 + o]) + (red[2048 + o] + red[3072 + o]);
-  }
-  __syncthreads();
-  if (nc == 1) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int e = tid + NT * m;
-      stx<true>(&wv[64 * jb * KINC + e], own[m]);
-      Wb[e] = own[m];
-    }
-  } else {
-    double* part = d.wpart + (u0 + c) * 1024;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) stx<true>(part + tid + NT * m, own[m]);
-    drain_stores();
-    __syncthreads();
-    unsigned& wlast = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 10);
-    if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(d.wcnt + jb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      wlast = old == (unsigned)(nc - 1) ? 1u : 0u;
-      if (wlast) __hip_atomic_store(d.wcnt + jb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!wlast) return;
-    // every chunk's partial, 4 chunks' loads in flight at a time, added in chunk order
-    double t[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int64_t c0 = 0; c0 < nc; c0 += 4) {
-      double x[4][4];
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-          x[cc][m] = c0 + cc < nc ? ldx<true>(d.wpart + (u0 + c0 + cc) * 1024 + tid + NT * m) : 0.0;
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) t[m] += x[cc][m];
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int e = tid + NT * m;
-      stx<true>(&wv[64 * jb * KINC + e], t[m]);
-      Wb[e] = t[m];
-    }
-  }
-  drain_stores();
-  __syncthreads();
-  if (tid == 0) {
-    publish(d.wflag + jb, d.epoch);
-    arrive_phase(d.ldone, d.epoch, d.nwb);
-  }
+  if (!have0 && !have1) return;
   WTRACE(2);
-  // F's new rows for this block: F[n0 + a][j] = -sum_{b <= a} L22^-1[a][b] w[j][b]
-  wait_flag(d, d.sync + 2, d.epoch);
+  // F's new rows for the stored halves: F[n0 + a][j] = -sum_{b <= a} L22^-1[a][b] w[j][b]
+  wait_flag(d, d.sync + 2, epoch);
   lat_l22inv(d, k, L22, Li);
-  for (int e = tid; e < 64 * k; e += NT) {
-    const int a = e >> 6, jl = e & 63;
-    const int64_t j = 64 * jb + jl;
-    if (j >= n0) continue;
-    double t = 0.0;
-    for (int b = 0; b <= a; ++b) t -= Li[a * KINC + b] * Wb[jl * KINC + b];
-    d.F[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + jl] = t;
-  }
-  if (jb == d.nwb - 1)
-    for (int e = tid; e < k * k; e += NT) {
-      const int a = e / k, b = e % k;
-      const int64_t j = n0 + b, jb2 = j / 64;
-      if (b <= a) d.F[fblk_off(jb2, ld) + (n0 + a - 64 * jb2) * 64 + j % 64] = Li[a * KINC + b];
+  for (int b = 0; b < nblk; ++b) {
+    if (!(b ? have1 : have0)) continue;
+    const int64_t jb = b ? blk1 : blk0;
+    for (int e = tid; e < 32 * k; e += NT) {
+      const int a = e >> 5, jl = e & 31;
+      const int64_t j = 64 * jb + 32 * h + jl;
+      if (j >= n0) continue;
+      double t = 0.0;
+      for (int bb = 0; bb <= a; ++bb) t -= Li[a * KINC + bb] * Wh[b * 512 + jl * KINC + bb];
+      d.F[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + 32 * h + jl] = t;
     }
+    if (jb == nwb - 1 && h == 0)
+      for (int e = tid; e < k * k; e += NT) {
+        const int a = e / k, bb = e % k;
+        const int64_t j = n0 + bb, jb2 = j / 64;
+        if (bb <= a) d.F[fblk_off(jb2, ld) + (n0 + a - 64 * jb2) * 64 + j % 64] = Li[a * KINC + bb];
+      }
+  }
 }
 
 // Wait (wave 0 polls, the workgroup joins at the barrier) until flags f[0, n)
@@ -593,9 +659,10 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
           const int e = lane + 64 * i;
           const int hh = e / (ZMB * KA), m = (e / KA) % ZMB, a = e % KA;
           v[i] = 0.0;
-          if (e < 2 * ZMB * KA && m0 + m < nm_all[hh]) {
-            const int64_t j = mrow[lo[hh] + m0 + m];
-            v[i] = wv[j * KINC + a] * coef(j);   // (no line of w is read before its flag)
+          // (selects, not a dynamic index into lo / nm_all: those would live in scratch)
+          if (e < 2 * ZMB * KA && m0 + m < (hh ? nm_all[1] : nm_all[0])) {
+            const int64_t j = mrow[(hh ? lo[1] : lo[0]) + m0 + m];
+            v[i] = ldx<true>(&wv[j * KINC + a]) * coef(j);   // L2-served: stored in this launch
           }
         }
 #pragma unroll
@@ -706,6 +773,278 @@ __device__ __forceinline__ void lat_zcompute(const double* slot, d4 (&acc)[2][4]
   }
 }
 
+// The sum of SS split-K partials (in split order) of the accumulator blocks
+// (m, nf + nb): all SS x NBE d4 loads in flight at once (L2-served: the splits
+// stored them in this launch). NBE = 1: only block nf + half (the other is zero).
+template <int SS, int NBP, int NBE>
+__device__ __forceinline__ void lat_psum(const double* p0, int m, int nf, int half, d4 (&tv)[NBP]) {
+  d4 x[SS][NBE];
+#pragma unroll
+  for (int s2 = 0; s2 < SS; ++s2)
+#pragma unroll
+    for (int e = 0; e < NBE; ++e) {
+      const int n = nf + (NBE == NBP ? e : half);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) x[s2][e][v] = ldx<true>(p0 + s2 * LAT_PART + ((m * 4 + n) * 4 + v) * 64);
+    }
+#pragma unroll
+  for (int e = 0; e < NBE; ++e) {
+    d4 t = x[0][e];
+#pragma unroll
+    for (int s2 = 1; s2 < SS; ++s2) t = t + x[s2][e];
+    if constexpr (NBE == NBP) {
+      tv[e] = t;
+    } else {
+#pragma unroll
+      for (int nb = 0; nb < NBP; ++nb) tv[nb] = nb == half ? t : d4{0.0, 0.0, 0.0, 0.0};
+    }
+  }
+}
+
+// The cells of GEMM tile `tile` (the share of split s of S, DESIGN.md section
+// 2.4): T = psi_new - T~ from the accumulators (SPLIT = false, S = 1) or from the
+// splits' stored partials (SPLIT = true; the caller waited until all are stored),
+// v_new = L22^-1 T, var = var_old - |v_new|^2, mu = mu_old + v_new^T z2, the new V
+// rows, and the fused var max / argmax. A separate function per SPLIT, so that the
+// accumulators are dead here once a split has stored them.
+template <int KA, class VT, bool SPLIT>
+__device__ __forceinline__ void lat_epi(const GPDesc& d, int64_t tile, int64_t s, double* sm, const d4 (&acc)[2][4]) {
+  constexpr int IXPT = 128 / KA;   // lattice columns x per tile
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  const GridLattice lat = d.lat;
+  const int64_t ntiy = (lat.ny + 63) / 64;
+  const int64_t tix = tile / ntiy, tiy = tile % ntiy;
+  const int S = d.ksplit;
+  const int64_t ix0 = tix * IXPT, iy0 = tiy * 64;
+  const unsigned epoch = d.epoch;
+  const int64_t n0 = d.n0;
+  const int k = (int)(d.N - n0);
+  const int64_t tiles = d.lat_tiles;
+  const double* p0 = d.gpart + tile * S * LAT_PART + (int64_t)w * 32 * 64 + lane;
+  // the L22 record (raised by the finish long before any K loop ends)
+  wait_flag(d, d.sync + 2, epoch);
+  WTRACE(3);
+  // ---- epilogue (LDS: the ring is dead) ----
+  constexpr int FW = IXPT + 64;
+  constexpr int NBP = KA == 8 ? 2 : 1;      // 16-column blocks per cell pass
+  constexpr int TW = 16 * NBP;              // Ts row width
+  constexpr int NPASS = 2 * (4 / NBP);      // cell passes of the whole tile
+  double* const L22 = sm;                   // [16][16] | z2 [16]
+  double* const Li = L22 + KINC * KINC + KINC;   // L22^-1 [16][16]
+  // psi(cell, new row a) = c_L exL[a][ix] eyL[a][iy] + c_H exH[a][ix] eyH[a][iy]:
+  // the new rows' separable tables (written through by the w units before their
+  // w halves counted in) for the tile's IXPT x 64 cells, [2 kinds][KA][IXPT | 64]
+  double* const Fn = Li + KINC * KINC;
+  double* const Ts = Fn + 2 * KA * FW;      // one cell pass of T: [4 waves][16 rows][TW]
+  double* const amx = Ts + 4 * 16 * TW;     // the waves' (max, argmax) of var
+  static_assert(KINC * KINC + KINC + KINC * KINC + 2 * 8 * (16 + 64) + 4 * 16 * 32 + 8 <= LAT_LDS &&
+                    KINC * KINC + KINC + KINC * KINC + 2 * 16 * (8 + 64) + 4 * 16 * 16 + 8 <= LAT_LDS,
+                "the epilogue's LDS fits the ring's");
+  // this split's share: passes p = s, s + S, ... (S <= NPASS), or half of pass
+  // s / 2 (S = 2 NPASS: one of the pass's two 16-column blocks, KA = 8)
+  const int npass_mine = S <= NPASS ? (int)((NPASS - 1 - s) / S + 1) : 1;
+  const int half = S <= NPASS ? -1 : (int)(s & 1);
+  auto pass_of = [&](int i) { return S <= NPASS ? (int)(s + (int64_t)i * S) : (int)(s >> 1); };
+  const GridLattice latc = lat;
+  const int cw = tid >> 6, cl = tid & 63;
+  const int ch = KA == 8 ? cl >> 5 : 0;
+  const int cyl = KA == 8 ? cl & 31 : cl & 15;
+  // (half >= 0: only the cells of 16-column block `half` of the pass, cyl >> 4)
+  const bool cact = (KA == 8 || cl < 16) && (half < 0 || (cyl >> 4) == half);
+  auto cell_of = [&](int p, int64_t& ix, int64_t& iy) {
+    const int m = p / (4 / NBP), nf = NBP * (p % (4 / NBP));
+    ix = ix0 + (KA == 8 ? 4 * cw + 2 * m + ch : 2 * cw + m);
+    iy = iy0 + 16 * nf + cyl;
+  };
+  auto cell_ok = [&](int64_t ix, int64_t iy) { return cact && ix < latc.nx && iy < latc.ny; };
+  const double* const rmu_in = d.rmu_in;
+  const double* const rvar_in = d.rvar_in;
+  // the old posterior of this thread's cell in each of its passes (resident
+  // from the previous step: plain loads), in flight with the loads below
+  // (S = 1: the first pass's only; the passes prefetch one ahead, registers are short)
+  // (S > 1: each pass loads its cell's with its partials, in one round trip)
+  double ov0 = 0.0, om0 = 0.0;
+  if constexpr (!SPLIT) {
+    int64_t ix, iy;
+    cell_of(0, ix, iy);
+    if (cell_ok(ix, iy)) {
+      const int64_t c = ix * latc.sx + iy * latc.sy;
+      ov0 = rvar_in[c];
+      om0 = rmu_in[c];
+    }
+  }
+  {
+    // one round trip: the record and the new rows' tables (L2-served loads: both
+    // were written in this launch)
+    constexpr int NR = (KINC * KINC + KINC + NT - 1) / NT;
+    constexpr int NF = (2 * KA * FW + NT - 1) / NT;
+    double rv[NR], fv[NF];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int e = tid + NT * i;
+      rv[i] = e < KINC * KINC + KINC ? ldx<true>(d.l22r + e) : 0.0;
+    }
+    const int64_t tstride = d.ld * d.tabw, tabw = d.tabw;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = tid + NT * i;
+      const int kind2 = e / (KA * FW), rem = e % (KA * FW);
+      const int a = rem / FW, col = rem % FW;
+      const bool isx = col < IXPT;
+      const int t = 2 * kind2 + (isx ? 0 : 1);
+      const int64_t idx = isx ? ix0 + col : iy0 + (col - IXPT);
+      fv[i] = (e < 2 * KA * FW && a < k) ? ldx<true>(&d.tab[t * tstride + (n0 + a) * tabw + idx]) : 0.0;
+    }
+    __syncthreads();   // the ring's last reads are done
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int e = tid + NT * i;
+      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+      if (e < KINC * KINC + KINC) L22[e] = use ? rv[i] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+      if (tid + NT * i < 2 * KA * FW) Fn[tid + NT * i] = fv[i];
+  }
+  __syncthreads();
+  if (tid < KINC) {
+    // column c of L22^-1 by forward substitution
+    const int c = tid;
+    double x[KINC];
+#pragma unroll
+    for (int i = 0; i < KINC; ++i) {
+      double t = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int b = 0; b < i; ++b) t -= L22[i * KINC + b] * x[b];
+      x[i] = (i < k && i >= c) ? t / L22[i * KINC + i] : 0.0;
+      Li[i * KINC + c] = x[i];
+    }
+  }
+  WTRACE(5);
+  // ---- cells: per pass (m, group of NBP column blocks) the waves put their
+  // blocks' T into Ts (row rho = g + 4 v of block (m, n) is, for KA = 8, lattice
+  // column h = rho / 8 of the wave's pair and new row a = rho % 8; for KA = 16 new
+  // row a = rho), then thread tid finishes one cell: source wave cw = tid / 64,
+  // (h, column) from the rest. ----
+  double bv = -__builtin_inf();
+  int64_t bi = INT64_MAX;
+  VT* const Vr = const_cast<VT*>(vres_ptr<VT>(d));
+  const int64_t vld = d.vld;
+  double* const omu = d.mu;
+  double* const ovar = d.var;
+  double* const rmu = d.rmu;
+  double* const rvar = d.rvar;
+  // one pass: T of blocks (m, nf .. nf + NBP) into Ts, then this thread's cell
+  auto do_pass = [&](int p, const d4 (&tv)[NBP], double cov, double com) {
+    int64_t ix, iy;
+    cell_of(p, ix, iy);
+    const bool ok = cell_ok(ix, iy);
+    const int64_t c = ix * latc.sx + iy * latc.sy;
+    __syncthreads();   // the previous pass's Ts reads (and Li) are done
+#pragma unroll
+    for (int nb = 0; nb < NBP; ++nb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) Ts[(w * 16 + q + 4 * v) * TW + 16 * nb + r] = tv[nb][v];
+    __syncthreads();
+    if (!ok) return;
+    const int ixc = (int)(ix - ix0), iyc = IXPT + (int)(iy - iy0);
+    const double* const Tc = Ts + (cw * 16 + (KA == 8 ? 8 * ch : 0)) * TW + cyl;
+    VT* const vt = Vr + (c / PBM) * vld * PBM + (c % PBM);
+    double vn[KA];
+    double vs = 0.0, ms = 0.0;
+#pragma unroll
+    for (int a = 0; a < KA; ++a) {
+      vn[a] = 0.0;
+      if (a < k) {
+        const double* fL = Fn + a * FW;
+        const double* fH = Fn + (KA + a) * FW;
+        const double pn = fL[ixc] * fL[iyc] + fH[ixc] * fH[iyc];
+        double t = pn - Tc[a * TW];
+#pragma unroll
+        for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+        vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
+        vs += vn[a] * vn[a];
+        ms += vn[a] * L22[KINC * KINC + a];
+        vt[(n0 + a) * PBM] = (VT)vn[a];
+      }
+    }
+    const double vc = cov - vs;
+    const double mc = com + ms;
+    omu[c] = mc;
+    ovar[c] = vc;
+    if (rmu) {
+      rmu[c] = mc;
+      rvar[c] = vc;
+    }
+    argmax_pair(bv, bi, vc, c);
+  };
+  if constexpr (!SPLIT) {
+    // every pass is this workgroup's; T is in the accumulators (compile-time blocks)
+    double ov = ov0, om = om0;
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      const int m = i / (4 / NBP), nf = NBP * (i % (4 / NBP));
+      d4 tv[NBP];
+#pragma unroll
+      for (int nb = 0; nb < NBP; ++nb) tv[nb] = acc[m][nf + nb];
+      const double cov = ov, com = om;
+      if (i + 1 < NPASS) {
+        int64_t ix, iy;
+        cell_of(i + 1, ix, iy);
+        if (cell_ok(ix, iy)) {
+          const int64_t c = ix * latc.sx + iy * latc.sy;
+          ov = rvar_in[c];
+          om = rmu_in[c];
+        }
+      }
+      do_pass(i, tv, cov, com);
+    }
+  } else {
+    for (int i = 0; i < npass_mine; ++i) {
+      const int p = pass_of(i);
+      const int m = p / (4 / NBP), nf = NBP * (p % (4 / NBP));
+      double cov = 0.0, com = 0.0;
+      {
+        int64_t ix, iy;
+        cell_of(p, ix, iy);
+        if (cell_ok(ix, iy)) {
+          const int64_t c = ix * latc.sx + iy * latc.sy;
+          cov = rvar_in[c];
+          com = rmu_in[c];
+        }
+      }
+      // the splits' partials of blocks (m, nf .. nf + NBP), added in split order
+      d4 tv[NBP];
+      if (S == 2) lat_psum<2, NBP, NBP>(p0, m, nf, half, tv);
+      else if (S == 4) lat_psum<4, NBP, NBP>(p0, m, nf, half, tv);
+      else lat_psum<8, NBP, (NBP == 2 ? 1 : NBP)>(p0, m, nf, half, tv);
+      do_pass(p, tv, cov, com);
+    }
+  }
+  WTRACE(6);
+  if (d.vmax || d.vargmax || d.status_host) {
+    // the waves' (max, argmax) meet in LDS; wave 0 counts the workgroup in
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+    int64_t* const ami = reinterpret_cast<int64_t*>(amx);
+    if (lane == 0) {
+      amx[2 * w] = bv;
+      ami[2 * w + 1] = bi;
+    }
+    __syncthreads();
+    if (w == 0) {
+      bv = amx[0];
+      bi = ami[1];
+#pragma unroll
+      for (int ww = 1; ww < 4; ++ww) argmax_pair(bv, bi, amx[2 * ww], ami[2 * ww + 1]);
+      var_argmax_group(d, bv, bi, tile * S + s, tiles * S);
+    }
+  }
+  WTRACE(4);
+}
+
 // One GEMM tile (split s of ksplit): 128 (a, ix) rows x 64 iy columns, i.e.
 // (128 / KA) x 64 cells, over the K rows of both parts: per part the lattice
 // y-rows q < round_up(ny, ZKS) (A = Z rows, B = axis-table rows ey(q, iy)), then
@@ -753,8 +1092,9 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     const int64_t q0 = (g - (pt ? nsp[0] : 0)) * ZKS;
     double* slot = sm + (t % LNST) * LSTG;
     const int64_t ar = (pt * zrows + q0 + 2 * w) * tabw + ix0;
-    dma_buf(rZ, slot + (2 * w) * 128, vA0, (unsigned)(8 * ar * KA));
-    dma_buf(rZ, slot + (2 * w + 1) * 128, vA1, (unsigned)(8 * (ar + tabw) * KA));
+    // the Z rows were stored in this launch: L2-served (sc1) DMA loads
+    dma_buf_sc1(rZ, slot + (2 * w) * 128, vA0, (unsigned)(8 * ar * KA));
+    dma_buf_sc1(rZ, slot + (2 * w + 1) * 128, vA1, (unsigned)(8 * (ar + tabw) * KA));
     double* bdst = slot + ZKS * 128 + 2 * w * 64;
     if (q0 < zq8) {
       dma_buf(rAx, bdst, vB, (unsigned)(8 * (((2 * pt + 1) * (tabw + 1) + q0 + 2 * w) * tabw + iy0)));
@@ -787,15 +1127,14 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   vm_wait_all();
   __syncthreads();
   WTRACE(2);
-  // the L22 record's flag (sync[2], raised by the finish long before any K loop
-  // ends): read with the partial stores, so the reducer rarely waits for it
-  unsigned& l22_seen = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 11);
-  if (tid == 0)
-    l22_seen = __hip_atomic_load(d.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch ? 1u : 0u;
-  // split-K: partials through memory, the last split reduces them in split order
-  const double* p0 = d.gpart + tile * S * LAT_PART + (int64_t)w * 32 * 64 + lane;
+  // ---- split-K: every split stores its partial; the tile's splits meet (the
+  // last to arrive raises the tile's flag), then split s sums the partials of
+  // ITS share of the tile in split order ((p0 + p1) + p2 ...: the same bits
+  // whichever split computes them) and finishes those cells. The splits of a
+  // tile wait only for each other: the host keeps every GEMM workgroup of the
+  // launch resident together (tiles x S <= the chip's slots) when S > 1.
+  const int64_t tiles = d.lat_tiles;
   if (S > 1) {
-    unsigned& lat_last = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 9);
     double* part = d.gpart + (tile * S + s) * LAT_PART + (int64_t)w * 32 * 64 + lane;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -806,198 +1145,17 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     drain_stores();
     __syncthreads();
     if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(d.gcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lat_last = old == (unsigned)(S - 1) ? 1u : 0u;
-      if (lat_last) __hip_atomic_store(d.gcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!lat_last) return;
-  }
-  __syncthreads();   // l22_seen is thread 0's (S == 1 has no barrier above)
-  if (!l22_seen) wait_flag(d, d.sync + 2, epoch);
-  WTRACE(3);
-  // ---- epilogue (LDS: the ring is dead) ----
-  const int64_t n0 = d.n0;
-  const int k = (int)(d.N - n0);
-  constexpr int FW = IXPT + 64;
-  constexpr int NBP = KA == 8 ? 2 : 1;      // 16-column blocks per cell pass
-  constexpr int TW = 16 * NBP;              // Ts row width
-  double* const L22 = sm;                   // [16][16] | z2 [16]
-  double* const Li = L22 + KINC * KINC + KINC;   // L22^-1 [16][16]
-  // psi(cell, new row a) = c_L exL[a][ix] eyL[a][iy] + c_H exH[a][ix] eyH[a][iy]:
-  // the new rows' separable tables (written through by the w units before their
-  // flags) for the tile's IXPT x 64 cells, [2 kinds][KA][IXPT | 64]
-  double* const Fn = Li + KINC * KINC;
-  double* const Ts = Fn + 2 * KA * FW;      // one cell pass of T: [4 waves][16 rows][TW]
-  static_assert(KINC * KINC + KINC + KINC * KINC + 2 * 8 * (16 + 64) + 4 * 16 * 32 <= LAT_LDS &&
-                    KINC * KINC + KINC + KINC * KINC + 2 * 16 * (8 + 64) + 4 * 16 * 16 <= LAT_LDS,
-                "the epilogue's LDS fits the ring's");
-  {
-    // the record and the new rows' tables (plain loads: no line of them is read in
-    // this launch before sync[2] / the w flags), in flight with the first partial
-    constexpr int NR = (KINC * KINC + KINC + NT - 1) / NT;
-    constexpr int NF = (2 * KA * FW + NT - 1) / NT;
-    double rv[NR], fv[NF];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int e = tid + NT * i;
-      rv[i] = e < KINC * KINC + KINC ? d.l22r[e] : 0.0;
-    }
-    const int64_t tstride = d.ld * d.tabw, tabw = d.tabw;
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int e = tid + NT * i;
-      const int kind2 = e / (KA * FW), rem = e % (KA * FW);
-      const int a = rem / FW, col = rem % FW;
-      const bool isx = col < IXPT;
-      const int t = 2 * kind2 + (isx ? 0 : 1);
-      const int64_t idx = isx ? ix0 + col : iy0 + (col - IXPT);
-      fv[i] = (e < 2 * KA * FW && a < k) ? d.tab[t * tstride + (n0 + a) * tabw + idx] : 0.0;
-    }
-    if (S > 1) {
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) acc[m][n][v] = ldx<true>(p0 + ((m * 4 + n) * 4 + v) * 64);
-    }
-    __syncthreads();   // the ring's last reads are done
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int e = tid + NT * i;
-      const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
-      if (e < KINC * KINC + KINC) L22[e] = use ? rv[i] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < NF; ++i)
-      if (tid + NT * i < 2 * KA * FW) Fn[tid + NT * i] = fv[i];
-  }
-  __syncthreads();
-  if (tid < KINC) {
-    // column c of L22^-1 by forward substitution (while the partials arrive)
-    const int c = tid;
-    double x[KINC];
-#pragma unroll
-    for (int i = 0; i < KINC; ++i) {
-      double t = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int b = 0; b < i; ++b) t -= L22[i * KINC + b] * x[b];
-      x[i] = (i < k && i >= c) ? t / L22[i * KINC + i] : 0.0;
-      Li[i * KINC + c] = x[i];
-    }
-  }
-  // every split's partial (this one's too) from memory, added in split order
-  // (p0 + p1) + p2 ...: the same bits whichever split arrives last
-  for (int s2 = 1; s2 < S; ++s2) {
-    double x[32];
-#pragma unroll
-    for (int e = 0; e < 32; ++e) x[e] = ldx<true>(p0 + s2 * LAT_PART + e * 64);
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) acc[m][n][v] += x[(m * 4 + n) * 4 + v];
-  }
-  __syncthreads();
-  WTRACE(5);
-  // ---- cells: one pass per (m, group of NBP column blocks); the waves put
-  // their blocks' T into Ts (row rho = g + 4 v of block (m, n) is, for KA = 8,
-  // lattice column h = rho / 8 of the wave's pair and new row a = rho % 8; for
-  // KA = 16 new row a = rho), then thread tid finishes one cell: source wave
-  // cw = tid / 64, (h, column) from the rest. ----
-  double bv = -__builtin_inf();
-  int64_t bi = INT64_MAX;
-  VT* const Vr = const_cast<VT*>(vres_ptr<VT>(d));
-  const int64_t vld = d.vld;
-  double* const omu = d.mu;
-  double* const ovar = d.var;
-  double* const rmu = d.rmu;
-  double* const rvar = d.rvar;
-  const double* const rmu_in = d.rmu_in;
-  const double* const rvar_in = d.rvar_in;
-  const int cw = tid >> 6, cl = tid & 63;
-  const int ch = KA == 8 ? cl >> 5 : 0;
-  const int cyl = KA == 8 ? cl & 31 : cl & 15;
-  const bool cact = KA == 8 || cl < 16;
-  constexpr int NPASS = 2 * (4 / NBP);
-  auto cell_of = [&](int p, int64_t& ix, int64_t& iy) {
-    const int m = p / (4 / NBP), nf = NBP * (p % (4 / NBP));
-    ix = ix0 + (KA == 8 ? 4 * cw + 2 * m + ch : 2 * cw + m);
-    iy = iy0 + 16 * nf + cyl;
-  };
-  auto cell_ok = [&](int64_t ix, int64_t iy) { return cact && ix < lat.nx && iy < lat.ny; };
-  // the old posterior of this thread's cell of the next pass, one pass ahead
-  double ov = 0.0, om = 0.0;
-  {
-    int64_t ix, iy;
-    cell_of(0, ix, iy);
-    if (cell_ok(ix, iy)) {
-      const int64_t c = ix * lat.sx + iy * lat.sy;
-      ov = rvar_in[c];
-      om = rmu_in[c];
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < NPASS; ++p) {
-    const int m = p / (4 / NBP), nf = NBP * (p % (4 / NBP));
-    __syncthreads();   // the previous pass's Ts reads (and Li) are done
-#pragma unroll
-    for (int nb = 0; nb < NBP; ++nb)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) Ts[(w * 16 + q + 4 * v) * TW + 16 * nb + r] = acc[m][nf + nb][v];
-    __syncthreads();
-    int64_t ix, iy;
-    cell_of(p, ix, iy);
-    const double cov = ov, com = om;
-    if (p + 1 < NPASS) {
-      int64_t ix2, iy2;
-      cell_of(p + 1, ix2, iy2);
-      if (cell_ok(ix2, iy2)) {
-        const int64_t c2 = ix2 * lat.sx + iy2 * lat.sy;
-        ov = rvar_in[c2];
-        om = rmu_in[c2];
+      unsigned* const cnt = d.gcnt + tile;
+      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (unsigned)(S - 1)) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publish(d.gcnt + tiles + tile, epoch);
       }
     }
-    if (!cell_ok(ix, iy)) continue;
-    const int64_t c = ix * lat.sx + iy * lat.sy;
-    const int ixc = (int)(ix - ix0), iyc = IXPT + (int)(iy - iy0);
-    const double* const Tc = Ts + (cw * 16 + (KA == 8 ? 8 * ch : 0)) * TW + cyl;
-    VT* const vt = Vr + (c / PBM) * vld * PBM + (c % PBM);
-    double vn[KA];
-    double vs = 0.0, ms = 0.0;
-#pragma unroll
-    for (int a = 0; a < KA; ++a) {
-      vn[a] = 0.0;
-      if (a < k) {
-        const double* fL = Fn + a * FW;
-        const double* fH = Fn + (KA + a) * FW;
-        const double pn = fL[ixc] * fL[iyc] + fH[ixc] * fH[iyc];
-        double t = pn - Tc[a * TW];
-#pragma unroll
-        for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
-        vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
-        vs += vn[a] * vn[a];
-        ms += vn[a] * L22[KINC * KINC + a];
-        vt[(n0 + a) * PBM] = (VT)vn[a];
-      }
-    }
-    const double vc = cov - vs;
-    const double mc = com + ms;
-    omu[c] = mc;
-    ovar[c] = vc;
-    if (rmu) {
-      rmu[c] = mc;
-      rvar[c] = vc;
-    }
-    argmax_pair(bv, bi, vc, c);
+    wait_flag(d, d.gcnt + tiles + tile, epoch);   // every split's partial is stored
   }
-  const int64_t tiles = d.lat_tiles;
-  WTRACE(6);
-  if (d.vmax || d.vargmax || d.status_host)
-    var_argmax_group(d, bv, bi, tile * 4 + w, tiles * 4);
-  WTRACE(4);
+  if (S > 1) lat_epi<KA, VT, true>(d, tile, s, sm, acc);
+  else lat_epi<KA, VT, false>(d, tile, s, sm, acc);
 }
 
 template <int KA, class VT>

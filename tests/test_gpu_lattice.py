@@ -311,3 +311,55 @@ def test_lattice_descriptors_by_value_equal_upload(monkeypatch, lattice):
         for sa, sb in zip(ra, rb):
             for xa, xb in zip(sa, sb):
                 assert np.array_equal(xa, xb), B
+
+
+@pytest.mark.parametrize("ksplit,wr", [(1, 1), (2, 2), (4, 4), (8, 8), (8, 1)])
+def test_lattice_split_and_row_parts_vs_oracle(monkeypatch, ksplit, wr):
+    """Every split-K factor of the GEMM tiles (1, 2, 4, 8: the splits share the
+    tile's cell passes; 8 = half a pass each) and row-part count of the w units
+    (1: no partials, 2 .. 8: partials added in part order), forced through the
+    context's diagnostic switches (MFGP_LAT_KSPLIT / MFGP_LAT_WR): two MF GPs on a
+    64 x 64 grid, appends of 8 and 5 rows, against the oracle at every cell."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    monkeypatch.setenv("MFGP_LAT_KSPLIT", str(ksplit))
+    monkeypatch.setenv("MFGP_LAT_WR", str(wr))
+    ctx = _lib.Context(0)
+    ctx.set_lattice("force")
+    hyp = _hyp("australia8_mf")
+    models, data = [], []
+    for i, (nl, nh) in enumerate([(200, 300), (150, 421)]):
+        Xs, X, y = _data(64, nl + nh + 20, seed=90 + i)
+        models.append(_model(ctx, hyp, X[:nl + nh], y[:nl + nh], nl, Xs))
+        data.append((X, y, nl, nl + nh))
+    M = Xs.shape[0]
+    mu = torch.empty(2 * M, dtype=torch.float64, device="cuda")
+    var = torch.empty_like(mu)
+    vmax = torch.empty(2, dtype=torch.float64, device="cuda")
+    _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
+    for k in (8, 5):
+        Xn = np.concatenate([X[n:n + k] for X, _, _, n in data])
+        yn = np.concatenate([y[n:n + k] for _, y, _, n in data])
+        Xt = torch.from_numpy(np.ascontiguousarray(Xn)).cuda()
+        yt = torch.from_numpy(np.ascontiguousarray(yn)).cuda()
+        _lib.batch_append_predict(models, Xt.data_ptr(), yt.data_ptr(), [k, k], mu.data_ptr(), var.data_ptr(),
+                                  vmax_ptr=vmax.data_ptr())
+        data = [(X, y, nl, n + k) for X, y, nl, n in data]
+        mh, vh = mu.cpu().numpy().reshape(2, M), var.cpu().numpy().reshape(2, M)
+        for i, (X, y, nl, n) in enumerate(data):
+            mu_r, var_r = _ref(hyp, X[:n], y[:n], nl, Xs)
+            assert _err(hyp, mh[i], vh[i], mu_r, var_r) < TOL, (ksplit, wr, k, i)
+        np.testing.assert_array_equal(vmax.cpu().numpy(), vh.max(axis=1))
+    for m in models:
+        assert m.stats()["lattice"] == 2, m.stats()
+    # the factor the steps leave behind (the next V-stream step's L21 comes from V)
+    ctx.set_lattice(False)
+    for k in (3,):
+        Xn = np.concatenate([X[n:n + k] for X, _, _, n in data])
+        yn = np.concatenate([y[n:n + k] for _, y, _, n in data])
+        _lib.batch_append_predict(models, Xn.ctypes.data, yn.ctypes.data, [k, k], mu.data_ptr(), var.data_ptr())
+        data = [(X, y, nl, n + k) for X, y, nl, n in data]
+        mh, vh = mu.cpu().numpy().reshape(2, M), var.cpu().numpy().reshape(2, M)
+        for i, (X, y, nl, n) in enumerate(data):
+            mu_r, var_r = _ref(hyp, X[:n], y[:n], nl, Xs)
+            assert _err(hyp, mh[i], vh[i], mu_r, var_r) < TOL, (ksplit, wr, "vstream", i)

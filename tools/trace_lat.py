@@ -27,6 +27,7 @@ assert L.mfgp_debug_set_stamps(ctypes.c_void_p(st.data_ptr())) == 0
 Xnew = torch.from_numpy(np.ascontiguousarray(np.stack([w.Xnew for w in wls], 1).reshape(T, B * k, 2))).to(dev)
 ynew = torch.from_numpy(np.ascontiguousarray(np.stack([w.ynew for w in wls], 1).reshape(T, B * k))).to(dev)
 ctx = _lib.context()
+ctx.set_lattice("force")   # B = 1: past the cost gate
 models = []
 for wl in wls:
     m = _lib.Model(ctx, _lib.MF, hyp, 1e-8)
@@ -52,16 +53,17 @@ used = tr[:, 0] > 0
 t0 = tr[used, 0].min()
 tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)   # us (100 MHz realtime counter)
 nprod, nwb = 16, 32
-import math
-def _units(t):
-    return sum(math.ceil((2040 - 64 * j) / t) for j in range(32))
-wch = next((t for t in (1024, 512) if B * _units(t) >= 2 * 256), 256)   # the host's rule
-nwu = _units(wch)
+# the host's rule (mfgp_capi.hip): units = block pairs x 2 halves x wr row parts,
+# wr doubling while the units of the batch are fewer than the CUs
+npair = (nwb + 1) // 2
+wr = int(os.environ.get("MFGP_LAT_WR", "0")) or next(r for r in (1, 2, 4, 8) if B * npair * 2 * r >= 256 or r == 8)
+nwu = npair * 2 * wr
+wch = wr
 _zq = 2 * 256 // (((G + 63) // 64) * 64)
 nzu = 2 * ((G + _zq - 1) // _zq)
 role = np.arange(NWG) // B
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
-print(f"B={B} (w chunk {wch}, {nwu} w units, {nzu} Z units per GP): percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
+print(f"B={B} (w row parts {wr}, {nwu} w units, {nzu} Z units per GP): percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
 for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w unit", (role >= nprod) & (role < nprod + nwu), (0, 1, 3, 2)),
                          ("Z unit", (role >= nprod + nwu) & (role < nprod + nwu + nzu), (0, 1, 3, 4, 5, 6, 2)),
                          ("gemm", (role >= nprod + nwu + nzu) & used, (0, 1, 2, 3, 5, 6, 4))):
