@@ -99,7 +99,7 @@ struct mfgp_ctx {
   bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
-  int lat_wr = 0;             // row parts per block of its w units (0: chosen per launch; MFGP_LAT_WR, diagnostics)
+  int lat_wu = 0;             // w units of a launch, all GPs (0: one per CU; MFGP_LAT_WU, diagnostics)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
@@ -185,7 +185,7 @@ struct mfgp_model {
   int64_t wv_ld = 0;
   unsigned* wflag = nullptr;  // [wv_ld / 64 + 2]
   unsigned* wcnt = nullptr;   // [wv_ld / 64 + 2]
-  double* wpart = nullptr;    // [wv_ld / 64 + 1][2][LAT_WR_MAX][512]
+  double* wpart = nullptr;    // [LAT_WU_MAX + wv_ld / 64 + 1][1024]
   double* gpart = nullptr;    // split-K partials
   size_t gpart_n = 0;
   unsigned* gcnt = nullptr;   // per GEMM tile
@@ -596,6 +596,7 @@ bool lat_eligible(const mfgp_model* m, int64_t n0) {
   const int64_t k = m->NL + m->NH - n0;
   if (!m->ctx->lattice || m->lat.nx <= 0 || m->M <= 0 || k < 1 || k > KINC || n0 < 1) return false;
   if (lat_tabw(m) > NT) return false;   // a Z unit's thread per lattice column
+  if ((n0 + 63) / 64 > LAT_NWB_MAX) return false;   // a w unit's blocks
   if (!lat_cond_ok(m)) return false;
   const int b = res_find(m, n0);
   return b >= 0 && m->res_depth[b] < LAT_MAXD;
@@ -643,7 +644,7 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     HIP_TRY(hipMemsetAsync(m->wflag, 0, sizeof(unsigned) * (ld / 64 + 2), s));   // below every epoch
     HIP_TRY(hipMalloc(&m->wcnt, sizeof(unsigned) * 2 * (ld / 64 + 2)));
     HIP_TRY(hipMemsetAsync(m->wcnt, 0, sizeof(unsigned) * 2 * (ld / 64 + 2), s));
-    HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 512 * 2 * LAT_WR_MAX * (ld / 64 + 1)));
+    HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 1024 * (LAT_WU_MAX + ld / 64 + 1)));
     m->wv_ld = ld;
   }
   if (m->gcnt_n != tiles) {
@@ -1148,7 +1149,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
-  if (const char* e = std::getenv("MFGP_LAT_WR")) c->lat_wr = std::max(0, std::min(LAT_WR_MAX, std::atoi(e)));
+  if (const char* e = std::getenv("MFGP_LAT_WU")) c->lat_wu = std::max(0, std::atoi(e));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
     const int v = std::atoi(e);
@@ -1863,15 +1864,13 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         S = p2;
         while (S > 1 && tiles_sum * S > 2 * (int64_t)c->ncu) S /= 2;
       }
-      // row parts per block of F: one per w unit while the block pairs alone give a
-      // unit per CU (B >= 8 at the headline), more for smaller batches (partials)
-      int wr = 1;
-      {
-        int64_t units = 0;
-        for (int i = 0; i < ninc; ++i) units += lat_wunits(hd[i].n0, 1);
-        while (wr < LAT_WR_MAX && units * wr < c->ncu) wr *= 2;
-        if (c->lat_wr > 0) wr = std::min(c->lat_wr, LAT_WR_MAX);
-      }
+      // w units: two per CU over the launch (equal shares of the F stream: with an
+      // uneven count the CUs holding one more unit set the stream's pace; two per CU
+      // keep twice the loads in flight: tools/probe_wloop.hip, B = 8: 25 vs 30 us),
+      // each GP's count by its F steps
+      const int64_t wu_total = c->lat_wu > 0 ? c->lat_wu : 2 * c->ncu;
+      int64_t wsteps_sum = 0;
+      for (int i = 0; i < ninc; ++i) wsteps_sum += lat_wsteps(hd[i].n0);
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
@@ -1896,8 +1895,11 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.ksplit = S;
         fd.lat_tiles = (int)tiles;
         fd.nwb = (int)((fd.n0 + 63) / 64);
-        fd.wr = wr;
-        fd.nwu = (int)lat_wunits(fd.n0, wr);
+        {
+          const int64_t st = lat_wsteps(fd.n0);
+          const int64_t u = (wu_total * st + wsteps_sum / 2) / wsteps_sum;
+          fd.nwu = (int)std::max<int64_t>(1, std::min<int64_t>({u, (int64_t)LAT_WU_MAX, st}));
+        }
         fd.wpart = m->wpart;
         fd.wcnt = m->wcnt;
         fd.lat_fbuild = (m->F_gen == m->gen && m->F_n >= fd.n0) ? 0 : 1;

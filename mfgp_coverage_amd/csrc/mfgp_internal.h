@@ -118,10 +118,9 @@ struct GPDesc {
   int lat_tiles;       // GEMM tiles per GP: ceil(nx / (64 / ka)) * ceil(ny / 64)
   int nwb;             // 64-row blocks of w: ceil(n0 / 64)
   int lat_fbuild;      // k_trinv_f: 1 = compute F for the n0 factor rows
-  int nwu;             // w work units: block pairs x 2 column halves x wr row parts (lat_wunits(n0, wr))
-  int wr;              // row parts per block of F (1: no partials; the host raises it for small batches)
-  double* wpart;       // the row parts' partial w halves [64-column blocks][2 halves][LAT_WR_MAX][32 x 16]
-  unsigned* wcnt;      // per (64-column block, half): arrivals of its row parts (zero between launches)
+  int nwu;             // w units of the GP: each an equal share of F's 16-row steps (lat_wsteps)
+  double* wpart;       // the units' partial w blocks [nwu + nwb][64 x 16] (unit u, block at position o of the pair order: slot u + o)
+  unsigned* wcnt;      // per 64-column block: arrivals of its units' partials (zero between launches)
   // lattice-axis form of the step (every term on the lattice's own axis values)
   double* axt;         // axis tables [4][tabw + 1][tabw]: exp(-(a_p - a_col)^2 / 2 l^2) of the grid's
                        // axis values, x then y, L then H lengthscale; row tabw: zeros
@@ -140,17 +139,20 @@ struct GPDesc {
   Hyp hp;              // hyperparameters of predict (predict time)
 };
 
-// lattice step: w is computed by units of one PAIR of 64-column blocks of F's
-// lower triangle (block p and block nwb - 1 - p: rows [64 p, n0) and [64 (nwb - 1
-// - p), n0), about n0 + 64 rows together, so every pair streams the same number
-// of bytes) x one 32-column half x one of wr row parts of each block
-constexpr int LAT_WR_MAX = 8;
+// lattice step: w is computed by units that each stream an equal share of F's
+// lower triangle, taken as one sequence of 16-row steps (block jb: ceil(n0 / 16) -
+// 4 jb steps, block after block); at most LAT_WU_MAX units per GP, and n0 within
+// LAT_NWB_MAX blocks of 64 columns
+constexpr int LAT_WU_MAX = 512;
+constexpr int LAT_NWB_MAX = 256;
 constexpr int ZKS = 8;   // lattice-axis GEMM: K rows per pipeline stage (Z / axis-table rows)
 // F's column block jb starts at fblk_off(jb, ld): blocks b < jb hold ld - 64 b rows of 64
 inline __host__ __device__ int64_t fblk_off(int64_t jb, int64_t ld) { return 64 * jb * ld - 2048 * jb * (jb - 1); }
 inline __host__ __device__ int64_t fblk_size(int64_t ld) { return fblk_off(ld / 64, ld); }
-inline __host__ __device__ int64_t lat_wpairs(int64_t n0) { return ((n0 + 63) / 64 + 1) / 2; }
-inline __host__ __device__ int64_t lat_wunits(int64_t n0, int64_t wr) { return lat_wpairs(n0) * 2 * wr; }
+inline __host__ __device__ int64_t lat_wsteps(int64_t n0) {
+  const int64_t C = (n0 + 15) / 16, nwb = (n0 + 63) / 64;
+  return nwb * C - 2 * nwb * (nwb - 1);
+}
 inline __host__ __device__ int64_t nblocks_factor(int64_t N) { return (N + 1 + NB - 1) / NB; }
 inline __host__ __device__ int64_t nblocks_rows(int64_t N) { return (N + NB - 1) / NB; }
 inline __host__ __device__ int64_t ntiles_grid(int64_t M) { return (M + PBM - 1) / PBM; }

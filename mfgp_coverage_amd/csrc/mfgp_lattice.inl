@@ -30,8 +30,8 @@
 // One launch per batch, grid (GPs, roles); per GP the roles are
 //   [0, nprod)                 producers + finish, exactly as k_inc_stream's
 //   [nprod, nprod + nwu)       w units (a pair of 64-column blocks of F, the
-//                              top block and the bottom one, x a 32-column half
-//                              x a row part): wait for the compact rows, then
+//                              top block and the bottom one, x a row part):
+//                              wait for the compact rows, then
 //                              w[j][a] = sum_{i >= j} F[i][j] L21c[i][a] on
 //                              MFMA; store w (or a partial: the last row part
 //                              adds them), count it into ldone; then F's new rows
@@ -202,16 +202,6 @@ __device__ __forceinline__ void lat_l22inv(const GPDesc& d, int k, double* L22, 
   __syncthreads();
 }
 
-// Row part rp of R of w's column block jb: rows [lo, hi) of [64 jb, n0), in parts
-// of a multiple of 16 rows (one MFMA step of the workgroup's four waves).
-__device__ __forceinline__ void lat_wpart_rows(int64_t n0, int64_t jb, int R, int rp, int64_t& lo, int64_t& hi) {
-  const int64_t L = n0 - 64 * jb;
-  const int64_t cs = ((L + R - 1) / R + 15) / 16 * 16;
-  lo = 64 * jb + rp * cs;
-  hi = lo + cs < n0 ? lo + cs : n0;
-  if (lo > hi) lo = hi;
-}
-
 // Compact row i, entry a (written by the producers in this launch: an L2-served
 // load of the agent scope, never a possibly stale L1 line).
 template <class VT>
@@ -224,29 +214,46 @@ __device__ __forceinline__ double l21c_ld(const double* l21c, int64_t i, int a) 
   }
 }
 
-// One w unit: w = F11^T L21^T, w[j][a] = sum_{i >= j} F[i][j] L21c[i][a], for the
-// 32-column half h of the PAIR of column blocks (p, nwb - 1 - p), row part rp of
-// each (the pair's two blocks hold ~n0 + 64 rows together, so every unit streams
-// the same bytes of F and they all end together). Per 16-row step each wave takes
-// 4 rows: lane (r, q) loads L21c[i][r] (the MFMA A operand, a = r) and F[i][32 h +
-// 2 r + c] for c = 0, 1 (B, one 16-byte load: the row's 256-byte half), RG steps per
-// batch, two batches in flight (registers, no LDS): the first batch of F is issued
-// before the wait for the compact rows. At the end of a block the waves' sums
-// meet in LDS in wave order; with one row part the unit stores its w half itself,
-// else each part stores a partial and the last of the block half's R parts adds
-// them in part order. Whoever stored a w half counts it into ldone[0] (the Z units
-// wait for all 2 nwb halves), then writes F's new rows for its columns,
-// -L22^-1 w^T (the top block's h = 0 unit also the L22^-1 entries).
+#ifndef MFGP_W_DEPTH
+#define MFGP_W_DEPTH 6
+#endif
+// The w units' share of F: F's lower triangle as one stream of 16-row steps,
+// block jb's rows [64 jb, n0) in nb(jb) = ceil(n0 / 16) - 4 jb steps, the blocks
+// in pair order 0, nwb - 1, 1, nwb - 2, ... (a pair's steps add up to the same K2
+// = 2 ceil(n0 / 16) - 4 (nwb - 1) whichever pair; a share then spans few blocks);
+// unit u of U takes the steps [u S / U, (u + 1) S / U) of the S in all. So every
+// unit streams the same bytes whatever n0 and the unit count (a unit per block
+// pair left 1 in 17 CUs with two units at B = 8, and the stream ran at the slower
+// CUs' rate). A block's steps spread over units u_first .. u_last of it; each
+// stores a partial of the block's w at slot u + (its position) of the GP's partials.
+__device__ __forceinline__ int64_t wst_first(int64_t C, int64_t nwb, int64_t jb) {
+  const int64_t K2 = 2 * C - 4 * (nwb - 1);
+  return 2 * jb < nwb ? jb * K2 : (nwb - 1 - jb) * K2 + C - 4 * (nwb - 1 - jb);
+}
+__device__ __forceinline__ int64_t wst_unit(int64_t s, int64_t S, int64_t U) { return ((s + 1) * U - 1) / S; }
+// block jb's position in the pair order (its partials: slots u + position, distinct
+// since a position's units start where the previous position's end)
+__device__ __forceinline__ int64_t wst_pos(int64_t nwb, int64_t jb) {
+  return 2 * jb < nwb ? 2 * jb : 2 * (nwb - 1 - jb) + 1;
+}
+
+// One w unit: w = F11^T L21^T, w[j][a] = sum_{i >= j} F[i][j] L21c[i][a], over the
+// unit's steps. Per step, wave w takes rows 4 w + q: lane (r, q) loads L21c[i][r]
+// (the MFMA A operand, a = r) and F[i][32 hh + 2 r + c] for hh, c = 0, 1 (B; two
+// 16-byte loads: 16 lanes cover a 512-byte row). Four steps in flight per wave in
+// registers. At the end of a block's steps the waves' sums meet in LDS in wave
+// order and the partial is stored (no wait: stores only, the stream goes on);
+// after the stream each of the unit's blocks counts its partial in, and whoever
+// counts a block in last adds its partials in slot order (the same bits whoever it
+// is), stores the block of w, counts it into ldone[0] (the Z units wait for all
+// nwb blocks) and writes F's new rows for its columns, -L22^-1 w^T (the top
+// block's also the L22^-1 entries).
 template <class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
-  constexpr int RG = 6;            // 16-row steps per batch
-  constexpr int WB = 16 * RG;      // rows per batch (the four waves)
+  constexpr int DEPTH = MFGP_W_DEPTH;   // steps in flight per wave
   const int64_t n0 = d.n0, ld = d.ld;
-  const int nwb = d.nwb, R = d.wr;
-  const int64_t p = u / (2 * R);
-  const int h = (int)((u / R) & 1), rp = (int)(u % R);
-  const int64_t blk0 = p, blk1 = nwb - 1 - p;
-  const int nblk = blk0 < blk1 ? 2 : 1;
+  const int nwb = d.nwb;
+  const int64_t U = d.nwu;
   const double* const l21c = d.l21c;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -258,7 +265,7 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   {
     const int64_t tabw = d.tabw, tstride = (d.ld) * tabw;
     const int64_t tot = 4 * (int64_t)k * tabw;
-    const int64_t per = (tot + d.nwu - 1) / d.nwu, e0 = u * per;
+    const int64_t per = (tot + U - 1) / U, e0 = u * per;
     const int64_t e1 = e0 + per < tot ? e0 + per : tot;
     for (int64_t e = e0 + tid; e < e1; e += NT) {
       const int t = (int)(e / (k * tabw));
@@ -275,183 +282,238 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       d.lidx[n0 + tid] = lattice_xy(d, pt[0], pt[1]);
     }
   }
-  // (scalars, not arrays indexed by the segment: a dynamically indexed local array
-  // lives in scratch, and a scratch load in the loop drains every outstanding load)
-  int64_t lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
-  lat_wpart_rows(n0, blk0, R, rp, lo0, hi0);
-  if (nblk == 2) lat_wpart_rows(n0, blk1, R, rp, lo1, hi1);
-  const int64_t nbt0 = (hi0 - lo0 + WB - 1) / WB, nbt1 = (hi1 - lo1 + WB - 1) / WB;
-  const int64_t T = nbt0 + nbt1;
-  // LDS: red [4 w][2 c][4 v][64] | the w halves this unit stored [2][32 jl][16 a] | L22 | Li
+  const int64_t C = (n0 + 15) / 16;
+  const int64_t K2 = 2 * C - 4 * (nwb - 1);
+  const int64_t S = (nwb / 2) * K2 + (nwb & 1) * (C - 4 * (nwb / 2));
+  const int64_t s0 = u * S / U, s1 = (u + 1) * S / U;
+  const int64_t T = s1 - s0;
+  // the unit's first step: pair p0, its first (odd0 = 0: block p0) or second block
+  // (nwb - 1 - p0), step st0 of it
+  const int64_t p0 = s0 / K2;
+  const int64_t rem0 = s0 - p0 * K2;
+  const bool odd0 = rem0 >= C - 4 * p0;
+  const int64_t jb0 = odd0 ? nwb - 1 - p0 : p0;
+  const int64_t st0 = odd0 ? rem0 - (C - 4 * p0) : rem0;
+  // LDS: red [4 w][2 acc][4 v][64] (one 32-column half at a time) | the unit's
+  // blocks [<= LAT_NWB_MAX] | their last-arrival marks | w of a block [64 jl][16 a]
+  // | L22 | Li
   double* const red = sm;
-  double* const Wh = sm + 2048;
-  double* const L22 = Wh + 2 * 32 * KINC;
+  int* const segs = reinterpret_cast<int*>(sm + 2048);
+  int* const lastm = segs + LAT_NWB_MAX;
+  double* const Wh = sm + 2048 + LAT_NWB_MAX;
+  double* const L22 = Wh + 64 * KINC;
   double* const Li = L22 + KINC * KINC + KINC;
-  static_assert(2048 + 2 * 32 * KINC + 2 * KINC * KINC + KINC <= LAT_LDS, "the w unit's LDS fits");
-  unsigned& wlast = *reinterpret_cast<unsigned*>(sm + LAT_LDS + 10);
-  bool have0 = false, have1 = false;
-  // rows of batch t: segment b (block blk0, then blk1), i = lo + WB s + 16 x + 4 w + q
-  struct Seg {
-    int64_t jb, lo, hi, i0;
+  static_assert(LAT_NWB_MAX <= NT, "one thread per block of the unit counts it in");
+  static_assert(2048 + LAT_NWB_MAX + 64 * KINC + 2 * KINC * KINC + KINC <= LAT_LDS, "the w unit's LDS fits");
+  // a cursor over the steps: block jb, step st of its nb, in pair p (second block: odd)
+  struct Cur {
+    int64_t jb, st, nb, p;
+    bool odd;
   };
-  auto seg = [&](int64_t t) {
-    const bool b = t >= nbt0;
-    Seg g;
-    g.jb = b ? blk1 : blk0;
-    g.lo = b ? lo1 : lo0;
-    g.hi = b ? hi1 : hi0;
-    g.i0 = g.lo + WB * (t - (b ? nbt0 : 0)) + 4 * w + q;
-    return g;
-  };
-  // lane (r, q) loads columns 32 h + 2 r, 2 r + 1 of a row with ONE 16-byte load
-  // (16 lanes: the row's 256-byte half): MFMA c = 0 takes the even columns, c = 1
-  // the odd ones
-  auto load_f = [&](int64_t t, dv2 (&f)[RG]) {
-    const Seg g = seg(t);
-    const GLOBAL dv2* Fr = reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + fblk_off(g.jb, ld) + 32 * h + 2 * r);
-#pragma unroll
-    for (int x = 0; x < RG; ++x) {
-      const int64_t i = g.i0 + 16 * x;
-      const int64_t ii = i < g.hi ? i : g.lo;
-      // F is read once per step and would evict the GEMM tiles' tables from L2
-      f[x] = __builtin_nontemporal_load(Fr + (ii - 64 * g.jb) * 32);
+  auto adv = [&](Cur& c) {
+    if (++c.st == c.nb) {
+      c.st = 0;
+      if (c.odd) {
+        ++c.p;
+        c.jb = c.p;
+      } else {
+        c.jb = nwb - 1 - c.p;
+      }
+      c.odd = !c.odd;
+      c.nb = C - 4 * c.jb;
     }
   };
-  // (unconditional loads -- a row past the part reloads its first row -- and the
-  // row mask applied at the MFMA: a branch around a load makes the compiler drain
-  // every outstanding load, the next batch's too, before the current one's MFMAs)
-  auto load_a = [&](int64_t t, double (&a)[RG], unsigned& live) {
-    const Seg g = seg(t);
-    live = 0;
+  const Cur cur0{jb0, st0, C - 4 * jb0, p0, odd0};
+  // lane (r, q) loads columns 32 hh + 2 r, 2 r + 1 (hh = 0, 1) of its row with two
+  // 16-byte loads: MFMA 2 hh + 0 takes the even columns, 2 hh + 1 the odd ones. A
+  // row past n0 (the block's last step) reloads row n0 - 1 (finite) and is masked.
+  auto row_of = [&](const Cur& c) { return 64 * c.jb + 16 * c.st + 4 * w + q; };
+  auto load_f = [&](const Cur& c, dv2 (&f)[2]) {
+    const int64_t i = row_of(c);
+    const int64_t ii = i < n0 ? i : n0 - 1;
+    const GLOBAL dv2* Fr =
+        reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + fblk_off(c.jb, ld) + (ii - 64 * c.jb) * 64 + 2 * r);
+    // plain loads: F stays in the memory-side cache across steps where it fits
+    // (tools/probe_wloop.hip: 2 units per CU, plain 25 us vs non-temporal 26-30 us)
+    f[0] = Fr[0];
+    f[1] = Fr[16];
+  };
+  auto load_a = [&](const Cur& c, double& a) {
+    const int64_t i = row_of(c);
+    a = l21c_ld<VT>(l21c, i < n0 ? i : n0 - 1, r);
+  };
+  d4 acc[4];
 #pragma unroll
-    for (int x = 0; x < RG; ++x) {
-      const int64_t i = g.i0 + 16 * x;
-      live |= (i < g.hi ? 1u : 0u) << x;
-      a[x] = l21c_ld<VT>(l21c, i < g.hi ? i : g.lo, r);
+  for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+  auto compute = [&](const dv2 (&f)[2], double a, bool live) {
+    const double av = live ? a : 0.0;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      acc[2 * hh] = mfma(av, f[hh].x, acc[2 * hh]);
+      acc[2 * hh + 1] = mfma(av, f[hh].y, acc[2 * hh + 1]);
     }
   };
-  d4 acc[2];
-  acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
-  auto compute = [&](const dv2 (&f)[RG], const double (&a)[RG], unsigned live) {
+  int nseg = 0;
+  // the end of block jb's steps in this unit: the waves' sums in wave order (one
+  // 32-column half at a time), stored as the unit's partial of the block
+  auto seg_done = [&](int64_t jb) {
+    // thread tid: outputs e = tid + 256 m, (jl, a) = (e >> 4, e & 15), jl = 32 hh +
+    // jh; lane (rr, g) register v of acc[2 hh + c] is w row a = g + 4 v, column
+    // jh = 2 rr + c
+    double own[4];
 #pragma unroll
-    for (int x = 0; x < RG; ++x) {
-      const double av = (live >> x) & 1u ? a[x] : 0.0;
-      acc[0] = mfma(av, f[x].x, acc[0]);
-      acc[1] = mfma(av, f[x].y, acc[1]);
-    }
-  };
-  // the end of block b's rows: the waves' sums in wave order, then w (or a partial)
-  auto block_done = [&](int b) {
-    const int64_t jb = b ? blk1 : blk0;
+    for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) red[w * 512 + (c * 4 + v) * 64 + lane] = acc[c][v];
-    acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
-    __syncthreads();
-    // thread tid: outputs e = tid + 256 m, (jl, a) = (e >> 4, e & 15); lane (rr, g)
-    // register v of acc[c] is w row a = g + 4 v, column jl = 2 rr + c
-    double own[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int e = tid + NT * m, jl = e >> 4, a = e & 15;
-      const int o = ((jl & 1) * 4 + (a >> 2)) * 64 + 16 * (a & 3) + (jl >> 1);
-      own[m] = (red[o] + red[512 + o]) + (red[1024 + o] + red[1536 + o]);
-    }
-    __syncthreads();
-    double* const wv = d.wv + (64 * jb + 32 * h) * KINC;
-    bool stored = true;
-    if (R > 1) {
-      double* const part = d.wpart + ((jb * 2 + h) * LAT_WR_MAX + rp) * 512;
-#pragma unroll
-      for (int m = 0; m < 2; ++m) stx<true>(part + tid + NT * m, own[m]);
-      drain_stores();
+        for (int v = 0; v < 4; ++v) red[w * 512 + (c * 4 + v) * 64 + lane] = acc[2 * hh + c][v];
       __syncthreads();
-      if (tid == 0) {
-        const unsigned old =
-            __hip_atomic_fetch_add(d.wcnt + jb * 2 + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        wlast = old == (unsigned)(R - 1) ? 1u : 0u;
-        if (wlast) __hip_atomic_store(d.wcnt + jb * 2 + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2) {
+        const int e = tid + NT * m2, jh = e >> 4, a = e & 15;
+        const int o = ((jh & 1) * 4 + (a >> 2)) * 64 + 16 * (a & 3) + (jh >> 1);
+        own[2 * hh + m2] = (red[o] + red[512 + o]) + (red[1024 + o] + red[1536 + o]);
       }
       __syncthreads();
-      stored = wlast != 0;
-      if (stored) {
-        // every part's partial, in part order: the same bits whichever arrives last
-        const double* const p0 = d.wpart + (jb * 2 + h) * LAT_WR_MAX * 512;
-        double x[LAT_WR_MAX][2];
-#pragma unroll
-        for (int rr = 0; rr < LAT_WR_MAX; ++rr)
-#pragma unroll
-          for (int m = 0; m < 2; ++m) x[rr][m] = rr < R ? ldx<true>(p0 + rr * 512 + tid + NT * m) : 0.0;
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          double t = x[0][m];
-#pragma unroll
-          for (int rr = 1; rr < LAT_WR_MAX; ++rr)
-            if (rr < R) t += x[rr][m];
-          own[m] = t;
-        }
-      }
     }
-    if (stored) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        stx<true>(wv + tid + NT * m, own[m]);
-        Wh[(b ? 512 : 0) + tid + NT * m] = own[m];
-      }
-      drain_stores();
-      __syncthreads();
-      if (tid == 0) arrive_phase(d.ldone, epoch, 2 * (int64_t)nwb);
-    }
-    if (b) have1 = stored;
-    else have0 = stored;
+    for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+    // own[2 hh + m2] is output e = 512 hh + tid + 256 m2 of the block
+    double* const part = d.wpart + (u + wst_pos(nwb, jb)) * 1024;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) stx<true>(part + tid + NT * m, own[m]);
+    if (tid == 0) segs[nseg] = (int)jb;
+    ++nseg;
   };
-  dv2 fA[RG], fB[RG];
-  double aA[RG], aB[RG];
-  unsigned mA = 0, mB = 0;
-  if (T > 0) load_f(0, fA);   // F does not depend on this launch: before the wait
-  wait_l21_from(d, nblk == 2 && lo1 < lo0 ? lo1 : lo0);
-  WTRACE(1);
-  if (nbt0 == 0) block_done(0);
-  if (T > 0) load_a(0, aA, mA);
-  // the next batch's loads are issued unconditionally (past the end: the last batch
-  // again, unused): a branch around them would make the compiler's wait for the
-  // current batch also wait for the next one's loads
-  for (int64_t t = 0; t < T; t += 2) {
-    load_f(t + 1 < T ? t + 1 : T - 1, fB);
-    load_a(t + 1 < T ? t + 1 : T - 1, aB, mB);
-    compute(fA, aA, mA);
-    if (t == nbt0 - 1) block_done(0);
-    if (t + 1 >= T) break;
-    load_f(t + 2 < T ? t + 2 : T - 1, fA);
-    load_a(t + 2 < T ? t + 2 : T - 1, aA, mA);
-    compute(fB, aB, mB);
-    if (t + 1 == nbt0 - 1) block_done(0);
+  // the pipeline: step t's loads go out with step t - DEPTH + 1's MFMAs. Loads
+  // past the unit's last step reload its last step (unused): a branch around a
+  // load would make the compiler's wait for the current step also wait for the
+  // loads behind it.
+  dv2 fb[DEPTH][2];
+  double ab[DEPTH];
+  Cur cl = cur0;   // the next step to load (clamped to the last)
+  int64_t tl = 0;
+  auto next_load = [&]() {
+    if (tl + 1 < T) {
+      adv(cl);
+      ++tl;
+    }
+  };
+  {
+    // the unit's lowest row: its first step's, or (spanning more blocks) at most
+    // pair p0 + 1's first block's first
+    const int64_t lo = 64 * jb0 + 16 * st0;
+    const int64_t lo2 = st0 + T > C - 4 * jb0 ? 64 * (p0 + 1) : lo;
+    wait_l21_from(d, lo < lo2 ? lo : lo2);
   }
-  if (nblk == 2) block_done(1);
+  WTRACE(1);
+  // the first DEPTH - 1 steps' loads in the loop's own order (F, then L21c, per
+  // step): the compiler's waits in the loop then count DEPTH - 1 steps in flight
+#pragma unroll
+  for (int b = 0; b + 1 < DEPTH; ++b) {
+    load_f(cl, fb[b]);
+    load_a(cl, ab[b]);
+    next_load();
+  }
+  Cur cc = cur0;   // the step being computed
+  // (whole groups of DEPTH steps, no exits in between: an exit path makes the
+  // compiler's waits at the loop head drain every load in flight; the buffers by
+  // compile-time index: registers)
+  for (int64_t t0 = 0; t0 < T; t0 += DEPTH) {
+#pragma unroll
+    for (int b = 0; b < DEPTH; ++b) {
+      const int64_t t = t0 + b;
+      // issue step t + DEPTH - 1 (into the buffer step t - 1 used), then compute
+      // step t (steps past T: the last step's rows again, masked)
+      load_f(cl, fb[(b + DEPTH - 1) % DEPTH]);
+      load_a(cl, ab[(b + DEPTH - 1) % DEPTH]);
+      next_load();
+      compute(fb[b], ab[b], t < T && row_of(cc) < n0);
+      if (t < T) {
+        if (cc.st + 1 == cc.nb || t + 1 == T) seg_done(cc.jb);
+        if (t + 1 < T) adv(cc);
+      }
+    }
+  }
   WTRACE(3);
-  if (!have0 && !have1) return;
+  // count the unit's partials in (one arrival per block, all at once)
+  drain_stores();
+  __syncthreads();
+  if (tid < nseg) {
+    const int64_t jb = segs[tid];
+    const unsigned old = __hip_atomic_fetch_add(d.wcnt + jb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t f = wst_first(C, nwb, jb);
+    const int64_t ncon = wst_unit(f + C - 4 * jb - 1, S, U) - wst_unit(f, S, U) + 1;
+    const bool last = old == (unsigned)(ncon - 1);
+    if (last) __hip_atomic_store(d.wcnt + jb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lastm[tid] = last ? 1 : 0;
+  }
+  __syncthreads();
+  // the blocks this unit counted in last, in a row (thread 0: a handful)
+  if (tid == 0) {
+    int nl = 0;
+    for (int g = 0; g < nseg; ++g)
+      if (lastm[g]) segs[nl++] = segs[g];
+    lastm[0] = nl;
+  }
+  __syncthreads();
+  const int nlast = lastm[0];
+  if (nlast == 0) return;
+  // the blocks' w: every contributor's partial in slot order (the same bits whoever
+  // is last), stored, then counted into ldone[0] together (one lane each; the Z
+  // units wait for all nwb blocks)
+  for (int g = 0; g < nlast; ++g) {
+    const int64_t jb = segs[g];
+    const int64_t f = wst_first(C, nwb, jb);
+    const int64_t ua = wst_unit(f, S, U), ub = wst_unit(f + C - 4 * jb - 1, S, U);
+    const double* const p0p = d.wpart + (ua + wst_pos(nwb, jb)) * 1024;
+    const int R = (int)(ub - ua + 1);
+    double own[4];
+    for (int r0 = 0; r0 < R; r0 += 4) {   // four partials' loads in flight at a time
+      double x[4][4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) x[rr][m] = r0 + rr < R ? ldx<true>(p0p + (r0 + rr) * 1024 + tid + NT * m) : 0.0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          if (r0 + rr < R) own[m] = (r0 + rr == 0) ? x[rr][m] : own[m] + x[rr][m];
+    }
+    double* const wv = d.wv + 64 * jb * KINC;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) stx<true>(wv + tid + NT * m, own[m]);
+  }
+  drain_stores();
+  __syncthreads();
+  if (tid < nlast) arrive_phase(d.ldone, epoch, (int64_t)nwb);
   WTRACE(2);
-  // F's new rows for the stored halves: F[n0 + a][j] = -sum_{b <= a} L22^-1[a][b] w[j][b]
+  // F's new rows for the blocks (read from the next launch on): F[n0 + a][j] =
+  // -sum_{b <= a} L22^-1[a][b] w[j][b], w reloaded (this workgroup stored it)
   wait_flag(d, d.sync + 2, epoch);
   lat_l22inv(d, k, L22, Li);
-  for (int b = 0; b < nblk; ++b) {
-    if (!(b ? have1 : have0)) continue;
-    const int64_t jb = b ? blk1 : blk0;
-    for (int e = tid; e < 32 * k; e += NT) {
-      const int a = e >> 5, jl = e & 31;
-      const int64_t j = 64 * jb + 32 * h + jl;
+  for (int g = 0; g < nlast; ++g) {
+    const int64_t jb = segs[g];
+    const double* const wv = d.wv + 64 * jb * KINC;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) Wh[tid + NT * m] = ldx<true>(wv + tid + NT * m);
+    __syncthreads();
+    for (int e = tid; e < 64 * k; e += NT) {
+      const int a = e >> 6, jl = e & 63;
+      const int64_t j = 64 * jb + jl;
       if (j >= n0) continue;
       double t = 0.0;
-      for (int bb = 0; bb <= a; ++bb) t -= Li[a * KINC + bb] * Wh[b * 512 + jl * KINC + bb];
-      d.F[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + 32 * h + jl] = t;
+      for (int bb = 0; bb <= a; ++bb) t -= Li[a * KINC + bb] * Wh[jl * KINC + bb];
+      d.F[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + jl] = t;
     }
-    if (jb == nwb - 1 && h == 0)
+    if (jb == nwb - 1)
       for (int e = tid; e < k * k; e += NT) {
         const int a = e / k, bb = e % k;
         const int64_t j = n0 + bb, jb2 = j / 64;
         if (bb <= a) d.F[fblk_off(jb2, ld) + (n0 + a - 64 * jb2) * 64 + j % 64] = Li[a * KINC + bb];
       }
+    __syncthreads();   // Wh is reused by the next block
   }
 }
 
@@ -1178,6 +1240,10 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     return;
   }
   if (role < np + d.nwu + d.nzu) {
+#ifdef MFGP_DIAG_LATNOZ   // diagnostic build: Z units count in at once (timing only, wrong results)
+    if (threadIdx.x == 0) arrive_phase(d.ldone + 2, d.epoch, d.nzu);
+    return;
+#endif
     lat_zunit<KA>(d, role - np - d.nwu, sm);
     return;
   }

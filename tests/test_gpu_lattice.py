@@ -313,17 +313,19 @@ def test_lattice_descriptors_by_value_equal_upload(monkeypatch, lattice):
                 assert np.array_equal(xa, xb), B
 
 
-@pytest.mark.parametrize("ksplit,wr", [(1, 1), (2, 2), (4, 4), (8, 8), (8, 1)])
-def test_lattice_split_and_row_parts_vs_oracle(monkeypatch, ksplit, wr):
+@pytest.mark.parametrize("ksplit,wu", [(1, 1), (2, 7), (4, 64), (8, 1024), (8, 2)])
+def test_lattice_split_and_w_units_vs_oracle(monkeypatch, ksplit, wu):
     """Every split-K factor of the GEMM tiles (1, 2, 4, 8: the splits share the
-    tile's cell passes; 8 = half a pass each) and row-part count of the w units
-    (1: no partials, 2 .. 8: partials added in part order), forced through the
-    context's diagnostic switches (MFGP_LAT_KSPLIT / MFGP_LAT_WR): two MF GPs on a
-    64 x 64 grid, appends of 8 and 5 rows, against the oracle at every cell."""
+    tile's cell passes; 8 = half a pass each) and w-unit count (the launch's total:
+    1 = one unit per GP streams all of its F and stores every block alone; 7, 64 =
+    blocks shared by several units, partials added in unit order; 1024 = one
+    16-row step per unit, clamped to the GP's steps), forced through the context's
+    diagnostic switches (MFGP_LAT_KSPLIT / MFGP_LAT_WU): two MF GPs on a 64 x 64
+    grid, appends of 8 and 5 rows, against the oracle at every cell."""
     import torch
     from mfgp_coverage_amd import _lib
     monkeypatch.setenv("MFGP_LAT_KSPLIT", str(ksplit))
-    monkeypatch.setenv("MFGP_LAT_WR", str(wr))
+    monkeypatch.setenv("MFGP_LAT_WU", str(wu))
     ctx = _lib.Context(0)
     ctx.set_lattice("force")
     hyp = _hyp("australia8_mf")
@@ -348,7 +350,7 @@ def test_lattice_split_and_row_parts_vs_oracle(monkeypatch, ksplit, wr):
         mh, vh = mu.cpu().numpy().reshape(2, M), var.cpu().numpy().reshape(2, M)
         for i, (X, y, nl, n) in enumerate(data):
             mu_r, var_r = _ref(hyp, X[:n], y[:n], nl, Xs)
-            assert _err(hyp, mh[i], vh[i], mu_r, var_r) < TOL, (ksplit, wr, k, i)
+            assert _err(hyp, mh[i], vh[i], mu_r, var_r) < TOL, (ksplit, wu, k, i)
         np.testing.assert_array_equal(vmax.cpu().numpy(), vh.max(axis=1))
     for m in models:
         assert m.stats()["lattice"] == 2, m.stats()
@@ -362,4 +364,4 @@ def test_lattice_split_and_row_parts_vs_oracle(monkeypatch, ksplit, wr):
         mh, vh = mu.cpu().numpy().reshape(2, M), var.cpu().numpy().reshape(2, M)
         for i, (X, y, nl, n) in enumerate(data):
             mu_r, var_r = _ref(hyp, X[:n], y[:n], nl, Xs)
-            assert _err(hyp, mh[i], vh[i], mu_r, var_r) < TOL, (ksplit, wr, "vstream", i)
+            assert _err(hyp, mh[i], vh[i], mu_r, var_r) < TOL, (ksplit, wu, "vstream", i)

@@ -53,17 +53,20 @@ used = tr[:, 0] > 0
 t0 = tr[used, 0].min()
 tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)   # us (100 MHz realtime counter)
 nprod, nwb = 16, 32
-# the host's rule (mfgp_capi.hip): units = block pairs x 2 halves x wr row parts,
-# wr doubling while the units of the batch are fewer than the CUs
-npair = (nwb + 1) // 2
-wr = int(os.environ.get("MFGP_LAT_WR", "0")) or next(r for r in (1, 2, 4, 8) if B * npair * 2 * r >= 256 or r == 8)
-nwu = npair * 2 * wr
+# the host's rule (mfgp_capi.hip): two w units per CU over the batch (MFGP_LAT_WU: the
+# total), each GP's count by its F steps (equal n0 here)
+n0 = NL + NH0
+C16 = (n0 + 15) // 16
+wsteps = nwb * C16 - 2 * nwb * (nwb - 1)
+wu_total = int(os.environ.get("MFGP_LAT_WU", "0")) or 512
+nwu = max(1, min((wu_total * wsteps + (B * wsteps) // 2) // (B * wsteps), 512, wsteps))
+wr = nwu
 wch = wr
 _zq = 2 * 256 // (((G + 63) // 64) * 64)
 nzu = 2 * ((G + _zq - 1) // _zq)
 role = np.arange(NWG) // B
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
-print(f"B={B} (w row parts {wr}, {nwu} w units, {nzu} Z units per GP): percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
+print(f"B={B} ({nwu} w units, {nzu} Z units per GP): percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
 for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w unit", (role >= nprod) & (role < nprod + nwu), (0, 1, 3, 2)),
                          ("Z unit", (role >= nprod + nwu) & (role < nprod + nwu + nzu), (0, 1, 3, 4, 5, 6, 2)),
                          ("gemm", (role >= nprod + nwu + nzu) & used, (0, 1, 2, 3, 5, 6, 4))):
