@@ -853,6 +853,20 @@ __device__ __forceinline__ void stx(double* p, double v) {
   else *p = v;
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The consumer's side of a hand-off. Every byte handed between workgroups of one
+// launch is stored write-through (sc1, drained before the flag) and loaded with
+// device-scope (sc1) loads that L2 does not serve from a possibly stale line, or
+// read plain only when no workgroup of that XCD can have cached the line earlier
+// in the launch (L2 is invalidated at kernel start); the consumer issues its
+// loads after it saw the flag (no speculation). An agent-scope acquire after the
+// wait (MFGP_ACQUIRE builds) states that order in the HIP memory model, but its
+// L2 invalidate costs the lattice step 105 -> 172 us per launch at B = 8 and the
+// drop-in step 87 -> 105 us (tools/ab_acquire.sh): off by default.
+__device__ __forceinline__ void acquire_agent() {
+#ifdef MFGP_ACQUIRE
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
 __device__ __forceinline__ void publish(unsigned* f, unsigned v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -872,6 +886,7 @@ __device__ void wait_flag(const GPDesc& d, const unsigned* f, unsigned v) {
     }
   }
   __syncthreads();
+  acquire_agent();
 }
 
 // Wait (wave 0; the workgroup joins at the barrier) until the compact rows of
@@ -895,7 +910,7 @@ __device__ void wait_l21(const GPDesc& d) {
       }
     }
   }
-  __syncthreads();
+  __syncthreads();  acquire_agent();
 }
 
 // Coordinates / observation of training row `row`: rows landing in this launch
@@ -1903,6 +1918,7 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
       }
     }
     __syncthreads();
+    acquire_agent();
     // plain loads: no line of the record is read in this launch before sync[2]
     // (an L2 miss for the first workgroup of an XCD, hits for the others)
     for (int e = tid; e < KINC * KINC + KINC; e += NT) {
@@ -2221,6 +2237,7 @@ __device__ __forceinline__ void vstream_wg_f32(const GPDesc& d, int64_t wgt, dou
       }
     }
     __syncthreads();
+    acquire_agent();
     for (int e = tid; e < KINC * KINC + KINC; e += NT) {
       const double v = d.l22r[e];
       const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);

@@ -155,7 +155,7 @@ __device__ void wait_l21_from(const GPDesc& d, int64_t lo) {
       }
     }
   }
-  __syncthreads();
+  __syncthreads();  acquire_agent();
 }
 
 // Spin (this wave) until *f == v; bounded like wait_flag.
@@ -167,7 +167,7 @@ __device__ __forceinline__ void spin_wave(const GPDesc& d, const unsigned* f, un
       if ((threadIdx.x & 63) == 0) atomicMin(d.status, SYNC_FAIL);
       break;
     }
-  }
+  }  acquire_agent();
 }
 
 template <class VT>
@@ -535,7 +535,7 @@ __device__ void wait_flags_all(const GPDesc& d, const unsigned* f, int64_t n, un
       }
     }
   }
-  __syncthreads();
+  __syncthreads();  acquire_agent();
 }
 
 // Exclusive prefix over the workgroup of NV per-thread counts (in thread order),
@@ -1257,9 +1257,15 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
 }
 
 // KA = 8 (appends of k <= 8 rows) or 16 (k <= 16): one kernel each, so each
-// carries only its own epilogue's registers
+// carries only its own epilogue's registers. Four workgroups per CU (<= 128
+// VGPRs, LAT_LDS): the roles' dispatch-order argument and the split-K tiles'
+// co-residency (tiles x S <= 2 per CU) rest on it (tests/test_codeobj.py).
+// MFGP_LAT_WAVES: a diagnostic override (8: a forced-spill build for that test).
+#ifndef MFGP_LAT_WAVES
+#define MFGP_LAT_WAVES MFGP_INC_WAVES
+#endif
 template <int KA, class VT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_lat(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_LAT_WAVES, MFGP_LAT_WAVES))) void k_inc_lat(
     const GPDesc* __restrict__ descs) {
   inc_lat_wg<KA, VT>(descs[blockIdx.x]);
 }
@@ -1271,7 +1277,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAV
 // idle stream time between consecutive steps (kernel trace: k_inc_lat ->
 // k_inc_lat gaps of 21 us under rocprofv3).
 template <int KA, class VT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_INC_WAVES, MFGP_INC_WAVES))) void k_inc_lat_arg(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_LAT_WAVES, MFGP_LAT_WAVES))) void k_inc_lat_arg(
     const DescArg a) {
   // index the kernarg segment itself: a dynamic index into the by-value argument
   // would copy all 9 KB of it to scratch

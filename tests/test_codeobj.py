@@ -8,7 +8,15 @@ seconds, surfacing only as MFGP_ERR_DEVICE after the bounded spin. These tests
 read the library's code object (tools/check_codeobj.py) and fail if either
 precondition is lost to a toolchain or inlining change: no call instruction in
 the stream kernels, <= 128 VGPRs and <= 40 KB of LDS (four 256-thread
-workgroups per CU), and no scratch beyond the few spill slots measured."""
+workgroups per CU), and no scratch beyond the few spill slots measured.
+
+The lattice step (k_inc_lat / k_inc_lat_arg, mfgp_lattice.inl) rests on the same
+residency: its roles wait only on roles dispatched before them, and with split-K
+the splits of a tile wait for each other, which the host allows only while every
+GEMM workgroup of the launch fits beside the rest (tiles x S <= 2 per CU of the
+four). Its guard: call-free, <= 128 VGPR + AGPR, <= 40 KB LDS, scratch <= 256
+bytes per lane (the measured spill slots: 80-180), and a forced-spill build
+(MFGP_LAT_WAVES=8: a 64-VGPR budget) must fail that bound."""
 import os
 import subprocess
 import sys
@@ -18,6 +26,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 STREAM = ("k_inc_stream", "k_vstream")
+LATTICE = ("k_inc_lat",)
+LAT_SCRATCH_MAX = 256
 
 
 @pytest.fixture(scope="module")
@@ -51,14 +61,44 @@ def test_every_kernel_is_call_free(report):
         assert r["calls"] == 0, (n, r)
 
 
-def test_forced_outline_is_caught(tmp_path):
+@pytest.fixture(scope="module")
+def diag_report(tmp_path_factory):
+    """One diagnostic build for both negative checks: the producer outlined
+    (MFGP_NOINLINE_PRODUCE) and the lattice kernels squeezed to 64 VGPRs
+    (MFGP_LAT_WAVES=8)."""
+    import check_codeobj
+    obj = tmp_path_factory.mktemp("diag") / "k.o"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                    "-DMFGP_NOINLINE_PRODUCE", "-DMFGP_LAT_WAVES=8", "-c",
+                    os.path.join(ROOT, "mfgp_coverage_amd", "csrc", "mfgp_kernels.hip"), "-o", str(obj)],
+                   check=True, capture_output=True)
+    return check_codeobj.kernel_report(str(obj))
+
+
+def test_forced_outline_is_caught(diag_report):
     """The check fires on the failure it guards against: a build with the
     producer outlined (MFGP_NOINLINE_PRODUCE) has a call inside k_inc_stream."""
-    import check_codeobj
-    obj = tmp_path / "k.o"
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                    "-DMFGP_NOINLINE_PRODUCE", "-c", os.path.join(ROOT, "mfgp_coverage_amd", "csrc", "mfgp_kernels.hip"),
-                    "-o", str(obj)], check=True, capture_output=True)
-    rep = check_codeobj.kernel_report(str(obj))
-    inc = [r for n, r in rep.items() if "k_inc_stream" in n]
+    inc = [r for n, r in diag_report.items() if "k_inc_stream" in n]
     assert inc and all(r["calls"] > 0 for r in inc), inc
+
+
+def _lattice(rep):
+    ks = {n: r for n, r in rep.items() if any(s in n for s in LATTICE)}
+    assert len(ks) == 8, sorted(rep)   # KA 8 / 16 x <double> / <float> of k_inc_lat and k_inc_lat_arg
+    return ks
+
+
+def _lattice_ok(r):
+    return (r["calls"] == 0 and r["vgpr"] + r["agpr"] <= 128 and r["lds"] <= 40 * 1024
+            and r["scratch"] <= LAT_SCRATCH_MAX)
+
+
+def test_lattice_kernels_fit_four_workgroups_per_cu(report):
+    for n, r in _lattice(report).items():
+        assert _lattice_ok(r), (n, r)
+
+
+def test_forced_spill_lattice_build_is_caught(diag_report):
+    """A lattice build squeezed to 64 VGPRs spills far past the scratch bound."""
+    lat = _lattice(diag_report)
+    assert all(not _lattice_ok(r) for r in lat.values()), lat
