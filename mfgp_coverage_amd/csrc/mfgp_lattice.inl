@@ -787,7 +787,12 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
   drain_stores();
   __syncthreads();
   WTRACE(6);
-  if (tid == 0) arrive_phase(d.ldone + 2, epoch, d.nzu);
+  // this unit's rows are stored (the GEMM stages over them wait for this flag),
+  // then the count of all Z units (the virtual stages wait for that)
+  if (tid == 0) {
+    publish(d.zflag + zu, epoch);
+    arrive_phase(d.ldone + 2, epoch, d.nzu);
+  }
   WTRACE(2);
 }
 
@@ -1108,11 +1113,14 @@ __device__ __forceinline__ void lat_epi(const GPDesc& d, int64_t tile, int64_t s
 }
 
 // One GEMM tile (split s of ksplit): 128 (a, ix) rows x 64 iy columns, i.e.
-// (128 / KA) x 64 cells, over the K rows of both parts: per part the lattice
-// y-rows q < round_up(ny, ZKS) (A = Z rows, B = axis-table rows ey(q, iy)), then
-// the part's virtual rows (A = Z rows, B = the row's own table row ey_j(iy)).
-// Split s takes stages s, s + S, ... For the last split to arrive: the cell
-// epilogue and the fused var max / argmax partials.
+// (128 / KA) x 64 cells, over the K rows of both parts: first every part's
+// lattice y-rows q < round_up(ny, ZKS) (A = Z rows, B = axis-table rows ey(q,
+// iy)), then every part's virtual rows (A = Z rows, B = the row's own table row
+// ey_j(iy)). Split s takes stages s, s + S, ... of each of the two lists. A wave
+// waits, before its DMA of an axis stage, only for the Z unit that stores its two
+// rows of it (zflag), so the K loop starts on the first Z units' rows while the
+// others are still at work; the virtual stages (rows of every Z unit) wait for
+// all of Z.
 template <int KA, class VT>
 __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t s, double* sm) {
   constexpr int IXPT = 128 / KA;   // lattice columns x per tile
@@ -1127,20 +1135,11 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   const int64_t ix0 = tix * IXPT, iy0 = tiy * 64;
   const int P = d.hp.kind == 0 ? 1 : 2;
   const int64_t zq8 = (lat.ny + ZKS - 1) / ZKS * ZKS;
+  const int ZQ = d.zq;
+  const int64_t nu = d.nzu / P;   // Z units per part
   const unsigned epoch = d.epoch;
-  WTRACE(0);
-  // every Z unit of the GP (they waited for all of w) -- one wait, then no flags
-  wait_phase(d, d.ldone + 2, epoch);
-  WTRACE(1);
-  // stages per part: the axis rows, then the virtual rows (counts from the Z units)
   const int* const zvl = d.zvl;
-  int64_t nsp[2] = {0, 0};
-  for (int pt = 0; pt < P; ++pt) {
-    const int64_t nv = __hip_atomic_load(zvl + pt * (zrows + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    nsp[pt] = (zq8 + (nv + ZKS - 1) / ZKS * ZKS) / ZKS;
-  }
-  const int64_t NS = nsp[0] + nsp[1];
-  const int64_t hi = s < NS ? (NS - s + S - 1) / S : 0;   // this split's stages
+  WTRACE(0);
   const __amdgpu_buffer_rsrc_t rZ = make_rsrc(d.zb, (int64_t)8 * P * zrows * tabw * KA);
   const __amdgpu_buffer_rsrc_t rAx = make_rsrc(d.axt, (int64_t)8 * 4 * (tabw + 1) * tabw);
   const __amdgpu_buffer_rsrc_t rTab = make_rsrc(d.tab, (int64_t)8 * 4 * tstride);
@@ -1148,17 +1147,31 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   const unsigned vA0 = (unsigned)(8 * (2 * lane)), vA1 = (unsigned)(8 * ((2 * lane) ^ 16));
   const unsigned vBc = (unsigned)(8 * (((lane & 31) * 2) ^ ((lane >> 5) << 4)));
   const unsigned vB = vBc + (unsigned)(8 * (lane >> 5) * tabw);
-  auto issue = [&](int64_t t) {   // stage t's DMAs: 3 per wave
-    const int64_t g = s + t * S;
-    const int pt = g < nsp[0] ? 0 : 1;
-    const int64_t q0 = (g - (pt ? nsp[0] : 0)) * ZKS;
-    double* slot = sm + (t % LNST) * LSTG;
+  // stage lists: NA axis stages (part-major), then the virtual stages of part 0
+  // and of part 1 (nv8[pt] / ZKS each, known once all of Z is stored)
+  const int64_t npa = zq8 / ZKS, NA = P * npa;
+  int64_t nvs[2] = {0, 0};
+  auto issue = [&](int64_t g, bool virt, int64_t slot_t) {   // stage g's DMAs: 3 per wave
+    int pt;
+    int64_t q0;
+    if (!virt) {
+      pt = g < npa ? 0 : 1;
+      q0 = (g - pt * npa) * ZKS;
+      // the Z unit that stores this wave's rows q0 + 2 w, + 1 (padding rows past
+      // ny: nobody's; zero since allocation)
+      const int64_t zc = (q0 + 2 * w) / ZQ;
+      if (zc < nu) spin_wave(d, d.zflag + pt * nu + zc, epoch);
+    } else {
+      pt = g < nvs[0] ? 0 : 1;
+      q0 = zq8 + (g - (pt ? nvs[0] : 0)) * ZKS;
+    }
+    double* slot = sm + (slot_t % LNST) * LSTG;
     const int64_t ar = (pt * zrows + q0 + 2 * w) * tabw + ix0;
     // the Z rows were stored in this launch: L2-served (sc1) DMA loads
     dma_buf_sc1(rZ, slot + (2 * w) * 128, vA0, (unsigned)(8 * ar * KA));
     dma_buf_sc1(rZ, slot + (2 * w + 1) * 128, vA1, (unsigned)(8 * (ar + tabw) * KA));
     double* bdst = slot + ZKS * 128 + 2 * w * 64;
-    if (q0 < zq8) {
+    if (!virt) {
       dma_buf(rAx, bdst, vB, (unsigned)(8 * (((2 * pt + 1) * (tabw + 1) + q0 + 2 * w) * tabw + iy0)));
     } else {
       // virtual rows: each half-wave its own training row's table row
@@ -1177,14 +1190,35 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   constexpr int D = LNST - 1;   // stages in flight ahead of the one consumed
   constexpr int CNT = 3;        // vector-memory ops per issued stage (every wave)
   static_assert(D * CNT <= 12, "vm_wait_bar covers the outstanding ops");
-  for (int64_t t = 0; t < D && t < hi; ++t) issue(t);
-  for (int64_t t = 0; t < hi; ++t) {
-    const int64_t after = (hi - 1 - t) < (D - 1) ? (hi - 1 - t) : (D - 1);
-    vm_wait_bar((int)after * CNT);
-    if (t + D < hi) issue(t + D);
+  // one pipelined pass over this split's stages of a list (stage t: list index
+  // s + t S); the ring slot runs on across the two passes
+  int64_t slot0 = 0;
+  auto pass = [&](int64_t nlist, bool virt) {
+    const int64_t hi = s < nlist ? (nlist - s + S - 1) / S : 0;
+    for (int64_t t = 0; t < D && t < hi; ++t) issue(s + t * S, virt, slot0 + t);
+    if (!virt) WTRACE(1);   // the first stages' Z units seen
+    for (int64_t t = 0; t < hi; ++t) {
+      const int64_t after = (hi - 1 - t) < (D - 1) ? (hi - 1 - t) : (D - 1);
+      vm_wait_bar((int)after * CNT);
 #ifndef MFGP_DIAG_LATNOCOMP   // diagnostic build: the pipeline without its compute (timing only)
-    lat_zcompute(sm + (t % LNST) * LSTG, acc, w, r, q);
+      lat_zcompute(sm + ((slot0 + t) % LNST) * LSTG, acc, w, r, q);
 #endif
+      // the next DMA after this stage's MFMAs: its wait for a Z unit never holds
+      // up a stage that is already here
+      if (t + D < hi) issue(s + (t + D) * S, virt, slot0 + t + D);
+    }
+    slot0 += hi;
+  };
+  pass(NA, false);
+  // the virtual stages: every Z unit of the GP stored its rows and counts
+  wait_phase(d, d.ldone + 2, epoch);
+  for (int pt = 0; pt < P; ++pt) {
+    const int64_t nv = __hip_atomic_load(zvl + pt * (zrows + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nvs[pt] = (nv + ZKS - 1) / ZKS;
+  }
+  if (nvs[0] + nvs[1] > 0) {
+    __syncthreads();   // the ring's last reads of the axis pass are done
+    pass(nvs[0] + nvs[1], true);
   }
   vm_wait_all();
   __syncthreads();
