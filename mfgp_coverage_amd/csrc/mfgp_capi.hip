@@ -99,7 +99,9 @@ struct mfgp_ctx {
   bool deferred = false;      // mfgp_append stages rows for a later (fused) bordered append
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
-  int lat_wu = 0;             // w units of a launch, all GPs (0: one per CU; MFGP_LAT_WU, diagnostics)
+  int lat_wu = 0;             // w units of a launch, all GPs (0: two per CU; MFGP_LAT_WU, diagnostics)
+  bool trinv_columns = false;  // F by the block-column k_trinv_f instead of recursive doubling (MFGP_TRINV_COLUMNS)
+  int factor_depth = 4;        // 64-column steps per trailing-update pass of the factor (MFGP_FACTOR_DEPTH; 1: one-level)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
@@ -745,13 +747,32 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   if (rc) return rc;
   HIP_TRY(launch_assemble(dd, count, max_tiles, c->stream));
   // Blocked right-looking Cholesky, per 64-column step: diagonal factor +
-  // inverse (k_potrf_diag), panel (k_panel), trailing update (k_syrk).
-  for (int kb = 0; kb < max_nb; ++kb) {
-    HIP_TRY(launch_potrf_diag(dd, count, kb, 0, c->stream));
-    const int64_t below = max_nb - kb - 1;
-    if (below > 0) {
-      HIP_TRY(launch_panel(dd, count, kb, below, c->stream));
-      HIP_TRY(launch_syrk(dd, count, kb, below * (below + 1) / 2, 0, c->stream));
+  // inverse (k_potrf_diag), panel (k_panel), trailing update. Two-level: the
+  // steps of a group of FD (c->factor_depth) update only the group's own columns
+  // (k_syrk_blk, one step deep), and the rest of the trailing matrix takes the
+  // group's FD steps in one pass (k_syrk_blk, FD deep) -- bit-equal to the
+  // one-level order, each trailing tile read and written once per group.
+  const int FD = std::max(1, c->factor_depth);
+  for (int64_t K0 = 0; K0 < max_nb; K0 += FD) {
+    const int64_t K1 = std::min<int64_t>(K0 + FD, max_nb);
+    for (int64_t kb = K0; kb < K1; ++kb) {
+      HIP_TRY(launch_potrf_diag(dd, count, (int)kb, 0, c->stream));
+      const int64_t below = max_nb - kb - 1;
+      if (below <= 0) continue;
+      HIP_TRY(launch_panel(dd, count, (int)kb, below, c->stream));
+      const int64_t jmax = std::min<int64_t>(K0 + FD - 1, max_nb - 1);
+      if (FD == 1) {
+        HIP_TRY(launch_syrk(dd, count, (int)kb, below * (below + 1) / 2, 0, c->stream));
+      } else if (jmax >= kb + 1) {
+        int64_t tiles = 0;
+        for (int64_t j = kb + 1; j <= jmax; ++j) tiles += max_nb - j;
+        HIP_TRY(launch_syrk_blk(dd, count, (int)kb, 1, (int)(kb + 1), (int)jmax, tiles, c->stream));
+      }
+    }
+    const int64_t jmin = K0 + FD;
+    if (FD > 1 && jmin < max_nb) {
+      const int64_t T = max_nb - jmin;
+      HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)jmin, INT32_MAX, T * (T + 1) / 2, c->stream));
     }
   }
   int64_t max_n = 0;
@@ -934,9 +955,31 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
     max_rows = std::max(max_rows, hd[i].n0 - hd[i].tab_lo);
     if (hd[i].lat_axbuild) max_axw = std::max(max_axw, hd[i].tabw);
   }
-  if (max_nbr > 0) HIP_TRY(launch_trinv_f(dd, count, max_nbr, c->stream));
+  // the builds a new factor / grid / hyperparameters need, timed as factor work
+  // (mfgp_ctx_get_timing's factor counters)
+  EvPair evb{};
+  if (max_nbr > 0 || max_rows > 0 || max_axw > 0) {
+    int rc = ev_begin(c, evb, 1);
+    if (rc) return rc;
+  }
+  if (max_nbr > 0) {
+    // recursive doubling needs a T scratch per GP (8 MB at n0 = 2048); MFGP_TRINV_COLUMNS=1:
+    // the block-column form (diagnostics)
+    const int64_t tstride = trinv_scratch(max_nbr);
+    double* tscr = nullptr;
+    if (!c->trinv_columns) {
+      int rc = ensure_ws(c, sizeof(double) * (size_t)(tstride * count));
+      if (rc) return rc;
+      tscr = c->ws;
+    }
+    HIP_TRY(launch_trinv_f(dd, count, max_nbr, tscr, tstride, c->stream));
+  }
   if (max_rows > 0) HIP_TRY(launch_lat_tables(dd, count, max_rows, c->stream));
   if (max_axw > 0) HIP_TRY(launch_lat_axes(dd, count, max_axw, c->stream));
+  {
+    int rc = ev_end(c, evb);
+    if (rc) return rc;
+  }
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
@@ -1150,6 +1193,8 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("MFGP_LAT_WU")) c->lat_wu = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("MFGP_TRINV_COLUMNS")) c->trinv_columns = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_FACTOR_DEPTH")) c->factor_depth = std::max(1, std::min(16, std::atoi(e)));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
     const int v = std::atoi(e);

@@ -113,6 +113,32 @@ __device__ __forceinline__ void store_tile(double* __restrict__ Ts, const Stage&
   }
 }
 
+// stage one 64x64 operand tile through registers (8 16-byte loads per thread)
+struct TileRegs {
+  dv2 v[8];
+};
+__device__ __forceinline__ void tile_fetch(TileRegs& t, const double* __restrict__ G, int64_t ld, int tid) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) t.v[p] = *reinterpret_cast<const GLOBAL dv2*>(gp(G) + (p * 8 + (tid >> 5)) * ld + (tid & 31) * 2);
+}
+// the tile's memory rows become k-rows: Ts[swz(k, i)] = G[k * ld + i]
+__device__ __forceinline__ void tile_put_k(double* __restrict__ Ts, const TileRegs& t, int tid) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int k = p * 8 + (tid >> 5), i = (tid & 31) * 2;
+    *reinterpret_cast<dv2*>(Ts + swz(k, i)) = t.v[p];
+  }
+}
+// transposed: Ts[swz(k, i)] = G[i * ld + k]
+__device__ __forceinline__ void tile_put_t(double* __restrict__ Ts, const TileRegs& t, int tid) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int i = p * 8 + (tid >> 5), k = (tid & 31) * 2;
+    Ts[swz(k, i)] = t.v[p].x;
+    Ts[swz(k + 1, i)] = t.v[p].y;
+  }
+}
+
 constexpr int PW = 128;                  // row width of the predict L image (= PRB)
 typedef __attribute__((address_space(3))) void* lds_vptr;
 

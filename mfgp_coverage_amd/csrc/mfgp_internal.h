@@ -170,6 +170,8 @@ hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStr
 hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStream_t s);
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s);
+hipError_t launch_syrk_blk(const GPDesc* d, int count, int kb0, int nk, int jmin, int jmax, int64_t max_tiles,
+                           hipStream_t s);
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s);
 #ifdef MFGP_STAMPS
 hipError_t set_stamps(long long* p);
@@ -202,7 +204,10 @@ hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipSt
 // axis tables (GPs with lat_axbuild); max_tabw = max over GPs of tabw
 hipError_t launch_lat_axes(const GPDesc* d, int count, int64_t max_tabw, hipStream_t s);
 // F = L^-1 of the n0 factor rows (block column per workgroup); max_nbr = max nblocks_rows(n0)
-hipError_t launch_trinv_f(const GPDesc* d, int count, int64_t max_nbr, hipStream_t s);
+// F = L^-1 for the lattice step: recursive doubling with tscr (trinv_scratch(max_nbr)
+// doubles per GP, tstride apart), or the block-column form without scratch
+hipError_t launch_trinv_f(const GPDesc* d, int count, int64_t max_nbr, double* tscr, int64_t tstride, hipStream_t s);
+int64_t trinv_scratch(int64_t nbr);
 hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf32, hipStream_t s);
 // MFGP_F32 full predict: round the fp64 V that k_predict wrote into d.V (rows [0, N)
 // of every tile) into the resident fp32 V (d.Vf)

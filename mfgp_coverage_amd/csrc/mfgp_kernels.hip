@@ -430,6 +430,81 @@ __global__ __launch_bounds__(NT) void k_syrk(const GPDesc* __restrict__ descs, i
       }
 }
 
+// Trailing update over nk consecutive 64-column steps kb0 .. kb0 + nk - 1 at once
+// (two-level blocking): A_ij -= sum_k L_ik L_jk^T for the lower tiles with jmin <=
+// j <= min(i, jmax). The accumulator stays in registers across the nk steps and
+// the MFMA sequence is k_syrk's, step after step, so the result is bit-equal to nk
+// k_syrk launches; the tile is read and written once instead of nk times, and
+// the next step's two operand tiles load while this step's MFMAs run.
+__global__ __launch_bounds__(NT) void k_syrk_blk(const GPDesc* __restrict__ descs, int kb0, int nk, int jmin,
+                                                 int jmax) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t nb = nblocks_factor(d.N);
+  if (kb0 >= nb) return;
+  const int64_t jm = jmax < nb - 1 ? jmax : nb - 1;
+  if (jmin > jm) return;
+  // tile t: column j (from jmin), row i >= j
+  int64_t t = blockIdx.x, ib = -1, jb = -1;
+  if (jm == nb - 1) {   // a triangle
+    const int64_t T = nb - jmin;
+    if (t >= T * (T + 1) / 2) return;
+    int ii, jj;
+    tri_index(t, ii, jj);
+    ib = jmin + ii;
+    jb = jmin + jj;
+  } else {              // a few columns
+    for (int64_t j = jmin; j <= jm; ++j) {
+      if (t < nb - j) {
+        ib = j + t;
+        jb = j;
+        break;
+      }
+      t -= nb - j;
+    }
+    if (ib < 0) return;
+  }
+  const int kn = (int)(kb0 + nk <= nb ? nk : nb - kb0);
+  __shared__ double As[TILE], Bs[TILE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t ld = d.ld;
+  double* __restrict__ A = d.A;
+  TileRegs ra, rb;
+  tile_fetch(ra, A + (int64_t)kb0 * NB * ld + ib * NB, ld, tid);
+  tile_fetch(rb, A + (int64_t)kb0 * NB * ld + jb * NB, ld, tid);
+  Acc acc;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
+        acc.c[mt][nt][v] = A[(jb * NB + col) * ld + ib * NB + row];
+      }
+  for (int s = 0; s < kn; ++s) {
+    if (s > 0) __syncthreads();   // the previous step's LDS reads are done
+    tile_put_k(As, ra, tid);
+    tile_put_k(Bs, rb, tid);
+    __syncthreads();
+    if (s + 1 < kn) {
+      const int64_t kc = (int64_t)(kb0 + s + 1) * NB;
+      tile_fetch(ra, A + kc * ld + ib * NB, ld, tid);
+      tile_fetch(rb, A + kc * ld + jb * NB, ld, tid);
+    }
+    tile_mma<true>(As, Bs, acc, wm, wn, lane);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = acc_row(wm, mt, q, v), col = acc_col(wn, nt, r);
+        A[(jb * NB + col) * ld + ib * NB + row] = acc.c[mt][nt][v];
+      }
+}
+
 // ---------------------------------------------------------------------------
 // Fused predict. One workgroup (256 threads, 4 waves; two workgroups per CU) =
 // one GP x 64 grid cells. For each 128-row block I of the training set
@@ -2521,6 +2596,12 @@ hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, h
 }
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s) {
   hipLaunchKernelGGL(k_syrk, dim3((unsigned)max_tri, count), dim3(NT), 0, s, d, kb, t0);
+  return hipGetLastError();
+}
+hipError_t launch_syrk_blk(const GPDesc* d, int count, int kb0, int nk, int jmin, int jmax, int64_t max_tiles,
+                           hipStream_t s) {
+  if (max_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_syrk_blk, dim3((unsigned)max_tiles, count), dim3(NT), 0, s, d, kb0, nk, jmin, jmax);
   return hipGetLastError();
 }
 hipError_t launch_predict(const GPDesc* d, int count, int64_t max_ctiles, hipStream_t s) {

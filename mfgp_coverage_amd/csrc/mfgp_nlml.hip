@@ -177,6 +177,88 @@ __global__ __launch_bounds__(NT) void k_trinv_f(const GPDesc* __restrict__ descs
   }
 }
 
+// ---------------------------------------------------------------------------
+// F = L^-1 of the n0 leading factor rows by recursive doubling (the lattice
+// step's F; replaces the block-column k_trinv_f, whose first workgroup ran the
+// whole column's chain of ~n0^2 / 8192 tile products, 1.9 ms for 8 GPs at the
+// headline). With L = [A 0; B C] over a group of 2h blocks of 64,
+//   L^-1 = [A^-1 0; -C^-1 B A^-1  C^-1],
+// so once every h-block diagonal group is inverted (level l - 1), level l (h =
+// 2^l) finishes the 2h-block groups in two launches of independent 64x64 output
+// tiles: T = B A^-1 (T_ij = sum_{k >= j} B_ik F11_kj), then F21 = -C^-1 T
+// (sum_{k <= i} F22_ik T_kj). Level 0's diagonal tiles are the factor's Linv
+// blocks. The top level's products are 16 deep at n0 = 2048 instead of 528.
+// Tiles of F are row-major 64 x 64 (fblk_off), T is a row-major scratch per GP.
+// ---------------------------------------------------------------------------
+// Level -1: the diagonal tiles F_JJ = Linv_JJ (row-major in F, column-major in Linv).
+__global__ __launch_bounds__(NT) void k_trinv_diag(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  const int64_t J = blockIdx.x;
+  if (!d.lat_fbuild || J >= nblocks_rows(d.n0)) return;
+  const double* Li = d.Linv + J * TILE;
+  double* Ft = d.F + fblk_off(J, d.ld);
+  for (int e = threadIdx.x; e < TILE; e += NT) {
+    const int r = e >> 6, c = e & 63;
+    Ft[e] = Li[c * NB + r];
+  }
+}
+
+// Level l, phase 0 (T = B F11) or 1 (F21 = -F22 T). Grid (groups x h x h tiles, GPs).
+template <int PHASE>
+__global__ __launch_bounds__(NT) void k_trinv_lvl(const GPDesc* __restrict__ descs, int h, double* __restrict__ tscr,
+                                                  int64_t tstride) {
+  const GPDesc& d = descs[blockIdx.y];
+  if (!d.lat_fbuild) return;
+  const int64_t nbr = nblocks_rows(d.n0), ld = d.ld;
+  const int64_t hh = (int64_t)h * h;
+  const int64_t grp = blockIdx.x / hh, rem = blockIdx.x % hh;
+  const int i = (int)(rem / h), j = (int)(rem % h);
+  const int64_t s = grp * 2 * h;                   // first block of the group
+  const int64_t h2 = nbr - s - h < h ? nbr - s - h : h;   // blocks in its second half
+  if (i >= h2) return;
+  double* const T = tscr + blockIdx.y * tstride + (grp * hh + (int64_t)i * h + j) * TILE;
+  __shared__ double As[TILE], Bs[TILE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int r = lane & 15, q = lane >> 4;
+  // operand tiles of product t: phase 0: A = B_ik (L, column-major), B = F11_kj
+  // (row-major), k = j + t; phase 1: A = F22_ik (row-major), B = T_kj, k = t
+  const int k0 = PHASE == 0 ? j : 0, k1 = PHASE == 0 ? h : i + 1;
+  auto a_src = [&](int k) -> const double* {
+    if (PHASE == 0) return d.A + (s + k) * NB * ld + (s + h + i) * NB;   // column-major tile, leading dim ld
+    return d.F + fblk_off(s + h + k, ld) + (int64_t)(i - k) * TILE;      // F22_ik: block column s+h+k, row s+h+i
+  };
+  auto b_src = [&](int k) -> const double* {
+    if (PHASE == 0) return d.F + fblk_off(s + j, ld) + (int64_t)(k - j) * TILE;   // F11_kj
+    return tscr + blockIdx.y * tstride + (grp * hh + (int64_t)k * h + j) * TILE;  // T_kj
+  };
+  Acc acc;
+  acc_zero(acc);
+  TileRegs ra, rb;
+  if (k0 < k1) {
+    tile_fetch(ra, a_src(k0), PHASE == 0 ? ld : NB, tid);
+    tile_fetch(rb, b_src(k0), NB, tid);
+  }
+  for (int k = k0; k < k1; ++k) {
+    __syncthreads();   // the previous product's LDS reads are done
+    if (PHASE == 0) tile_put_k(As, ra, tid);   // column-major B_ik: memory rows are its columns -> As[k][i] = B[i][k]
+    else tile_put_t(As, ra, tid);              // row-major F22_ik: As[k][i] = F[i][k]
+    tile_put_k(Bs, rb, tid);                   // row-major right operand: Bs[k][j] = X[k][j]
+    __syncthreads();
+    if (k + 1 < k1) {                          // the next product's tiles in flight during this one
+      tile_fetch(ra, a_src(k + 1), PHASE == 0 ? ld : NB, tid);
+      tile_fetch(rb, b_src(k + 1), NB, tid);
+    }
+    tile_mma<PHASE == 1>(As, Bs, acc, wm, wn, lane);
+  }
+  double* const out = PHASE == 0 ? T : d.F + fblk_off(s + j, ld) + (int64_t)(h + i - j) * TILE;   // F21_ij
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) out[acc_row(wm, mt, q, v) * NB + acc_col(wn, nt, r)] = acc.c[mt][nt][v];
+}
+
 // K^-1 = X^T X over the real rows (k < N): tile (I, J), I >= J, sums K >= I.
 __global__ __launch_bounds__(NT) void k_kinv(const GPDesc* __restrict__ descs, const double* __restrict__ Xi,
                                              double* __restrict__ Kv) {
@@ -276,10 +358,27 @@ __global__ __launch_bounds__(NT) void k_nlml_grad(const GPDesc* __restrict__ des
   if (tid < NHYP) part[(int64_t)blockIdx.x * NHYP + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
-hipError_t launch_trinv_f(const GPDesc* d, int count, int64_t max_nbr, hipStream_t s) {
+hipError_t launch_trinv_f(const GPDesc* d, int count, int64_t max_nbr, double* tscr, int64_t tstride, hipStream_t s) {
   if (max_nbr <= 0 || count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_trinv_f, dim3((unsigned)max_nbr, count), dim3(NT), 0, s, d);
+  if (!tscr) {   // (no scratch: the block-column form)
+    hipLaunchKernelGGL(k_trinv_f, dim3((unsigned)max_nbr, count), dim3(NT), 0, s, d);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_trinv_diag, dim3((unsigned)max_nbr, count), dim3(NT), 0, s, d);
+  for (int64_t h = 1; h < max_nbr; h *= 2) {
+    const int64_t groups = (max_nbr + 2 * h - 1) / (2 * h);
+    const dim3 grid((unsigned)(groups * h * h), count);
+    hipLaunchKernelGGL(k_trinv_lvl<0>, grid, dim3(NT), 0, s, d, (int)h, tscr, tstride);
+    hipLaunchKernelGGL(k_trinv_lvl<1>, grid, dim3(NT), 0, s, d, (int)h, tscr, tstride);
+  }
   return hipGetLastError();
+}
+// doubles of T scratch per GP for recursive doubling over nbr blocks: the largest
+// level's groups x h x h tiles
+int64_t trinv_scratch(int64_t nbr) {
+  int64_t m = 0;
+  for (int64_t h = 1; h < nbr; h *= 2) m = std::max(m, (nbr + 2 * h - 1) / (2 * h) * h * h);
+  return m * TILE;
 }
 hipError_t launch_nlml_value(const GPDesc* d, int count, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_nlml_value, dim3(count), dim3(NT), 0, s, d, out);
