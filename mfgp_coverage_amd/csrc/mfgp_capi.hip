@@ -100,6 +100,9 @@ struct mfgp_ctx {
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
   int lat_wu = 0;             // w units of a launch, all GPs (0: two per CU; MFGP_LAT_WU, diagnostics)
+  int lat_selfg = -1;         // w units read L21 from V themselves (-1: for one GP; MFGP_LAT_SELFG, diagnostics)
+  bool lat_gemm2 = true;      // the step's GEMM and cells as a second launch (k_lat_gemm2; MFGP_LAT_GEMM2=0:
+                              // in-launch split-K tiles, diagnostics)
   bool trinv_columns = false;  // F by the block-column k_trinv_f instead of recursive doubling (MFGP_TRINV_COLUMNS)
   int factor_depth = 4;        // 64-column steps per trailing-update pass of the factor (MFGP_FACTOR_DEPTH; 1: one-level)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
@@ -532,6 +535,9 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.nwu = 0;
   d.wpart = nullptr;
   d.wcnt = nullptr;
+  d.lat_selfg = 0;
+  d.lat_g2 = 0;
+  d.pad_g2_ = 0;
   d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
   d.hp = d.hf;
 }
@@ -586,6 +592,10 @@ bool lat_cond_ok(const mfgp_model* m) {
 int64_t lat_tabw(const mfgp_model* m) { return round_up(std::max<int64_t>(m->lat.nx, m->lat.ny), 64); }
 int64_t lat_tiles(const mfgp_model* m, int ka) {
   return ((m->lat.nx + 128 / ka - 1) / (128 / ka)) * ((m->lat.ny + 63) / 64);
+}
+// k_lat_gemm2's tiles: 64 (a, ix) rows x 64 iy columns
+int64_t lat_tiles2(const mfgp_model* m, int ka) {
+  return ((m->lat.nx + 64 / ka - 1) / (64 / ka)) * ((m->lat.ny + 63) / 64);
 }
 // Z units of the lattice-axis form: parts x ceil(ny / zq), zq lattice y-rows each
 // (two per thread group of tabw threads)
@@ -947,10 +957,11 @@ int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
 // and the separable tables they need (k_trinv_f / k_lat_tables: only when a model
 // enters the mode with a new factor, grid or hyperparameters).
 int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
-  int64_t max_blocks = 0, max_nbr = 0, max_rows = 0, max_axw = 0;
+  int64_t max_blocks = 0, max_nbr = 0, max_rows = 0, max_axw = 0, max_tiles = 0;
   for (int i = 0; i < count; ++i) {
     max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu +
-                                                   (int64_t)hd[i].lat_tiles * hd[i].ksplit);
+                                                   (hd[i].lat_g2 ? 0 : (int64_t)hd[i].lat_tiles * hd[i].ksplit));
+    max_tiles = std::max<int64_t>(max_tiles, hd[i].lat_tiles);
     if (hd[i].lat_fbuild) max_nbr = std::max(max_nbr, nblocks_rows(hd[i].n0));
     max_rows = std::max(max_rows, hd[i].n0 - hd[i].tab_lo);
     if (hd[i].lat_axbuild) max_axw = std::max(max_axw, hd[i].tabw);
@@ -984,6 +995,7 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
   HIP_TRY(launch_inc_lat(dd, count, max_blocks, hd[0].ka, hd[0].vf32, c->stream));
+  if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2(dd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
@@ -1010,14 +1022,17 @@ int enqueue_inc_stream_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
 }
 
 int enqueue_inc_lat_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
-  int64_t max_blocks = 0;
-  for (int i = 0; i < count; ++i)
+  int64_t max_blocks = 0, max_tiles = 0;
+  for (int i = 0; i < count; ++i) {
     max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu +
-                                                   (int64_t)hd[i].lat_tiles * hd[i].ksplit);
+                                                   (hd[i].lat_g2 ? 0 : (int64_t)hd[i].lat_tiles * hd[i].ksplit));
+    max_tiles = std::max<int64_t>(max_tiles, hd[i].lat_tiles);
+  }
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
   HIP_TRY(launch_inc_lat_arg(hd, count, max_blocks, hd[0].ka, hd[0].vf32, c->stream));
+  if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2_arg(hd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
@@ -1193,6 +1208,8 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("MFGP_LAT_WU")) c->lat_wu = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("MFGP_LAT_SELFG")) c->lat_selfg = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_LAT_GEMM2")) c->lat_gemm2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_TRINV_COLUMNS")) c->trinv_columns = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_FACTOR_DEPTH")) c->factor_depth = std::max(1, std::min(16, std::atoi(e)));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
@@ -1875,28 +1892,33 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       }
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];
-        tiles_sum += lat_tiles(m, ka);
+        tiles_sum += c->lat_gemm2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
         // K stages of the axis rows (virtual rows add more)
         const int64_t nst = (m->kind == MFGP_SF ? 1 : 2) * (round_up(m->lat.ny, ZKS) / ZKS);
         nst_min = std::min(nst_min, nst);
       }
-      // the lattice step has a fixed cost (its chain of dependent phases, ~58 us)
-      // plus the F stream (~2 TB/s effective); the V stream reads 8 n0 M bytes per GP
-      // (~5.5 TB/s) -- measured at 128x128, N = 2048 (tools/bench_lattice.py, us per
-      // launch, V stream / lattice): B = 1 60 / 65, B = 2 107 / 72, B = 4 185 / 91,
-      // B = 8 345 / 119; configs[4] (32 GPs, 256x256, N = 8192, fp32 V) 11.2 / 2.4 ms
-      double vs_us = 10.0, lat_us = 58.0;
+      // the lattice step has a fixed cost (its chain of dependent phases) plus the F
+      // stream and the GEMM (~0.8 us per million n0^2); the V stream reads 8 n0 M
+      // bytes per GP (~5.5 TB/s) -- measured at 128x128, N = 2048 (us per step, V
+      // stream / lattice with the second-launch GEMM, round 3): B = 8 345 / 80; B = 1
+      // 60 / 57 back to back, but ~66 / ~67+ in the drop-in simulator's step (one GP,
+      // ~40 us of host work between launches: rocprofv3, tools/prof_dropin.sh), so
+      // the fixed cost is priced at 64 and one GP at this size keeps the V stream;
+      // configs[4] (32 GPs, 256x256, N = 8192, fp32 V) 11.2 / 2.4 ms
+      double vs_us = 10.0, lat_us = 64.0;
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];
         const double n0 = (double)hd[i].n0, es = m->dtype == MFGP_F32 ? 4.0 : 8.0;
         vs_us += (double)m->M * n0 * es / 5.5e6;
-        lat_us += 4.0 * n0 * n0 / 2.0e6;
+        lat_us += 0.81 * n0 * n0 / 1.0e6;
       }
       if (lat_us >= vs_us && !c->lat_force) lat = false;
     }
     if (lat) {
       // split-K so that the GEMM tiles fill the chip about twice, >= 4 stages each
+      // (the second-launch GEMM splits K inside its workgroups: S = 1 here)
       int S = (int)std::min<int64_t>(8, std::max<int64_t>(1, (2 * c->ncu + tiles_sum - 1) / tiles_sum));
+      if (c->lat_gemm2) S = 1;
       // (split s takes every S-th stage: at least 4 each)
       S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nst_min / 4));
       if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, nst_min));
@@ -1913,13 +1935,22 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       // uneven count the CUs holding one more unit set the stream's pace; two per CU
       // keep twice the loads in flight: tools/probe_wloop.hip, B = 8: 25 vs 30 us),
       // each GP's count by its F steps
-      const int64_t wu_total = c->lat_wu > 0 ? c->lat_wu : 2 * c->ncu;
+      // and at least ~8 steps each: a block's partials are summed by one unit, four
+      // partials per round trip (one GP at 128x128, N = 2048: 512 units 57.1 us per
+      // launch, 256 units 52.4, 128 units 52.7; tools/sweep_lat_b1.sh)
       int64_t wsteps_sum = 0;
       for (int i = 0; i < ninc; ++i) wsteps_sum += lat_wsteps(hd[i].n0);
+      const int64_t wu_total =
+          c->lat_wu > 0 ? c->lat_wu : std::min<int64_t>(2 * c->ncu, std::max<int64_t>(c->ncu / 2, wsteps_sum / 8));
+      // w units that gather L21 from V themselves start the F stream at once; each
+      // row's gather is repeated in every block column it meets (~2x F's bytes in
+      // cache lines), which a batch's concurrent streams pay for (B = 8: 101.7 vs
+      // 99.5 us) and one GP does not (57.1 vs 60.3 us)
+      const int selfg = c->lat_selfg >= 0 ? c->lat_selfg : (ninc == 1 ? 1 : 0);
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
-        const int64_t tiles = lat_tiles(m, ka);
+        const int64_t tiles = c->lat_gemm2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
         const int64_t nzu = lat_nzu(m);
         if ((rc = ensure_lat(m, tiles, S, ka, nzu))) return rc;
         const int bin = res_find(m, fd.n0);
@@ -1958,6 +1989,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.nzu = (int)nzu;
         fd.zq = lat_zq(m);
         fd.lat_axbuild = m->axt_gen == m->gen ? 0 : 1;
+        fd.lat_selfg = selfg;
+        fd.lat_g2 = c->lat_gemm2 ? 1 : 0;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }
     }
@@ -1968,7 +2001,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     if (np > nv && (rc = assign_predict_scratch(c, hd + nb + nv, np - nv))) return rc;
     // one GP, append + one-pass predict fused, nothing else: launch with the
     // descriptor by value (no upload) and the status published into a mapped word
-    if (fuse && !lat && nb == 1 && ninc == 1 && np == 1 && nv == 1) {
+    // (the lattice step of one GP publishes its status the same way)
+    const bool single = fuse && nb == 1 && ninc == 1 && np == 1 && nv == 1;
+    if (single) {
       mfgp_model* m = order[0];
       if (!m->status_host) {
         HIP_TRY(hipHostMalloc(&m->status_host, sizeof(int), hipHostMallocMapped));
@@ -1983,6 +2018,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
           it->host = m->status_host;
           break;
         }
+    }
+    if (single && !lat) {
+      mfgp_model* m = order[0];
       EvPair ev{};
       if ((rc = ev_begin(c, ev, 0))) return rc;
       HIP_TRY(launch_inc_stream1(hd[0], hd[0].nprod + ntiles_wg(hd[0].M, hd[0].rsplit, hd[0].vf32), hd[0].vf32,

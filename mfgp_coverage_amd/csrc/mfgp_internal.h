@@ -135,6 +135,10 @@ struct GPDesc {
   int nzu;             // Z units per GP: parts x ceil(ny / zq)
   int zq;              // lattice y-rows per Z unit (2 NT / tabw)
   int lat_axbuild;     // k_lat_axes: 1 = build axt (new grid or hyperparameters)
+  int lat_selfg;       // k_inc_lat: 1 = the w units gather L21 from V themselves (lattice cells)
+  int lat_g2;          // 1 = the GEMM and cells run as a second launch (k_lat_gemm2; lat_tiles are
+                       // its 64-row tiles), k_inc_lat has no GEMM roles
+  int pad_g2_;
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -193,6 +197,10 @@ hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int
 hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s);
 // the same for count <= DESC_ARG_MAX GPs from host descriptors passed by value
 hipError_t launch_inc_stream_arg(const GPDesc* h, int count, int64_t max_blocks, int vf32, hipStream_t s);
+// the second launch of a lattice step (lat_g2): its GEMM and cells, max_tiles =
+// max over GPs of lat_tiles
+hipError_t launch_lat_gemm2(const GPDesc* d, int count, int64_t max_tiles, int ka, int vf32, hipStream_t s);
+hipError_t launch_lat_gemm2_arg(const GPDesc* h, int count, int64_t max_tiles, int ka, int vf32, hipStream_t s);
 // lattice-separable append + predict (k_inc_lat); max_blocks = max over GPs of
 // nprod + nwu + lat_tiles * ksplit
 hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);

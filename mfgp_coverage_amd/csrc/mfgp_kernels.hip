@@ -55,12 +55,26 @@ __device__ long long* g_stamps;
                  (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                                \
     }                                                                                                \
   } while (0)
+// the lattice step's second launch (k_lat_gemm2): its workgroups at role 1024 + tile
+#define WTRACE2(slot)                                                                                \
+  do {                                                                                               \
+    if (threadIdx.x == 0) {                                                                          \
+      long long* wt_ = g_stamps + 64 + 8 * ((1024 + blockIdx.y) * gridDim.x + blockIdx.x);           \
+      wt_[slot] = __builtin_amdgcn_s_memrealtime();                                                  \
+      if ((slot) == 0)                                                                               \
+        wt_[7] = ((long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |                       \
+                 (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                                \
+    }                                                                                                \
+  } while (0)
 #else
 #define FSTAMP(id) \
   do {             \
   } while (0)
 #define WTRACE(slot) \
   do {               \
+  } while (0)
+#define WTRACE2(slot) \
+  do {                \
   } while (0)
 #endif
 #ifndef MFGP_SPIN_SLEEP
@@ -2663,6 +2677,25 @@ hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, in
   else if (ka == 8) hipLaunchKernelGGL((k_inc_lat_arg<8, double>), g, dim3(NT), 0, s, a);
   else if (vf32) hipLaunchKernelGGL((k_inc_lat_arg<16, float>), g, dim3(NT), 0, s, a);
   else hipLaunchKernelGGL((k_inc_lat_arg<16, double>), g, dim3(NT), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_lat_gemm2(const GPDesc* d, int count, int64_t max_tiles, int ka, int vf32, hipStream_t s) {
+  const dim3 g(count, (unsigned)max_tiles);
+  if (ka == 8 && vf32) hipLaunchKernelGGL((k_lat_gemm2<8, float>), g, dim3(G2NT), 0, s, d);
+  else if (ka == 8) hipLaunchKernelGGL((k_lat_gemm2<8, double>), g, dim3(G2NT), 0, s, d);
+  else if (vf32) hipLaunchKernelGGL((k_lat_gemm2<16, float>), g, dim3(G2NT), 0, s, d);
+  else hipLaunchKernelGGL((k_lat_gemm2<16, double>), g, dim3(G2NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_lat_gemm2_arg(const GPDesc* h, int count, int64_t max_tiles, int ka, int vf32, hipStream_t s) {
+  if (count < 1 || count > DESC_ARG_MAX) return hipErrorInvalidValue;
+  DescArg a;
+  std::memcpy(a.d, h, sizeof(GPDesc) * count);
+  const dim3 g(count, (unsigned)max_tiles);
+  if (ka == 8 && vf32) hipLaunchKernelGGL((k_lat_gemm2_arg<8, float>), g, dim3(G2NT), 0, s, a);
+  else if (ka == 8) hipLaunchKernelGGL((k_lat_gemm2_arg<8, double>), g, dim3(G2NT), 0, s, a);
+  else if (vf32) hipLaunchKernelGGL((k_lat_gemm2_arg<16, float>), g, dim3(G2NT), 0, s, a);
+  else hipLaunchKernelGGL((k_lat_gemm2_arg<16, double>), g, dim3(G2NT), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_lat_axes(const GPDesc* d, int count, int64_t max_tabw, hipStream_t s) {

@@ -338,15 +338,40 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     f[0] = Fr[0];
     f[1] = Fr[16];
   };
+  // The A operand L21[r][i]. When every new point is the lattice cell its rounded
+  // axis estimate names (the producers' fast-path test, inc_gather_fast; every wave
+  // tests the same points, so the verdict is uniform), L21[r][.] is the V column
+  // of that cell, read here straight from the resident V (rows < n0: not written
+  // in this launch): the F stream starts at once instead of after the producers'
+  // compact rows (~9 us). Otherwise the compact rows, after the producers' flags.
+  const VT* asrc;
+  int64_t astr;
+  bool selfg;
+  {
+    const GridLattice L = d.lat;
+    const double* p = row_pt(d, n0 + (r < k ? r : 0));
+    const double px = p[0], py = p[1];
+    const int ix = (int)rint(fmin(fmax((px - L.x0) * L.xinv, 0.0), (double)(L.nx - 1)));
+    const int iy = (int)rint(fmin(fmax((py - L.y0) * L.yinv, 0.0), (double)(L.ny - 1)));
+    const int64_t cr = (px == px && py == py) ? ix * L.sx + iy * L.sy : 0;
+    const dv2 g = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid))[cr];
+    const bool miss = r < k && !(g.x == px && g.y == py);
+    selfg = d.lat_selfg && L.nx > 0 && d.vres >= n0 && vres_ptr<VT>(d) != nullptr && __ballot(miss) == 0;
+    asrc = selfg ? vres_ptr<VT>(d) + (cr / PBM) * d.vld * PBM + (cr % PBM)
+                 : reinterpret_cast<const VT*>(l21c) + r;
+    astr = selfg ? (int64_t)PBM : (int64_t)KINC;
+  }
   auto load_a = [&](const Cur& c, double& a) {
     const int64_t i = row_of(c);
-    a = l21c_ld<VT>(l21c, i < n0 ? i : n0 - 1, r);
+    // L2-served (the compact rows were stored in this launch)
+    a = (double)__hip_atomic_load(gp(asrc) + (i < n0 ? i : n0 - 1) * astr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   d4 acc[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+  // (columns a >= k of w are never read: zero)
   auto compute = [&](const dv2 (&f)[2], double a, bool live) {
-    const double av = live ? a : 0.0;
+    const double av = (live && r < k) ? a : 0.0;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       acc[2 * hh] = mfma(av, f[hh].x, acc[2 * hh]);
@@ -399,7 +424,7 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       ++tl;
     }
   };
-  {
+  if (!selfg) {
     // the unit's lowest row: its first step's, or (spanning more blocks) at most
     // pair p0 + 1's first block's first
     const int64_t lo = 64 * jb0 + 16 * st0;
@@ -868,6 +893,45 @@ __device__ __forceinline__ void lat_psum(const double* p0, int m, int nf, int ha
   }
 }
 
+// The epilogue's inputs of GEMM tile `tile`: the L22 record and the new rows'
+// separable tables for the tile's cells (L2-served loads: both were written in
+// this launch, before the L22 flag that the tile saw at its start). The GEMM
+// issues them before it stores its split-K partial, so that they arrive while
+// the tile's splits meet.
+template <int KA>
+struct LatEpiIn {
+  static constexpr int IXPT = 128 / KA;
+  static constexpr int FW = IXPT + 64;
+  static constexpr int NR = (KINC * KINC + KINC + NT - 1) / NT;
+  static constexpr int NF = (2 * KA * FW + NT - 1) / NT;
+  double rv[NR], fv[NF];
+};
+template <int KA>
+__device__ __forceinline__ void lat_epi_load(const GPDesc& d, int64_t tile, LatEpiIn<KA>& in) {
+  using E = LatEpiIn<KA>;
+  const int tid = threadIdx.x;
+  const int64_t ntiy = (d.lat.ny + 63) / 64;
+  const int64_t ix0 = (tile / ntiy) * E::IXPT, iy0 = (tile % ntiy) * 64;
+  const int64_t n0 = d.n0;
+  const int k = (int)(d.N - n0);
+#pragma unroll
+  for (int i = 0; i < E::NR; ++i) {
+    const int e = tid + NT * i;
+    in.rv[i] = e < KINC * KINC + KINC ? ldx<true>(d.l22r + e) : 0.0;
+  }
+  const int64_t tstride = d.ld * d.tabw, tabw = d.tabw;
+#pragma unroll
+  for (int i = 0; i < E::NF; ++i) {
+    const int e = tid + NT * i;
+    const int kind2 = e / (KA * E::FW), rem = e % (KA * E::FW);
+    const int a = rem / E::FW, col = rem % E::FW;
+    const bool isx = col < E::IXPT;
+    const int t = 2 * kind2 + (isx ? 0 : 1);
+    const int64_t idx = isx ? ix0 + col : iy0 + (col - E::IXPT);
+    in.fv[i] = (e < 2 * KA * E::FW && a < k) ? ldx<true>(&d.tab[t * tstride + (n0 + a) * tabw + idx]) : 0.0;
+  }
+}
+
 // The cells of GEMM tile `tile` (the share of split s of S, DESIGN.md section
 // 2.4): T = psi_new - T~ from the accumulators (SPLIT = false, S = 1) or from the
 // splits' stored partials (SPLIT = true; the caller waited until all are stored),
@@ -875,7 +939,8 @@ __device__ __forceinline__ void lat_psum(const double* p0, int m, int nf, int ha
 // rows, and the fused var max / argmax. A separate function per SPLIT, so that the
 // accumulators are dead here once a split has stored them.
 template <int KA, class VT, bool SPLIT>
-__device__ __forceinline__ void lat_epi(const GPDesc& d, int64_t tile, int64_t s, double* sm, const d4 (&acc)[2][4]) {
+__device__ __forceinline__ void lat_epi(const GPDesc& d, int64_t tile, int64_t s, double* sm, const d4 (&acc)[2][4],
+                                        const LatEpiIn<KA>& in) {
   constexpr int IXPT = 128 / KA;   // lattice columns x per tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -890,8 +955,7 @@ __device__ __forceinline__ void lat_epi(const GPDesc& d, int64_t tile, int64_t s
   const int k = (int)(d.N - n0);
   const int64_t tiles = d.lat_tiles;
   const double* p0 = d.gpart + tile * S * LAT_PART + (int64_t)w * 32 * 64 + lane;
-  // the L22 record (raised by the finish long before any K loop ends)
-  wait_flag(d, d.sync + 2, epoch);
+  (void)epoch;
   WTRACE(3);
   // ---- epilogue (LDS: the ring is dead) ----
   constexpr int FW = IXPT + 64;
@@ -929,7 +993,7 @@ __device__ __forceinline__ void lat_epi(const GPDesc& d, int64_t tile, int64_t s
   const double* const rmu_in = d.rmu_in;
   const double* const rvar_in = d.rvar_in;
   // the old posterior of this thread's cell in each of its passes (resident
-  // from the previous step: plain loads), in flight with the loads below
+  // from the previous step: plain loads)
   // (S = 1: the first pass's only; the passes prefetch one ahead, registers are short)
   // (S > 1: each pass loads its cell's with its partials, in one round trip)
   double ov0 = 0.0, om0 = 0.0;
@@ -943,27 +1007,11 @@ __device__ __forceinline__ void lat_epi(const GPDesc& d, int64_t tile, int64_t s
     }
   }
   {
-    // one round trip: the record and the new rows' tables (L2-served loads: both
-    // were written in this launch)
-    constexpr int NR = (KINC * KINC + KINC + NT - 1) / NT;
-    constexpr int NF = (2 * KA * FW + NT - 1) / NT;
-    double rv[NR], fv[NF];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int e = tid + NT * i;
-      rv[i] = e < KINC * KINC + KINC ? ldx<true>(d.l22r + e) : 0.0;
-    }
-    const int64_t tstride = d.ld * d.tabw, tabw = d.tabw;
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int e = tid + NT * i;
-      const int kind2 = e / (KA * FW), rem = e % (KA * FW);
-      const int a = rem / FW, col = rem % FW;
-      const bool isx = col < IXPT;
-      const int t = 2 * kind2 + (isx ? 0 : 1);
-      const int64_t idx = isx ? ix0 + col : iy0 + (col - IXPT);
-      fv[i] = (e < 2 * KA * FW && a < k) ? ldx<true>(&d.tab[t * tstride + (n0 + a) * tabw + idx]) : 0.0;
-    }
+    // the record and the new rows' tables (lat_epi_load, issued by the caller)
+    using E = LatEpiIn<KA>;
+    constexpr int NR = E::NR, NF = E::NF;
+    const double(&rv)[NR] = in.rv;
+    const double(&fv)[NF] = in.fv;
     __syncthreads();   // the ring's last reads are done
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
@@ -1140,6 +1188,9 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   const unsigned epoch = d.epoch;
   const int* const zvl = d.zvl;
   WTRACE(0);
+  // the L22 record (raised by the finish long before: the tile waits for Z units
+  // and w anyway), so that the epilogue's loads can go out with the K loop's end
+  wait_flag(d, d.sync + 2, epoch);
   const __amdgpu_buffer_rsrc_t rZ = make_rsrc(d.zb, (int64_t)8 * P * zrows * tabw * KA);
   const __amdgpu_buffer_rsrc_t rAx = make_rsrc(d.axt, (int64_t)8 * 4 * (tabw + 1) * tabw);
   const __amdgpu_buffer_rsrc_t rTab = make_rsrc(d.tab, (int64_t)8 * 4 * tstride);
@@ -1223,6 +1274,9 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   vm_wait_all();
   __syncthreads();
   WTRACE(2);
+  // the epilogue's inputs: in flight with the split-K partial's stores and the
+  // splits' meeting (issued behind the stores: the accumulators are then free)
+  LatEpiIn<KA> ein;
   // ---- split-K: every split stores its partial; the tile's splits meet (the
   // last to arrive raises the tile's flag), then split s sums the partials of
   // ITS share of the tile in split order ((p0 + p1) + p2 ...: the same bits
@@ -1238,6 +1292,7 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int v = 0; v < 4; ++v) stx<true>(part + ((m * 4 + n) * 4 + v) * 64, acc[m][n][v]);
+    lat_epi_load<KA>(d, tile, ein);
     drain_stores();
     __syncthreads();
     if (tid == 0) {
@@ -1249,9 +1304,11 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
       }
     }
     wait_flag(d, d.gcnt + tiles + tile, epoch);   // every split's partial is stored
+  } else {
+    lat_epi_load<KA>(d, tile, ein);
   }
-  if (S > 1) lat_epi<KA, VT, true>(d, tile, s, sm, acc);
-  else lat_epi<KA, VT, false>(d, tile, s, sm, acc);
+  if (S > 1) lat_epi<KA, VT, true>(d, tile, s, sm, acc, ein);
+  else lat_epi<KA, VT, false>(d, tile, s, sm, acc, ein);
 }
 
 template <int KA, class VT>
@@ -1275,7 +1332,10 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
   }
   if (role < np + d.nwu + d.nzu) {
 #ifdef MFGP_DIAG_LATNOZ   // diagnostic build: Z units count in at once (timing only, wrong results)
-    if (threadIdx.x == 0) arrive_phase(d.ldone + 2, d.epoch, d.nzu);
+    if (threadIdx.x == 0) {
+      publish(d.zflag + (role - np - d.nwu), d.epoch);
+      arrive_phase(d.ldone + 2, d.epoch, d.nzu);
+    }
     return;
 #endif
     lat_zunit<KA>(d, role - np - d.nwu, sm);
@@ -1285,7 +1345,7 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
   return;
 #endif
   const int64_t g = role - np - d.nwu - d.nzu;
-  if (g >= (int64_t)d.lat_tiles * d.ksplit) return;
+  if (d.lat_g2 || g >= (int64_t)d.lat_tiles * d.ksplit) return;   // (lat_g2: k_lat_gemm2 follows)
   const int64_t tile = g % d.lat_tiles, s = g / d.lat_tiles;
   lat_gemm<KA, VT>(d, tile, s, sm);
 }
@@ -1318,6 +1378,274 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_LAT_WAV
   (void)a;
   const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
   inc_lat_wg<KA, VT>(descs[blockIdx.x]);
+}
+
+// ---------------------------------------------------------------------------
+// The lattice step's GEMM and cells as a second launch (k_lat_gemm2, the default):
+// one 1024-thread workgroup per 64 (a, ix) x 64 iy tile, its K rows split four
+// ways over four groups of four waves -- split s takes the stages s, s + 4, ... of
+// each list, the order of the in-launch split-K at S = 4 -- and the splits' sums
+// meeting in LDS in split order, ((p0 + p1) + p2) + p3, then one cell per thread.
+// So no split-K partial goes through memory (64 KB stored and re-read per split
+// tile in the one-launch form: 66 MB per step at B = 8) and no hand-off flag is
+// polled: the kernel boundary orders the Z rows, the L22 record, the new rows'
+// tables and w after the first launch (producers, w units, Z units).
+// Measured at the headline (B = 8, per-workgroup traces, tools/trace_lat.py): the
+// one-launch form ended at 99-104 us, ~40 us after its last Z unit (K loop under
+// the Z units' flags, the split-K meeting through memory, the cells); the two
+// launches end at ~80 us: the first at ~58, this one ~2 us later and ~20 us long
+// (K loop ~16 us, the splits' meeting ~1.5, the cells ~2).
+// ---------------------------------------------------------------------------
+constexpr int G2S = 4;                          // K splits per workgroup
+constexpr int G2NT = 64 * 4 * G2S;              // threads per workgroup
+constexpr int G2R = 64;                         // (a, ix) rows per tile
+constexpr int G2STG = ZKS * G2R + ZKS * 64;     // doubles per stage: A [8][64] | B [8][64]
+constexpr int G2NST = 4;                        // stages in each split's ring
+constexpr int G2RING = G2S * G2NST * G2STG;     // the four rings
+constexpr int G2PARTS = (G2S - 1) * G2R * 64;  // splits 1..3's sums [3][64][64] (in the rings' place)
+static_assert(G2PARTS <= G2RING, "splits 1..3's sums fit the rings' place");
+constexpr int G2EPI = KINC * KINC + KINC + KINC * KINC + 2 * 16 * (4 + 64) + 2 * 16;
+constexpr int G2LDS = G2RING + G2EPI;           // 149 KB
+static_assert(2 * 8 * (8 + 64) <= 2 * 16 * (4 + 64), "both KA's tables fit");
+
+template <int KA, class VT>
+__device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
+  constexpr int IXPT = G2R / KA;   // lattice columns x per tile
+  constexpr int FW = IXPT + 64;
+  const int k = (int)(d.N - d.n0);
+  if (k <= 0 || k > KINC) return;
+  if (d.gate && *d.gate == 0) return;
+  if (tile >= d.lat_tiles) return;   // (the grid is the batch's largest)
+  __shared__ double sm[G2LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wg = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s = wg >> 2, w = wg & 3;   // split, wave in the split
+  const int r = lane & 15, q = lane >> 4;
+  const GridLattice lat = d.lat;
+  const int64_t ntiy = (lat.ny + 63) / 64;
+  const int64_t tix = tile / ntiy, tiy = tile % ntiy;
+  const int64_t ix0 = tix * IXPT, iy0 = tiy * 64;
+  const int64_t tabw = d.tabw, zrows = d.zrows, tstride = d.ld * tabw;
+  const int P = d.hp.kind == 0 ? 1 : 2;
+  const int64_t zq8 = (lat.ny + ZKS - 1) / ZKS * ZKS;
+  const int64_t n0 = d.n0;
+  double* const L22 = sm + G2RING;                 // [16][16] | z2 [16]
+  double* const Li = L22 + KINC * KINC + KINC;     // L22^-1 [16][16]
+  double* const Fn = Li + KINC * KINC;             // new rows' tables [2][KA][FW]
+  double* const amx = Fn + 2 * 16 * (4 + 64);      // the waves' (max, argmax)
+  WTRACE2(0);
+  // ---- the cells' inputs (written by the first launch) ----
+  for (int e = tid; e < KINC * KINC + KINC; e += G2NT) {
+    const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+    L22[e] = use ? d.l22r[e] : 0.0;
+  }
+  for (int e = tid; e < 2 * KA * FW; e += G2NT) {
+    const int kind2 = e / (KA * FW), rem = e % (KA * FW);
+    const int a = rem / FW, col = rem % FW;
+    const bool isx = col < IXPT;
+    const int t = 2 * kind2 + (isx ? 0 : 1);
+    const int64_t idx = isx ? ix0 + col : iy0 + (col - IXPT);
+    Fn[e] = a < k ? d.tab[t * tstride + (n0 + a) * tabw + idx] : 0.0;
+  }
+  __syncthreads();
+  if (tid < KINC) {
+    // column c of L22^-1 by forward substitution
+    const int c = tid;
+    double x[KINC];
+#pragma unroll
+    for (int i = 0; i < KINC; ++i) {
+      double t = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int b = 0; b < i; ++b) t -= L22[i * KINC + b] * x[b];
+      x[i] = (i < k && i >= c) ? t / L22[i * KINC + i] : 0.0;
+      Li[i * KINC + c] = x[i];
+    }
+  }
+  // ---- the K loop: split s, wave w: tile rows 16 w + r, all 64 columns ----
+  // Each split streams its stages through its own LDS ring (buffer_load ... lds,
+  // G2NST stages, one s_barrier per stage for the whole workgroup: the four splits
+  // run in lockstep, a split past its own stages idles). Loading the MFMA operands
+  // straight into registers instead (no ring, no barriers) was not faster (K loop
+  // 18.3 vs 15.8 us at B = 8): the loop runs at ~34 TF of the ~45 TF a bare f64
+  // MFMA loop reaches with four waves per SIMD.
+  const __amdgpu_buffer_rsrc_t rZ = make_rsrc(d.zb, (int64_t)8 * P * zrows * tabw * KA);
+  const __amdgpu_buffer_rsrc_t rAx = make_rsrc(d.axt, (int64_t)8 * 4 * (tabw + 1) * tabw);
+  const __amdgpu_buffer_rsrc_t rTab = make_rsrc(d.tab, (int64_t)8 * 4 * tstride);
+  // lane offsets of a stage's DMAs (one instruction moves two 64-double rows: lanes
+  // 0-31 row 2 w, 32-63 row 2 w + 1): A rows swizzled by ((row & 3) << 4), B rows
+  // by ((row & 1) << 4) (swz)
+  const int kr = 2 * w + (lane >> 5);
+  const unsigned vA = (unsigned)(8 * (((lane & 31) * 2) ^ ((kr & 3) << 4)) + 8 * (lane >> 5) * tabw * KA);
+  const unsigned vBc = (unsigned)(8 * (((lane & 31) * 2) ^ ((lane >> 5) << 4)));
+  const unsigned vB = vBc + (unsigned)(8 * (lane >> 5) * tabw);
+  const int64_t npa = zq8 / ZKS, NA = P * npa;
+  int64_t nvs[2] = {0, 0};
+  for (int pt = 0; pt < P; ++pt) nvs[pt] = (d.zvl[pt * (zrows + 1)] + ZKS - 1) / ZKS;
+  double* const ring = sm + s * G2NST * G2STG;
+  auto issue = [&](int64_t g, bool virt, int64_t slot_t) {   // list entry g: 2 DMAs per wave
+    int pt;
+    int64_t q0;
+    if (!virt) {
+      pt = g < npa ? 0 : 1;
+      q0 = (g - pt * npa) * ZKS;
+    } else {
+      pt = g < nvs[0] ? 0 : 1;
+      q0 = zq8 + (g - (pt ? nvs[0] : 0)) * ZKS;
+    }
+    double* slot = ring + (slot_t % G2NST) * G2STG;
+    dma_buf(rZ, slot + (2 * w) * G2R, vA, (unsigned)(8 * ((pt * zrows + q0 + 2 * w) * tabw + ix0) * KA));
+    double* bdst = slot + ZKS * G2R + 2 * w * 64;
+    if (!virt) {
+      dma_buf(rAx, bdst, vB, (unsigned)(8 * (((2 * pt + 1) * (tabw + 1) + q0 + 2 * w) * tabw + iy0)));
+    } else {
+      // virtual rows: each half-wave its own training row's table row
+      const int* vl = d.zvl + pt * (zrows + 1) + 1 + (q0 - zq8) + 2 * w;
+      const int64_t j = (lane >> 5) ? vl[1] : vl[0];
+      dma_buf(rTab, bdst, vBc + (unsigned)(8 * j * tabw), (unsigned)(8 * ((2 * pt + 1) * tstride + iy0)));
+    }
+  };
+  d4 acc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
+  constexpr int D = G2NST - 1;   // stages in flight ahead of the one consumed
+  constexpr int CNT = 2;         // DMAs per issued stage (every wave)
+  static_assert((D - 1) * CNT <= 12, "vm_wait_bar covers the outstanding DMAs");
+  int64_t slot0 = 0;
+  auto pass = [&](int64_t nlist, bool virt) {
+    const int64_t hi = s < nlist ? (nlist - s + G2S - 1) / G2S : 0;   // this split's stages
+    const int64_t him = (nlist + G2S - 1) / G2S;                      // split 0's: the most
+    for (int64_t t = 0; t < D && t < hi; ++t) issue(s + t * G2S, virt, slot0 + t);
+    for (int64_t t = 0; t < him; ++t) {
+      // this wave's DMA groups issued for stages after t
+      const int64_t last = hi < t + D ? hi : t + D;
+      const int64_t after = last > t + 1 ? last - (t + 1) : 0;
+      vm_wait_bar((int)after * CNT);
+      if (t < hi) {
+        const double* slot = ring + ((slot0 + t) % G2NST) * G2STG;
+        const double* As = slot;
+        const double* Bs = slot + ZKS * G2R;
+        double a[2], b[2][4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int kk = 4 * e + q;
+          a[e] = As[kk * G2R + ((16 * w + r) ^ ((kk & 3) << 4))];
+#pragma unroll
+          for (int n = 0; n < 4; ++n) b[e][n] = Bs[swz(kk, 16 * n + r)];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // the reads ahead of the MFMAs
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[n] = mfma(a[e], b[e][n], acc[n]);
+        if (t + D < hi) issue(s + (t + D) * G2S, virt, slot0 + t + D);
+      }
+    }
+    slot0 += him;
+  };
+  pass(NA, false);
+  if (nvs[0] + nvs[1] > 0) {
+    __syncthreads();   // the ring's last reads of the axis pass are done
+    pass(nvs[0] + nvs[1], true);
+  }
+  vm_wait_all();
+  __syncthreads();   // every ring read is done: the rings become the splits' sums
+  WTRACE2(2);
+  // ---- the splits meet: 1..3 store their sums, split 0 adds them in split order ----
+  // element (16 w + q + 4 v, 16 n + r) of split s's tile is acc[n][v] of its lane
+  double* const Tt = sm;   // the tile's T~ [64][64] (split 1's place, then the sum)
+  if (s > 0) {
+    double* const P_ = sm + (s - 1) * G2R * 64;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) P_[(16 * w + q + 4 * v) * 64 + 16 * n + r] = acc[n][v];
+  }
+  __syncthreads();
+  if (s == 0) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int o = (16 * w + q + 4 * v) * 64 + 16 * n + r;
+        double t = acc[n][v] + sm[o];
+        t = t + sm[G2R * 64 + o];
+        t = t + sm[2 * G2R * 64 + o];
+        Tt[o] = t;
+      }
+  }
+  __syncthreads();
+  WTRACE2(3);
+  // ---- cells: thread t < IXPT x 64 finishes cell (ix0 + t / 64, iy0 + t % 64) ----
+  double bv = -__builtin_inf();
+  int64_t bi = INT64_MAX;
+  if (tid < IXPT * 64) {
+    const int ixl = tid >> 6, iyl = tid & 63;
+    const int64_t ix = ix0 + ixl, iy = iy0 + iyl;
+    if (ix < lat.nx && iy < lat.ny) {
+      const int64_t c = ix * lat.sx + iy * lat.sy;
+      const double cov = d.rvar_in[c], com = d.rmu_in[c];
+      VT* const vt = const_cast<VT*>(vres_ptr<VT>(d)) + (c / PBM) * d.vld * PBM + (c % PBM);
+      const double* const Tc = Tt + (ixl * KA) * 64 + iyl;
+      const int iyc = IXPT + iyl;
+      double vn[KA];
+      double vs = 0.0, ms = 0.0;
+#pragma unroll
+      for (int a = 0; a < KA; ++a) {
+        vn[a] = 0.0;
+        if (a < k) {
+          const double* fL = Fn + a * FW;
+          const double* fH = Fn + (KA + a) * FW;
+          const double pn = fL[ixl] * fL[iyc] + fH[ixl] * fH[iyc];
+          double t = pn - Tc[a * 64];
+#pragma unroll
+          for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+          vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
+          vs += vn[a] * vn[a];
+          ms += vn[a] * L22[KINC * KINC + a];
+          vt[(n0 + a) * PBM] = (VT)vn[a];
+        }
+      }
+      const double vc = cov - vs;
+      const double mc = com + ms;
+      d.mu[c] = mc;
+      d.var[c] = vc;
+      if (d.rmu) {
+        d.rmu[c] = mc;
+        d.rvar[c] = vc;
+      }
+      argmax_pair(bv, bi, vc, c);
+    }
+  }
+  WTRACE2(6);
+  if (d.vmax || d.vargmax || d.status_host) {
+    // the waves' (max, argmax) meet in LDS in wave order; wave 0 counts the tile in
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+    int64_t* const ami = reinterpret_cast<int64_t*>(amx);
+    if (lane == 0) {
+      amx[2 * wg] = bv;
+      ami[2 * wg + 1] = bi;
+    }
+    __syncthreads();
+    if (wg == 0) {
+      bv = amx[0];
+      bi = ami[1];
+      for (int ww = 1; ww < G2NT / 64; ++ww) argmax_pair(bv, bi, amx[2 * ww], ami[2 * ww + 1]);
+      var_argmax_group(d, bv, bi, tile, d.lat_tiles);
+    }
+  }
+  WTRACE2(4);
+}
+
+template <int KA, class VT>
+__global__ __launch_bounds__(G2NT) void k_lat_gemm2(const GPDesc* __restrict__ descs) {
+  lat_gemm2<KA, VT>(descs[blockIdx.x], blockIdx.y);
+}
+template <int KA, class VT>
+__global__ __launch_bounds__(G2NT) void k_lat_gemm2_arg(const DescArg a) {
+  (void)a;
+  const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
+  lat_gemm2<KA, VT>(descs[blockIdx.x], blockIdx.y);
 }
 
 // The separable tables of rows [tab_lo, n0) (full-path refresh; the step itself

@@ -365,3 +365,72 @@ def test_lattice_split_and_w_units_vs_oracle(monkeypatch, ksplit, wu):
         for i, (X, y, nl, n) in enumerate(data):
             mu_r, var_r = _ref(hyp, X[:n], y[:n], nl, Xs)
             assert _err(hyp, mh[i], vh[i], mu_r, var_r) < TOL, (ksplit, wu, "vstream", i)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_lattice_gemm2_equals_in_launch_split4(monkeypatch, dtype):
+    """The step's GEMM and cells as a second launch (k_lat_gemm2, the default: four
+    K splits inside one 1024-thread workgroup, their sums meeting in LDS) against
+    the one-launch form with split-K 4 through memory (MFGP_LAT_GEMM2=0,
+    MFGP_LAT_KSPLIT=4): the same stages per split and the same order of the
+    splits' sums, so the same bits -- mean, variance, fused max / argmax -- over
+    ragged batches (1 and 3 GPs) with off-lattice training rows (the virtual
+    stages), appends of 8, 3 and 12 rows (KA = 8 and 16), and the default form
+    against the oracle at every cell."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    hyp = _hyp("australia8_mf")
+    G = 64
+    dt = _lib.F32 if dtype == "f32" else _lib.F64
+
+    def run(ctx, B, check_oracle):
+        models, data = [], []
+        for i in range(B):
+            nl, nh = 120 + 13 * i, 160 - 7 * i
+            Xs, X, y = _data(G, nl + nh + 40, seed=90 + i)
+            X[5:9] += 0.31 / (G - 1)   # off-lattice lofi rows: virtual K rows
+            models.append(_model(ctx, hyp, X[:nl + nh], y[:nl + nh], nl, Xs, dtype=dt))
+            data.append((X, y, nl, nl + nh))
+        M = Xs.shape[0]
+        mu = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        var = torch.empty_like(mu)
+        vmax = torch.empty(B, dtype=torch.float64, device="cuda")
+        vam = torch.empty(B, dtype=torch.int64, device="cuda")
+        _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
+        out = []
+        for k in (8, 3, 12):
+            Xn = np.concatenate([X[n:n + k] for X, _, _, n in data])
+            yn = np.concatenate([y[n:n + k] for _, y, _, n in data])
+            Xt = torch.from_numpy(np.ascontiguousarray(Xn)).cuda()
+            yt = torch.from_numpy(np.ascontiguousarray(yn)).cuda()
+            _lib.batch_append_predict(models, Xt.data_ptr(), yt.data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
+                                      vmax_ptr=vmax.data_ptr(), vargmax_ptr=vam.data_ptr())
+            data = [(X, y, nl, n + k) for X, y, nl, n in data]
+            out.append((mu.cpu().numpy(), var.cpu().numpy(), vmax.cpu().numpy(), vam.cpu().numpy()))
+        assert all(m.stats()["lattice"] == 3 for m in models), [m.stats() for m in models]
+        if check_oracle:
+            mu_h, var_h = out[-1][0].reshape(B, M), out[-1][1].reshape(B, M)
+            for i, (X, y, nl, n) in enumerate(data):
+                mu_r, var_r = _ref(hyp, X[:n], y[:n], nl, Xs)
+                if dtype == "f64":
+                    assert _err(hyp, mu_h[i], var_h[i], mu_r, var_r) < TOL, i
+                else:
+                    e = O.parity_errors_f32(mu_h[i], var_h[i], mu_r, var_r, O.prior_variance(hyp))
+                    assert max(e) < O.F32_TOL, (i, e)
+                assert np.isclose(out[-1][2][i], var_h[i].max()) and out[-1][3][i] == int(np.argmax(var_h[i]))
+        ctx.synchronize()
+        return out
+
+    for B in (1, 3):
+        monkeypatch.setenv("MFGP_LAT_GEMM2", "0")
+        monkeypatch.setenv("MFGP_LAT_KSPLIT", "4")
+        a = _lib.Context(0)
+        monkeypatch.delenv("MFGP_LAT_GEMM2")
+        monkeypatch.delenv("MFGP_LAT_KSPLIT")
+        b = _lib.Context(0)
+        a.set_lattice("force")
+        b.set_lattice("force")
+        ra, rb = run(a, B, False), run(b, B, True)
+        for sa, sb in zip(ra, rb):
+            for xa, xb in zip(sa, sb):
+                assert np.array_equal(xa, xb), B

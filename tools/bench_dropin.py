@@ -33,5 +33,6 @@ for s in range(T):
     ts["updt_hifi"].append(t1 - t0); ts["predict"].append(t2 - t1); ts["np.diag+amax"].append(t3 - t2)
 import json
 res = {"mode": "deferred" if DEFERRED else "eager", "grid": G, "N_L": NL, "N_H": NH0 + K, "agents": K,
-       "steps_timed": T - 10, "us_median": {k: round(1e6 * float(np.median(v[10:])), 1) for k, v in ts.items()}}
+       "steps_timed": T - 10, "us_median": {k: round(1e6 * float(np.median(v[10:])), 1) for k, v in ts.items()},
+       "stats": {k: v for k, v in gp._dev().stats().items() if k in ("lattice", "lattice_arg", "vstream", "inc_factor")}}
 print(json.dumps(res))

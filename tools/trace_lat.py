@@ -58,21 +58,23 @@ nprod, nwb = 16, 32
 n0 = NL + NH0
 C16 = (n0 + 15) // 16
 wsteps = nwb * C16 - 2 * nwb * (nwb - 1)
-wu_total = int(os.environ.get("MFGP_LAT_WU", "0")) or 512
+wu_total = int(os.environ.get("MFGP_LAT_WU", "0")) or min(512, max(128, B * wsteps // 8))
 nwu = max(1, min((wu_total * wsteps + (B * wsteps) // 2) // (B * wsteps), 512, wsteps))
 wr = nwu
 wch = wr
 _zq = 2 * 256 // (((G + 63) // 64) * 64)
 nzu = 2 * ((G + _zq - 1) // _zq)
 role = np.arange(NWG) // B
+G2 = bool(used[role >= 1024].any())   # the GEMM as a second launch (k_lat_gemm2): roles 1024 + tile
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
 print(f"B={B} ({nwu} w units, {nzu} Z units per GP): percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
 for name, sel, slots in (("producer", role < nprod, (0, 1, 4)), ("w unit", (role >= nprod) & (role < nprod + nwu), (0, 1, 3, 2)),
                          ("Z unit", (role >= nprod + nwu) & (role < nprod + nwu + nzu), (0, 1, 3, 4, 5, 6, 2)),
-                         ("gemm", (role >= nprod + nwu + nzu) & used, (0, 1, 2, 3, 5, 6, 4))):
+                         ("gemm", ((role >= 1024) if G2 else (role >= nprod + nwu + nzu)) & used,
+                          (0, 2, 3, 6, 4) if G2 else (0, 1, 2, 3, 5, 6, 4))):
     for sl in slots:
         print(f"  {name:9s} slot {sl}: {q(tr[sel, sl])}")
-gm = (role >= nprod + nwu + nzu) & used
+gm = ((role >= 1024) if G2 else (role >= nprod + nwu + nzu)) & used
 w = tr[(role >= nprod) & (role < nprod + nwu)]
 print(f"  w units published (slot 2, last arrivers): {q(w[:, 2])}")
 print(f"  w unit F loop (slot 3 - slot 1): {q(w[:, 3] - w[:, 1])}; reduce+publish (2 - 3): {q(w[:, 2] - w[:, 3])}")
