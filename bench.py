@@ -136,18 +136,25 @@ def pmc_traffic(kernel="k_predict", tag=None):
     correction of MI355X_MICROARCH.md section HBM)."""
     import glob
     import csv
+    import re
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.csv")))
     # profiles/<round>_hbm_traffic.csv: the headline; <round>_<tag>_hbm_traffic.csv: another workload
     files = [f for f in files if (f"_{tag}_" in os.path.basename(f)) == (tag is not None)
              and (tag is not None or "configs4" not in os.path.basename(f))]
     if not files:
         return None, None
+    # kernel: one name, or several (the launches of one step: their bytes add up)
+    names = [kernel] if isinstance(kernel, str) else list(kernel)
+    tot, found = 0.0, set()
     with open(files[-1]) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Name"]:
-                tot = float(row["fetch_bytes_corrected"]) + float(row["write_bytes"])
-                return tot, os.path.relpath(files[-1], ROOT)
-    return None, None
+            for n in names:
+                if n not in found and re.search(rf"::{n}(?![A-Za-z0-9_])", row["Name"]):
+                    tot += float(row["fetch_bytes_corrected"]) + float(row["write_bytes"])
+                    found.add(n)
+    if len(found) != len(names):
+        return None, None
+    return tot, os.path.relpath(files[-1], ROOT)
 
 
 def pmc_mfma(kernel):
@@ -493,19 +500,28 @@ def main():
         default_cfg = (a.workload, G, NL, NH, B, k, a.hyp, a.dtype) == ("headline", 128, 1024, 1024, 8, 8,
                                                                          "australia8_mf", "f64")
         c4_cfg = (G, NL, NH, B, a.hyp, a.dtype) == (256, 4096, 4096, 32, "australia9_mf", "f32")
+        # the lattice step is two launches (k_inc_lat: producers, w, Z; k_lat_gemm2: the
+        # GEMM and cells) unless MFGP_LAT_GEMM2=0 (the GEMM inside k_inc_lat)
+        g2 = os.environ.get("MFGP_LAT_GEMM2", "1") != "0"
         kern = "k_inc_lat" if lattice else ("k_inc_stream" if FUSED else "k_vstream")
+        if lattice and g2:
+            kern = ("k_inc_lat", "k_lat_gemm2")
         traffic, traffic_src = None, None
         if default_cfg or c4_cfg:
             # batches of <= 8 GPs run the step with its descriptors as the kernel argument
-            # (k_inc_lat_arg); larger ones upload them (k_inc_lat)
+            # (k_inc_lat_arg, k_lat_gemm2_arg); larger ones upload them (k_inc_lat, k_lat_gemm2)
             if lattice and B <= 8:
-                traffic, traffic_src = pmc_traffic("k_inc_lat_arg", "configs4" if c4_cfg else None)
+                ka_ = ("k_inc_lat_arg", "k_lat_gemm2_arg") if g2 else "k_inc_lat_arg"
+                traffic, traffic_src = pmc_traffic(ka_, "configs4" if c4_cfg else None)
                 if traffic is not None:
-                    kern = "k_inc_lat_arg"
+                    kern = ka_
             if traffic is None:
                 traffic, traffic_src = pmc_traffic(kern, "configs4" if c4_cfg else None)
+        kern = kern if isinstance(kern, str) else " + ".join(kern)
         if lattice:
-            update = ("incremental, lattice-separable, one launch per step (k_inc_lat): bordered-Cholesky append, "
+            update = ("incremental, lattice-separable, " + ("two launches per step (k_inc_lat: append, w, Z; "
+                      "k_lat_gemm2: GEMM + cells)" if g2 else "one launch per step (k_inc_lat)") +
+                      ": bordered-Cholesky append, "
                       "w = K11^-1 K12 from the resident L^-1; every training term lies on the grid's lattice, so "
                       "L21 V_old = sum over lattice rows of Z (w c ex summed per row) times axis-table rows: a "
                       "K = 2 ny f64 MFMA GEMM, no pass over V; mean / variance updated from the previous posterior")
@@ -516,8 +532,9 @@ def main():
                     "timing": f"HIP events around each of {inc['R']} launches of an untimed pass after the timed "
                               "region (no events inside the timed region)",
                     "design_note": "bytes = F's lower triangle (the w pass), the posterior in / out, the new V rows "
-                                   "and the Z rows; the launch is a chain of dependent phases (producers -> w -> "
-                                   "Z -> GEMM -> cells), latency- not bandwidth-bound (DESIGN.md section 2.4)"}
+                                   "and the Z rows; avg_launch_ms spans the step's launches (HIP events before the "
+                                   "first, after the last); the step is a chain of dependent phases (producers -> "
+                                   "w -> Z | GEMM -> cells), latency- not bandwidth-bound (DESIGN.md section 2.4)"}
         else:
             update = ("incremental, one launch per step (k_inc_stream): bordered-Cholesky append + one pass over "
                       "the resident V = L^-1 psi^T" if FUSED else

@@ -434,6 +434,8 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   WTRACE(1);
   // the first DEPTH - 1 steps' loads in the loop's own order (F, then L21c, per
   // step): the compiler's waits in the loop then count DEPTH - 1 steps in flight
+  // (issuing their F loads before the wait for the compact rows: within noise at
+  // B = 8, 89.3k vs 88.9k GP-updates/s, and 128 spilled VGPRs at KA = 16)
 #pragma unroll
   for (int b = 0; b + 1 < DEPTH; ++b) {
     load_f(cl, fb[b]);
@@ -807,7 +809,17 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
     const int64_t q0 = c * ZQ + hh * ZH;   // rows q0 .. q0 + ZH - 1, contiguous in zb
     const int64_t nrow = ny - q0 < ZH ? ny - q0 : ZH;
     double* const zr = zb + (part * zrows + q0) * tabw * KA;
-    for (int64_t e = tid; e < nrow * tabw * KA; e += NT) stx<true>(zr + e, zst[e]);
+    if (d.lat_g2) {
+      // read by the next launch (k_lat_gemm2): plain stores, no drain, no flags
+      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) zr[e] = zst[e];
+    } else {
+      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) stx<true>(zr + e, zst[e]);
+    }
+  }
+  if (d.lat_g2) {
+    WTRACE(6);
+    WTRACE(2);
+    return;
   }
   drain_stores();
   __syncthreads();
@@ -1400,7 +1412,10 @@ constexpr int G2S = 4;                          // K splits per workgroup
 constexpr int G2NT = 64 * 4 * G2S;              // threads per workgroup
 constexpr int G2R = 64;                         // (a, ix) rows per tile
 constexpr int G2STG = ZKS * G2R + ZKS * 64;     // doubles per stage: A [8][64] | B [8][64]
-constexpr int G2NST = 4;                        // stages in each split's ring
+#ifndef MFGP_G2NST
+#define MFGP_G2NST 4
+#endif
+constexpr int G2NST = MFGP_G2NST;               // stages in each split's ring
 constexpr int G2RING = G2S * G2NST * G2STG;     // the four rings
 constexpr int G2PARTS = (G2S - 1) * G2R * 64;  // splits 1..3's sums [3][64][64] (in the rings' place)
 static_assert(G2PARTS <= G2RING, "splits 1..3's sums fit the rings' place");
@@ -1602,16 +1617,18 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
           vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
           vs += vn[a] * vn[a];
           ms += vn[a] * L22[KINC * KINC + a];
-          vt[(n0 + a) * PBM] = (VT)vn[a];
+          __hip_atomic_store(vt + (n0 + a) * PBM, (VT)vn[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       const double vc = cov - vs;
       const double mc = com + ms;
-      d.mu[c] = mc;
-      d.var[c] = vc;
+      // write-through stores (sc1): the launch leaves no dirty L2 lines for its end
+      // to write back (MI355X_MICROARCH.md: a release writes back the XCD L2s)
+      __hip_atomic_store(d.mu + c, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.var + c, vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d.rmu) {
-        d.rmu[c] = mc;
-        d.rvar[c] = vc;
+        __hip_atomic_store(d.rmu + c, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.rvar + c, vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       argmax_pair(bv, bi, vc, c);
     }
