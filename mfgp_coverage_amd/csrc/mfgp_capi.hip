@@ -994,7 +994,7 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
-  HIP_TRY(launch_inc_lat(dd, count, max_blocks, hd[0].ka, hd[0].vf32, c->stream));
+  HIP_TRY(launch_inc_lat(dd, count, max_blocks, hd[0].ka, hd[0].vf32, !hd[0].lat_g2, c->stream));
   if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2(dd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
@@ -1031,7 +1031,7 @@ int enqueue_inc_lat_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
   EvPair ev{};
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
-  HIP_TRY(launch_inc_lat_arg(hd, count, max_blocks, hd[0].ka, hd[0].vf32, c->stream));
+  HIP_TRY(launch_inc_lat_arg(hd, count, max_blocks, hd[0].ka, hd[0].vf32, !hd[0].lat_g2, c->stream));
   if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2_arg(hd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }

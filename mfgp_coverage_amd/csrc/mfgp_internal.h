@@ -203,10 +203,12 @@ hipError_t launch_lat_gemm2(const GPDesc* d, int count, int64_t max_tiles, int k
 hipError_t launch_lat_gemm2_arg(const GPDesc* h, int count, int64_t max_tiles, int ka, int vf32, hipStream_t s);
 // lattice-separable append + predict (k_inc_lat); max_blocks = max over GPs of
 // nprod + nwu + lat_tiles * ksplit
-hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
+// g1: the GEMM tiles are roles of this launch (else k_lat_gemm2 follows: lat_g2)
+hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, bool g1, hipStream_t s);
 // the same with the `count` <= DESC_ARG_MAX host descriptors `h` passed by value as
 // the kernel argument (DescArg: no device copy of the descriptor array)
-hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s);
+hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, bool g1,
+                              hipStream_t s);
 // separable tables and lattice indices of rows [tab_lo, n0); max_rows = max over GPs of n0 - tab_lo
 hipError_t launch_lat_tables(const GPDesc* d, int count, int64_t max_rows, hipStream_t s);
 // axis tables (GPs with lat_axbuild); max_tabw = max over GPs of tabw

@@ -2660,23 +2660,38 @@ hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf
   else hipLaunchKernelGGL(k_vstream<double>, dim3((unsigned)max_ctiles, count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
-hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s) {
+hipError_t launch_inc_lat(const GPDesc* d, int count, int64_t max_blocks, int ka, int vf32, bool g1, hipStream_t s) {
   const dim3 g(count, (unsigned)max_blocks);
-  if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat<8, float>), g, dim3(NT), 0, s, d);
-  else if (ka == 8) hipLaunchKernelGGL((k_inc_lat<8, double>), g, dim3(NT), 0, s, d);
-  else if (vf32) hipLaunchKernelGGL((k_inc_lat<16, float>), g, dim3(NT), 0, s, d);
-  else hipLaunchKernelGGL((k_inc_lat<16, double>), g, dim3(NT), 0, s, d);
+  if (g1) {
+    if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat<8, float, true>), g, dim3(NT), 0, s, d);
+    else if (ka == 8) hipLaunchKernelGGL((k_inc_lat<8, double, true>), g, dim3(NT), 0, s, d);
+    else if (vf32) hipLaunchKernelGGL((k_inc_lat<16, float, true>), g, dim3(NT), 0, s, d);
+    else hipLaunchKernelGGL((k_inc_lat<16, double, true>), g, dim3(NT), 0, s, d);
+  } else {
+    if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat<8, float, false>), g, dim3(NT), 0, s, d);
+    else if (ka == 8) hipLaunchKernelGGL((k_inc_lat<8, double, false>), g, dim3(NT), 0, s, d);
+    else if (vf32) hipLaunchKernelGGL((k_inc_lat<16, float, false>), g, dim3(NT), 0, s, d);
+    else hipLaunchKernelGGL((k_inc_lat<16, double, false>), g, dim3(NT), 0, s, d);
+  }
   return hipGetLastError();
 }
-hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, hipStream_t s) {
+hipError_t launch_inc_lat_arg(const GPDesc* h, int count, int64_t max_blocks, int ka, int vf32, bool g1,
+                              hipStream_t s) {
   if (count < 1 || count > DESC_ARG_MAX) return hipErrorInvalidValue;
   DescArg a;
   std::memcpy(a.d, h, sizeof(GPDesc) * count);
   const dim3 g(count, (unsigned)max_blocks);
-  if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat_arg<8, float>), g, dim3(NT), 0, s, a);
-  else if (ka == 8) hipLaunchKernelGGL((k_inc_lat_arg<8, double>), g, dim3(NT), 0, s, a);
-  else if (vf32) hipLaunchKernelGGL((k_inc_lat_arg<16, float>), g, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL((k_inc_lat_arg<16, double>), g, dim3(NT), 0, s, a);
+  if (g1) {
+    if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat_arg<8, float, true>), g, dim3(NT), 0, s, a);
+    else if (ka == 8) hipLaunchKernelGGL((k_inc_lat_arg<8, double, true>), g, dim3(NT), 0, s, a);
+    else if (vf32) hipLaunchKernelGGL((k_inc_lat_arg<16, float, true>), g, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_inc_lat_arg<16, double, true>), g, dim3(NT), 0, s, a);
+  } else {
+    if (ka == 8 && vf32) hipLaunchKernelGGL((k_inc_lat_arg<8, float, false>), g, dim3(NT), 0, s, a);
+    else if (ka == 8) hipLaunchKernelGGL((k_inc_lat_arg<8, double, false>), g, dim3(NT), 0, s, a);
+    else if (vf32) hipLaunchKernelGGL((k_inc_lat_arg<16, float, false>), g, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_inc_lat_arg<16, double, false>), g, dim3(NT), 0, s, a);
+  }
   return hipGetLastError();
 }
 hipError_t launch_lat_gemm2(const GPDesc* d, int count, int64_t max_tiles, int ka, int vf32, hipStream_t s) {

@@ -1323,7 +1323,10 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
   else lat_epi<KA, VT, false>(d, tile, s, sm, acc, ein);
 }
 
-template <int KA, class VT>
+// G1: the GEMM tiles are roles of this launch (the one-launch form, MFGP_LAT_GEMM2=0);
+// without them (the default, k_lat_gemm2 follows) the kernel carries no GEMM code,
+// which cuts its spilled VGPRs from 58 to 16 (KA = 8)
+template <int KA, class VT, bool G1>
 __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
   const int k = (int)(d.N - d.n0);
   if (k <= 0 || k > KINC) return;   // the host guarantees 0 < k <= KINC
@@ -1356,10 +1359,12 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
 #ifdef MFGP_DIAG_LATNOGEMM   // diagnostic build: producers, w and Z only (timing only)
   return;
 #endif
-  const int64_t g = role - np - d.nwu - d.nzu;
-  if (d.lat_g2 || g >= (int64_t)d.lat_tiles * d.ksplit) return;   // (lat_g2: k_lat_gemm2 follows)
-  const int64_t tile = g % d.lat_tiles, s = g / d.lat_tiles;
-  lat_gemm<KA, VT>(d, tile, s, sm);
+  if constexpr (G1) {
+    const int64_t g = role - np - d.nwu - d.nzu;
+    if (d.lat_g2 || g >= (int64_t)d.lat_tiles * d.ksplit) return;
+    const int64_t tile = g % d.lat_tiles, s = g / d.lat_tiles;
+    lat_gemm<KA, VT>(d, tile, s, sm);
+  }
 }
 
 // KA = 8 (appends of k <= 8 rows) or 16 (k <= 16): one kernel each, so each
@@ -1370,10 +1375,10 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
 #ifndef MFGP_LAT_WAVES
 #define MFGP_LAT_WAVES MFGP_INC_WAVES
 #endif
-template <int KA, class VT>
+template <int KA, class VT, bool G1>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_LAT_WAVES, MFGP_LAT_WAVES))) void k_inc_lat(
     const GPDesc* __restrict__ descs) {
-  inc_lat_wg<KA, VT>(descs[blockIdx.x]);
+  inc_lat_wg<KA, VT, G1>(descs[blockIdx.x]);
 }
 
 // The same step with the batch's descriptors as a by-value kernel argument (up
@@ -1382,14 +1387,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_LAT_WAV
 // on the copy engine, and its hand-off back to the compute queue put ~16 us of
 // idle stream time between consecutive steps (kernel trace: k_inc_lat ->
 // k_inc_lat gaps of 21 us under rocprofv3).
-template <int KA, class VT>
+template <int KA, class VT, bool G1>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFGP_LAT_WAVES, MFGP_LAT_WAVES))) void k_inc_lat_arg(
     const DescArg a) {
   // index the kernarg segment itself: a dynamic index into the by-value argument
   // would copy all 9 KB of it to scratch
   (void)a;
   const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
-  inc_lat_wg<KA, VT>(descs[blockIdx.x]);
+  inc_lat_wg<KA, VT, G1>(descs[blockIdx.x]);
 }
 
 // ---------------------------------------------------------------------------

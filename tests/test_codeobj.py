@@ -84,7 +84,9 @@ def test_forced_outline_is_caught(diag_report):
 
 def _lattice(rep):
     ks = {n: r for n, r in rep.items() if any(s in n for s in LATTICE)}
-    assert len(ks) == 8, sorted(rep)   # KA 8 / 16 x <double> / <float> of k_inc_lat and k_inc_lat_arg
+    # KA 8 / 16 x <double> / <float> x GEMM roles in the launch or not (k_lat_gemm2), of
+    # k_inc_lat and k_inc_lat_arg
+    assert len(ks) == 16, sorted(rep)
     return ks
 
 
@@ -102,3 +104,13 @@ def test_forced_spill_lattice_build_is_caught(diag_report):
     """A lattice build squeezed to 64 VGPRs spills far past the scratch bound."""
     lat = _lattice(diag_report)
     assert all(not _lattice_ok(r) for r in lat.values()), lat
+
+
+def test_lattice_gemm2_kernels_fit_one_workgroup_per_cu(report):
+    """The lattice step's second launch (k_lat_gemm2, 1024-thread workgroups): no
+    calls, <= 128 VGPRs (16 waves on a CU), its LDS within the CU's 160 KB, no spills."""
+    ks = {n: r for n, r in report.items() if "k_lat_gemm2" in n}
+    assert len(ks) == 8, sorted(report)
+    for n, r in ks.items():
+        assert r["calls"] == 0 and r["vgpr"] + r["agpr"] <= 128 and r["lds"] <= 160 * 1024, (n, r)
+        assert r["scratch"] == 0 and r["vgpr_spill"] == 0, (n, r)
