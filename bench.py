@@ -501,8 +501,13 @@ def main():
                                                                          "australia8_mf", "f64")
         c4_cfg = (G, NL, NH, B, a.hyp, a.dtype) == (256, 4096, 4096, 32, "australia9_mf", "f32")
         # the lattice step is two launches (k_inc_lat: producers, w, Z; k_lat_gemm2: the
-        # GEMM and cells) unless MFGP_LAT_GEMM2=0 (the GEMM inside k_inc_lat)
-        g2 = os.environ.get("MFGP_LAT_GEMM2", "1") != "0"
+        # GEMM and cells) where k_lat_gemm2's tiles fill the chip once or twice (the
+        # library's rule, mfgp_capi.hip), else one (the GEMM inside k_inc_lat);
+        # MFGP_LAT_GEMM2=1 / 0 forces either
+        ka_ = 8 if k <= 8 else 16
+        t2 = B * (-(-G // (64 // ka_))) * (-(-G // 64))
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        g2 = {"1": True, "0": False}.get(os.environ.get("MFGP_LAT_GEMM2", ""), ncu <= t2 <= 2 * ncu)
         kern = "k_inc_lat" if lattice else ("k_inc_stream" if FUSED else "k_vstream")
         if lattice and g2:
             kern = ("k_inc_lat", "k_lat_gemm2")

@@ -101,8 +101,9 @@ struct mfgp_ctx {
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
   int lat_wu = 0;             // w units of a launch, all GPs (0: two per CU; MFGP_LAT_WU, diagnostics)
   int lat_selfg = -1;         // w units read L21 from V themselves (-1: for one GP; MFGP_LAT_SELFG, diagnostics)
-  bool lat_gemm2 = true;      // the step's GEMM and cells as a second launch (k_lat_gemm2; MFGP_LAT_GEMM2=0:
-                              // in-launch split-K tiles, diagnostics)
+  int lat_gemm2 = -1;         // the step's GEMM and cells as a second launch (k_lat_gemm2): -1 where its
+                              // tiles fill the chip once or twice, 1 always, 0 never (in-launch split-K
+                              // tiles); MFGP_LAT_GEMM2, diagnostics and tests
   bool trinv_columns = false;  // F by the block-column k_trinv_f instead of recursive doubling (MFGP_TRINV_COLUMNS)
   int factor_depth = 4;        // 64-column steps per trailing-update pass of the factor (MFGP_FACTOR_DEPTH; 1: one-level)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
@@ -1209,7 +1210,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("MFGP_LAT_WU")) c->lat_wu = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("MFGP_LAT_SELFG")) c->lat_selfg = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MFGP_LAT_GEMM2")) c->lat_gemm2 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_LAT_GEMM2")) c->lat_gemm2 = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("MFGP_TRINV_COLUMNS")) c->trinv_columns = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_FACTOR_DEPTH")) c->factor_depth = std::max(1, std::min(16, std::atoi(e)));
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
@@ -1886,13 +1887,24 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     res_depth.assign(ninc, 0);
     int ka = 8;
     int64_t tiles_sum = 0, nst_min = INT64_MAX;
+    bool g2 = false;
     if (lat) {
       for (int i = 0; i < ninc; ++i) {
         if (order[i]->NL + order[i]->NH - hd[i].n0 > 8) ka = 16;
       }
+      // the GEMM as a second launch (k_lat_gemm2: no split-K partials through memory,
+      // no hand-off flags) where its tiles fill the chip once or twice: at the
+      // headline (B = 8, 256 tiles) 80 vs 100 us per step; a batch of many more tiles
+      // (configs[4]: 4096) keeps the in-launch tiles, whose GEMM overlaps the other
+      // GPs' F streams (2.35 vs 3.05 ms per step), and so does one GP (52 vs 57 us)
+      {
+        int64_t t2 = 0;
+        for (int i = 0; i < ninc; ++i) t2 += lat_tiles2(order[i], ka);
+        g2 = c->lat_gemm2 > 0 || (c->lat_gemm2 < 0 && t2 >= c->ncu && t2 <= 2 * (int64_t)c->ncu);
+      }
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];
-        tiles_sum += c->lat_gemm2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
+        tiles_sum += g2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
         // K stages of the axis rows (virtual rows add more)
         const int64_t nst = (m->kind == MFGP_SF ? 1 : 2) * (round_up(m->lat.ny, ZKS) / ZKS);
         nst_min = std::min(nst_min, nst);
@@ -1918,7 +1930,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       // split-K so that the GEMM tiles fill the chip about twice, >= 4 stages each
       // (the second-launch GEMM splits K inside its workgroups: S = 1 here)
       int S = (int)std::min<int64_t>(8, std::max<int64_t>(1, (2 * c->ncu + tiles_sum - 1) / tiles_sum));
-      if (c->lat_gemm2) S = 1;
+      if (g2) S = 1;
       // (split s takes every S-th stage: at least 4 each)
       S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nst_min / 4));
       if (c->lat_ksplit > 0) S = (int)std::max<int64_t>(1, std::min<int64_t>(c->lat_ksplit, nst_min));
@@ -1940,8 +1952,13 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       // launch, 256 units 52.4, 128 units 52.7; tools/sweep_lat_b1.sh)
       int64_t wsteps_sum = 0;
       for (int i = 0; i < ninc; ++i) wsteps_sum += lat_wsteps(hd[i].n0);
-      const int64_t wu_total =
-          c->lat_wu > 0 ? c->lat_wu : std::min<int64_t>(2 * c->ncu, std::max<int64_t>(c->ncu / 2, wsteps_sum / 8));
+      // ... and for a large batch about 512 steps each, up to eight units per CU (more
+      // loads queued: configs[4], 32 GPs at N = 8192, 2.86 ms per step with 512 units,
+      // 2.41 with 2048; the headline keeps 512: 384 and 448 were slower)
+      int64_t wu_total = std::max<int64_t>(c->ncu / 2, wsteps_sum / 8);
+      if (wu_total > 2 * c->ncu)
+        wu_total = std::max<int64_t>(2 * c->ncu, std::min<int64_t>(8 * c->ncu, wsteps_sum / 512));
+      if (c->lat_wu > 0) wu_total = c->lat_wu;
       // w units that gather L21 from V themselves start the F stream at once; each
       // row's gather is repeated in every block column it meets (~2x F's bytes in
       // cache lines), which a batch's concurrent streams pay for (B = 8: 101.7 vs
@@ -1950,7 +1967,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
-        const int64_t tiles = c->lat_gemm2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
+        const int64_t tiles = g2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
         const int64_t nzu = lat_nzu(m);
         if ((rc = ensure_lat(m, tiles, S, ka, nzu))) return rc;
         const int bin = res_find(m, fd.n0);
@@ -1990,7 +2007,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.zq = lat_zq(m);
         fd.lat_axbuild = m->axt_gen == m->gen ? 0 : 1;
         fd.lat_selfg = selfg;
-        fd.lat_g2 = c->lat_gemm2 ? 1 : 0;
+        fd.lat_g2 = g2 ? 1 : 0;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }
     }

@@ -369,7 +369,8 @@ def test_lattice_split_and_w_units_vs_oracle(monkeypatch, ksplit, wu):
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_lattice_gemm2_equals_in_launch_split4(monkeypatch, dtype):
-    """The step's GEMM and cells as a second launch (k_lat_gemm2, the default: four
+    """The step's GEMM and cells as a second launch (k_lat_gemm2, the default where its
+    tiles fill the chip once or twice, forced here with MFGP_LAT_GEMM2=1: four
     K splits inside one 1024-thread workgroup, their sums meeting in LDS) against
     the one-launch form with split-K 4 through memory (MFGP_LAT_GEMM2=0,
     MFGP_LAT_KSPLIT=4): the same stages per split and the same order of the
@@ -425,9 +426,10 @@ def test_lattice_gemm2_equals_in_launch_split4(monkeypatch, dtype):
         monkeypatch.setenv("MFGP_LAT_GEMM2", "0")
         monkeypatch.setenv("MFGP_LAT_KSPLIT", "4")
         a = _lib.Context(0)
-        monkeypatch.delenv("MFGP_LAT_GEMM2")
+        monkeypatch.setenv("MFGP_LAT_GEMM2", "1")   # (these batches are below the chip's size)
         monkeypatch.delenv("MFGP_LAT_KSPLIT")
         b = _lib.Context(0)
+        monkeypatch.delenv("MFGP_LAT_GEMM2")
         a.set_lattice("force")
         b.set_lattice("force")
         ra, rb = run(a, B, False), run(b, B, True)
