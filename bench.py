@@ -504,10 +504,8 @@ def main():
         # GEMM and cells) where k_lat_gemm2's tiles fill the chip once or twice (the
         # library's rule, mfgp_capi.hip), else one (the GEMM inside k_inc_lat);
         # MFGP_LAT_GEMM2=1 / 0 forces either
-        ka_ = 8 if k <= 8 else 16
-        t2 = B * (-(-G // (64 // ka_))) * (-(-G // 64))
-        ncu = torch.cuda.get_device_properties(0).multi_processor_count
-        g2 = {"1": True, "0": False}.get(os.environ.get("MFGP_LAT_GEMM2", ""), ncu <= t2 <= 2 * ncu)
+        # (the model's lattice_g2 counter says which ran)
+        g2 = inc["stats"].get("lattice_g2", 0) >= K
         kern = "k_inc_lat" if lattice else ("k_inc_stream" if FUSED else "k_vstream")
         if lattice and g2:
             kern = ("k_inc_lat", "k_lat_gemm2")

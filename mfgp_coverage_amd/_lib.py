@@ -292,11 +292,13 @@ class Model:
         the steps that took the lattice-separable path (k_inc_lat); {lattice_virtual}: the
         off-lattice training rows (extra K rows) the last lattice step ran, as its
         device counters hold them (MF: summed over both kernel parts); {lattice_arg}:
-        the lattice steps launched with their descriptors by value (k_inc_lat_arg)."""
-        out = (ctypes.c_int64 * 11)()
-        check(lib().mfgp_model_stats(self.handle, out, 11))
+        the lattice steps launched with their descriptors by value (k_inc_lat_arg);
+        {lattice_g2}: the lattice steps whose GEMM and cells ran as a second launch
+        (k_lat_gemm2)."""
+        out = (ctypes.c_int64 * 12)()
+        check(lib().mfgp_model_stats(self.handle, out, 12))
         keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream",
-                "lattice_nx", "lattice_ny", "lattice", "lattice_virtual", "lattice_arg")
+                "lattice_nx", "lattice_ny", "lattice", "lattice_virtual", "lattice_arg", "lattice_g2")
         return dict(zip(keys, (int(v) for v in out)))
 
     def sample_points(self, threshold, max_points):

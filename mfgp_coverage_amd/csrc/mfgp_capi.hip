@@ -169,6 +169,7 @@ struct mfgp_model {
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0, n_lattice = 0;
   int64_t n_lattice_arg = 0;   // lattice steps launched with their descriptors by value (k_inc_lat_arg)
+  int64_t n_lattice_g2 = 0;    // lattice steps whose GEMM and cells ran as a second launch (k_lat_gemm2)
   // state generation: a new factor from scratch, a new grid or new hyperparameters
   // start a new one (the resident posterior, F and the tables belong to one)
   uint64_t gen = 1;
@@ -1712,10 +1713,10 @@ int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
     if (m->kind == MFGP_MF) HIP_TRY(hipMemcpy(&nv[1], m->zvl + m->zb_rows + 1, sizeof(int), hipMemcpyDeviceToHost));
     virt = (int64_t)nv[0] + nv[1];
   }
-  const int64_t v[11] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+  const int64_t v[12] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
                          m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice, virt,
-                         m->n_lattice_arg};
-  for (int i = 0; i < n && i < 11; ++i) out[i] = v[i];
+                         m->n_lattice_arg, m->n_lattice_g2};
+  for (int i = 0; i < n && i < 12; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
@@ -2080,6 +2081,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       if (lat && i < ninc) {
         m->n_lattice += 1;
         if (lat_arg) m->n_lattice_arg += 1;
+        if (g2) m->n_lattice_g2 += 1;
         m->F_n = m->v_n;   // F's new rows and the new rows' tables came with the step
         m->F_gen = m->gen;
         m->tab_n = m->v_n;

@@ -57,22 +57,45 @@ def shard_cells(M: int, world: int, rank: int, row: int = 1):
 
 
 def _gather_blocks(block, M, world, group):
-    """All-gather the ranks' [2, m_r] blocks (padded to the largest one) into [2, M]."""
+    """All-gather the ranks' [2, m_r] blocks (padded to the largest one) into [2, M].
+    block["data"]: this rank's block as host [2, m] (gloo), or block["mine"]: a
+    device [2, mmax] tensor the predict wrote into (nccl: no host round trip before
+    the collective, one device-to-host copy of the gathered blocks after it)."""
     import torch
     import torch.distributed as dist
 
-    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
     mmax = max(hi - lo for lo, hi in block["bounds"])
-    mine = torch.zeros((2, mmax), dtype=torch.float64, device=dev)
-    m = block["data"].shape[1]
-    if m:
-        mine[:, :m] = torch.from_numpy(block["data"]).to(dev)
-    parts = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(parts, mine, group=group)
+    mine = block.get("mine")
+    if mine is None:
+        dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        mine = torch.zeros((2, mmax), dtype=torch.float64, device=dev)
+        m = block["data"].shape[1]
+        if m:
+            mine[:, :m] = torch.from_numpy(block["data"]).to(dev)
+    parts = torch.empty((world, 2, mmax), dtype=torch.float64, device=mine.device)
+    dist.all_gather(list(parts.unbind(0)), mine, group=group)
+    ph = parts.cpu().numpy()
     out = np.empty((2, M), dtype=np.float64)
-    for (lo, hi), p in zip(block["bounds"], parts):
-        out[:, lo:hi] = p[:, :hi - lo].cpu().numpy()
+    for r, (lo, hi) in enumerate(block["bounds"]):
+        out[:, lo:hi] = ph[r, :, :hi - lo]
     return out
+
+
+def predict_block_device(model, xs_blk, mmax):
+    """The posterior of `model` at the cells xs_blk written straight into a device
+    tensor [2, mmax] (row 0 mean, row 1 variance; columns past the block zero) by
+    the batched C ABI's device-output path: no host copy of mean / variance."""
+    import torch
+
+    from . import _lib
+
+    mine = torch.zeros((2, mmax), dtype=torch.float64, device="cuda")
+    if xs_blk.shape[0]:
+        model._sync_data()
+        model._push_hyp()
+        model._grid_to_device(xs_blk)
+        _lib.batch_predict([model._dev()], mine[0].data_ptr(), mine[1].data_ptr())
+    return mine
 
 
 def predict_sharded(model, X_star, world=None, rank=None, group=None):
@@ -98,10 +121,17 @@ def predict_sharded(model, X_star, world=None, rank=None, group=None):
     row = lattice_row(xs)
     bounds = [shard_cells(M, world, r, row) for r in range(world)]
     lo, hi = bounds[rank]
-    if hi > lo:
-        mu, cov = model.predict(xs[lo:hi])
-        data = np.stack([np.asarray(mu, dtype=np.float64).reshape(-1), np.diag(cov)])
+    import torch.distributed as dist
+
+    if hasattr(model, "_dev") and dist.get_backend(group) == "nccl":
+        mmax = max(b - a for a, b in bounds)
+        block = {"bounds": bounds, "mine": predict_block_device(model, xs[lo:hi], mmax)}
     else:
-        data = np.empty((2, 0))
-    full = _gather_blocks({"bounds": bounds, "data": data}, M, world, group)
+        if hi > lo:
+            mu, cov = model.predict(xs[lo:hi])
+            data = np.stack([np.asarray(mu, dtype=np.float64).reshape(-1), np.diag(cov)])
+        else:
+            data = np.empty((2, 0))
+        block = {"bounds": bounds, "data": data}
+    full = _gather_blocks(block, M, world, group)
     return full[0].reshape(-1, 1), DiagCov(full[1])

@@ -409,6 +409,7 @@ def test_lattice_gemm2_equals_in_launch_split4(monkeypatch, dtype):
             data = [(X, y, nl, n + k) for X, y, nl, n in data]
             out.append((mu.cpu().numpy(), var.cpu().numpy(), vmax.cpu().numpy(), vam.cpu().numpy()))
         assert all(m.stats()["lattice"] == 3 for m in models), [m.stats() for m in models]
+        assert all(m.stats()["lattice_g2"] == (3 if check_oracle else 0) for m in models), [m.stats() for m in models]
         if check_oracle:
             mu_h, var_h = out[-1][0].reshape(B, M), out[-1][1].reshape(B, M)
             for i, (X, y, nl, n) in enumerate(data):

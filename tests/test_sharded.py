@@ -176,3 +176,23 @@ def test_predict_sharded_gpu_gloo(kind):
     # the unsharded device predict of the same model: the same factor, so to rounding
     np.testing.assert_allclose(res[0][1][0][0], mu0[:, 0], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(res[1][1][0][1], np.diag(cov0), rtol=1e-7, atol=1e-13)
+
+
+@pytest.mark.gpu
+def test_predict_block_device_equals_predict():
+    """The nccl path of predict_sharded: a rank's block predicted straight into a
+    device tensor (no host round trip before the all_gather) holds the same bits as
+    the host predict of that block, zero past it."""
+    import torch
+    from mfgp_coverage_amd.gaussian_process import MFGP
+    from mfgp_coverage_amd.sharded import predict_block_device, shard_cells
+    Xs, X, y = _data(48, 180, 2)
+    gp = MFGP(X[:90], y[:90], X[90:170], y[90:170], 1, 1)
+    gp.hyp = HYP_MF
+    gp.updt_info(gp.X_L, gp.y_L, gp.X_H, gp.y_H)
+    lo, hi = shard_cells(Xs.shape[0], 3, 1, 48)
+    mmax = hi - lo + 48
+    mine = predict_block_device(gp, Xs[lo:hi], mmax).cpu().numpy()
+    mu, cov = gp.predict(Xs[lo:hi])
+    assert np.array_equal(mine[0, :hi - lo], mu[:, 0]) and np.array_equal(mine[1, :hi - lo], np.diag(cov))
+    assert not mine[:, hi - lo:].any()
