@@ -136,6 +136,16 @@ int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k);
  * device memory. Results for host buffers are kept with the model: predicts of
  * an unchanged model return them again (the same bits, no launch). */
 int mfgp_predict(mfgp_model* m, double* mu, double* var);
+/* mfgp_predict without the host copy (the drop-in predict's path): the result is
+ * left in the model's mapped pinned result buffer, which is handed over to the
+ * caller -- *mu, *var point into it (writable, [M] each) until
+ * mfgp_release_view(*view); the model takes another buffer from a process-wide
+ * pool for its next host-bound predict, so a predict of an unchanged model after
+ * a view recomputes. M = 0: *mu = *var = *view = NULL. */
+int mfgp_predict_view(mfgp_model* m, double** mu, double** var, void** view);
+/* Return a buffer handed over by mfgp_predict_view (any thread, any time, also
+ * after its model or context is destroyed). */
+int mfgp_release_view(void* view);
 
 /* Sizes and state readers (the Python mirror's .X/.L attributes). */
 int64_t mfgp_model_n(const mfgp_model* m);      /* N = NL + NH */

@@ -58,6 +58,9 @@ SIGNATURES = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "mfgp_append": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "mfgp_predict": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mfgp_predict_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)]),
+    "mfgp_release_view": (ctypes.c_int, [ctypes.c_void_p]),
     "mfgp_model_n": (ctypes.c_int64, [ctypes.c_void_p]),
     "mfgp_model_nl": (ctypes.c_int64, [ctypes.c_void_p]),
     "mfgp_model_m": (ctypes.c_int64, [ctypes.c_void_p]),
@@ -221,6 +224,32 @@ def context(device=None):
     return ctxs[dev]
 
 
+class _ViewLease:
+    """One buffer handed over by mfgp_predict_view; returned to the pool when the
+    last array over it is gone."""
+
+    __slots__ = ("view",)
+
+    def __init__(self, view):
+        self.view = view
+
+    def __del__(self):
+        if _lib is not None and self.view:
+            _lib.mfgp_release_view(ctypes.c_void_p(self.view))
+            self.view = None
+
+
+class _HostView:
+    """[n] float64 at a host address, for np.asarray (which keeps this object, and
+    so the lease, as the array's base)."""
+
+    __slots__ = ("__array_interface__", "lease")
+
+    def __init__(self, addr, n, lease):
+        self.__array_interface__ = {"shape": (int(n),), "typestr": "<f8", "data": (int(addr), False), "version": 3}
+        self.lease = lease
+
+
 class Model:
     """Owning handle of one device-resident GP (mfgp_model)."""
 
@@ -273,6 +302,18 @@ class Model:
         var = np.empty(M, dtype=np.float64)
         check(lib().mfgp_predict(self.handle, ptr(mu) if M else None, ptr(var) if M else None))
         return mu, var
+
+    def predict_view(self):
+        """predict() without the host copy: (mu, var) are writable arrays over the
+        model's pinned result buffer, handed over to them (mfgp_predict_view); the
+        buffer goes back to the library's pool when both arrays are gone."""
+        mu_p, var_p, view = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().mfgp_predict_view(self.handle, ctypes.byref(mu_p), ctypes.byref(var_p), ctypes.byref(view)))
+        M = lib().mfgp_model_m(self.handle)
+        if not view.value:
+            return np.empty(M, dtype=np.float64), np.empty(M, dtype=np.float64)
+        lease = _ViewLease(view.value)
+        return np.asarray(_HostView(mu_p.value, M, lease)), np.asarray(_HostView(var_p.value, M, lease))
 
     def factor(self):
         n = lib().mfgp_model_n(self.handle)

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -896,8 +897,20 @@ bool is_device_ptr(const void* p);
 // The model's mapped pinned result buffer [2][M] (spec_out): host-bound predict
 // outputs are written there by the kernels over the bus and kept, so that the
 // predicts of an unchanged model return them (the same bits, no launch).
+// Result buffers handed over by mfgp_predict_view come back here (process-wide:
+// a view may outlive its model and context); ensure_spec_out takes one of at least
+// the size it needs before it allocates. Bounded: beyond VIEW_POOL_MAX the
+// returned buffer is freed.
+struct ViewBuf {
+  double* host;
+  int64_t cap;   // doubles per half ([2][cap])
+};
+std::mutex g_view_mu;
+std::vector<ViewBuf> g_view_pool;
+constexpr size_t VIEW_POOL_MAX = 8;
+
 int ensure_spec_out(mfgp_model* m) {
-  if (m->spec_cap >= m->M) return MFGP_OK;
+  if (m->spec_out && m->spec_cap >= m->M) return MFGP_OK;
   mfgp_ctx* c = m->ctx;
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (m->spec_out) HIP_TRY(hipHostFree(m->spec_out));
@@ -905,6 +918,23 @@ int ensure_spec_out(mfgp_model* m) {
   m->spec_out_dev = nullptr;
   m->spec_cap = 0;
   m->spec_valid = false;
+  {
+    std::lock_guard<std::mutex> g(g_view_mu);
+    for (size_t i = 0; i < g_view_pool.size(); ++i)
+      if (g_view_pool[i].cap >= m->M) {
+        // (the pool's buffers are laid out [2][cap]: mu at 0, var at cap)
+        m->spec_out = g_view_pool[i].host;
+        m->spec_cap = g_view_pool[i].cap;
+        g_view_pool.erase(g_view_pool.begin() + (long)i);
+        break;
+      }
+  }
+  if (m->spec_out) {
+    void* dev = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dev, m->spec_out, 0));
+    m->spec_out_dev = static_cast<double*>(dev);
+    return MFGP_OK;
+  }
   HIP_TRY(hipHostMalloc(&m->spec_out, sizeof(double) * 2 * (size_t)m->M, hipHostMallocMapped));
   void* dev = nullptr;
   HIP_TRY(hipHostGetDevicePointer(&dev, m->spec_out, 0));
@@ -925,14 +955,14 @@ int model_out(mfgp_model* m, double* mu, double* var, double*& kmu, double*& kva
   int rc = ensure_spec_out(m);
   if (rc) return rc;
   kmu = m->spec_out_dev;
-  kvar = m->spec_out_dev + m->M;
+  kvar = m->spec_out_dev + m->spec_cap;
   return MFGP_OK;
 }
 
 void model_out_done(mfgp_model* m, double* mu, double* var, bool host) {
   if (!host) return;
-  std::memcpy(mu, m->spec_out, sizeof(double) * m->M);
-  std::memcpy(var, m->spec_out + m->M, sizeof(double) * m->M);
+  if (mu != m->spec_out) std::memcpy(mu, m->spec_out, sizeof(double) * m->M);
+  if (var != m->spec_out + m->spec_cap) std::memcpy(var, m->spec_out + m->spec_cap, sizeof(double) * m->M);
   m->spec_valid = true;
 }
 
@@ -1629,13 +1659,51 @@ int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t
   mfgp_ctx* c = m->ctx;
   int rc = ensure_spec_out(m);
   if (rc) return rc;
-  rc = batch_run(&m, 1, X, y, &k, m->spec_out_dev, m->spec_out_dev + m->M, nullptr, nullptr, MFGP_ASYNC, true, true);
+  rc = batch_run(&m, 1, X, y, &k, m->spec_out_dev, m->spec_out_dev + m->spec_cap, nullptr, nullptr, MFGP_ASYNC, true, true);
   if (rc == MFGP_OK) rc = mfgp_ctx_synchronize(c);
   if (rc != MFGP_OK) {
     m->factored = false;   // a failed step leaves no usable factor
     return rc;
   }
   m->spec_valid = true;
+  return MFGP_OK;
+}
+
+int mfgp_predict_view(mfgp_model* m, double** mu, double** var, void** view) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (!mu || !var || !view) return set_err(MFGP_ERR_ARG, "null output");
+  *mu = *var = nullptr;
+  *view = nullptr;
+  if (m->M == 0) return mfgp_predict(m, nullptr, nullptr);
+  if ((rc = ensure_spec_out(m))) return rc;
+  // the predict's host outputs are the result buffer itself: no copy
+  if ((rc = mfgp_predict(m, m->spec_out, m->spec_out + m->spec_cap))) return rc;
+  ViewBuf* v = new ViewBuf{m->spec_out, m->spec_cap};
+  *mu = m->spec_out;
+  *var = m->spec_out + m->spec_cap;
+  *view = v;
+  // the buffer is the caller's now: the model's next host-bound predict takes another
+  m->spec_out = nullptr;
+  m->spec_out_dev = nullptr;
+  m->spec_cap = 0;
+  m->spec_valid = false;
+  return MFGP_OK;
+}
+
+int mfgp_release_view(void* view) {
+  if (!view) return MFGP_OK;
+  ViewBuf* v = static_cast<ViewBuf*>(view);
+  bool keep = false;
+  {
+    std::lock_guard<std::mutex> g(g_view_mu);
+    if (g_view_pool.size() < VIEW_POOL_MAX) {
+      g_view_pool.push_back(*v);
+      keep = true;
+    }
+  }
+  if (!keep) (void)hipHostFree(v->host);
+  delete v;
   return MFGP_OK;
 }
 
@@ -1649,11 +1717,11 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var) {
     const size_t b = sizeof(double) * (size_t)m->M;
     if (is_device_ptr(mu) && is_device_ptr(var)) {
       HIP_TRY(hipMemcpyAsync(mu, m->spec_out_dev, b, hipMemcpyDeviceToDevice, c->stream));
-      HIP_TRY(hipMemcpyAsync(var, m->spec_out_dev + m->M, b, hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(var, m->spec_out_dev + m->spec_cap, b, hipMemcpyDeviceToDevice, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
     } else {
-      std::memcpy(mu, m->spec_out, b);
-      std::memcpy(var, m->spec_out + m->M, b);
+      if (mu != m->spec_out) std::memcpy(mu, m->spec_out, b);
+      if (var != m->spec_out + m->spec_cap) std::memcpy(var, m->spec_out + m->spec_cap, b);
     }
     return MFGP_OK;
   }

@@ -161,7 +161,8 @@ class _DeviceGP:
         self._sync_data()
         self._push_hyp()
         self._grid_to_device(X_star)
-        mu, var = self._dev().predict()
+        # (the arrays are the model's pinned result buffer, handed over: no copy)
+        mu, var = self._dev().predict_view()
         return mu.reshape(-1, 1), DiagCov(var)
 
     @property

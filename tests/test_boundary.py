@@ -123,3 +123,38 @@ def test_diagcov_semantics():
     assert float(2.0 * one[0, 0]) == 0.5
     np.testing.assert_array_equal(np.asarray(one), [[0.25]])
     assert (np.array([[1.0]]) + 2.0 * one)[0, 0] == 1.5
+
+
+@pytest.mark.gpu
+def test_predict_arrays_are_the_callers(lib):
+    """predict() returns the model's pinned result buffer itself (mfgp_predict_view,
+    no host copy). Each call's arrays are the caller's: a later predict, append or
+    in-place edit of one call's arrays changes no other call's; dropped arrays
+    return their buffer to the pool and a model keeps working across many calls."""
+    import gc
+    from mfgp_coverage_amd.gaussian_process import MFGP
+    from mfgp_coverage_amd.synthetic import HYP, grid
+    hyp = HYP["australia8_mf"]
+    xs = grid(48)
+    rng = np.random.default_rng(5)
+    X = xs[rng.choice(xs.shape[0], 200, replace=False)]
+    y = rng.standard_normal((200, 1))
+    m = MFGP(X[:80], y[:80], X[80:150], y[80:150], 1, 1)
+    m.hyp = hyp.copy()
+    m.updt_info(m.X_L, m.y_L, m.X_H, m.y_H)
+    mu0, cov0 = m.predict(xs)
+    keep_mu, keep_var = mu0.copy(), np.diag(cov0).copy()
+    assert mu0.flags.writeable and mu0.dtype == np.float64 and mu0.shape == (xs.shape[0], 1)
+    mu1, cov1 = m.predict(xs)   # an unchanged model: the same bits, another buffer
+    np.testing.assert_array_equal(mu1, mu0)
+    np.testing.assert_array_equal(np.diag(cov1), np.diag(cov0))
+    mu1[:] = -1.0               # the caller's own array
+    mu2, _ = m.predict(xs)
+    np.testing.assert_array_equal(mu2, keep_mu)
+    for s in range(12):         # the drop-in step, arrays dropped as the simulator does
+        m.updt_hifi(X[150 + 4 * s:154 + 4 * s], y[150 + 4 * s:154 + 4 * s])
+        mu, cov = m.predict(xs)
+        del mu, cov
+        gc.collect()
+    np.testing.assert_array_equal(mu0, keep_mu.reshape(-1, 1))   # untouched by later steps
+    np.testing.assert_array_equal(np.diag(cov0), keep_var)
