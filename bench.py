@@ -12,13 +12,14 @@ all-gathered over RCCL for the loss/variance aggregation of runner.py:144-147.
 
 Two update paths are timed back to back on the same workload, with identical
 results (tests/test_gpu_incremental.py, tests/test_gpu_lattice*.py):
-  value          -- the library's default path: ONE launch per step. On the
-                    headline's lattice grid that is the lattice-separable step
-                    (k_inc_lat_arg): bordered-Cholesky
-                    append, w = K11^-1 K12 from the resident L^-1, the separable
-                    SE kernel turns L21 V_old into a K = 2 ny GEMM, and mean /
-                    variance are updated from the resident posterior; elsewhere
-                    the one-pass V stream (k_inc_stream);
+  value          -- the library's default path. On the headline's lattice grid
+                    that is the lattice-separable step,
+                    two launches per step at B = 8 (k_inc_lat_arg: bordered-
+                    Cholesky append, w = K11^-1 K12 from the resident L^-1 and the
+                    Z sums; k_lat_gemm2_arg: the separable SE kernel turns L21 V_old
+                    into a K = 2 ny GEMM, and mean / variance are updated from the
+                    resident posterior); elsewhere the one-pass V stream
+                    (k_inc_stream, one launch);
   full_recompute -- what the reference does per update: full refactor
                     (k_assemble/potrf/panel/syrk) and V recomputed from scratch
                     (k_predict).
@@ -105,6 +106,12 @@ def parse():
     p.add_argument("--warmup", type=int, default=None)
     p.add_argument("--full-steps", type=int, default=None, help="timed steps of the full-recompute run")
     p.add_argument("--seeds-per-gpu", type=int, default=None)
+    p.add_argument("--seeds", type=int, default=None,
+                   help="total seeds over all ranks (default gpus x seeds-per-gpu); need not divide evenly")
+    p.add_argument("--warm-ms", type=float, default=300.0,
+                   help="after the warm-up steps, keep stepping (untimed) until this much wall time has passed")
+    p.add_argument("--sim-iterations", type=int, default=None,
+                   help="iterations of the lockstep Todescato simulation leg (0: skip)")
     p.add_argument("--grid", type=int, default=None)
     p.add_argument("--nl", type=int, default=None)
     p.add_argument("--nh", type=int, default=None)
@@ -118,9 +125,9 @@ def parse():
                    help="allow a diagnostic library (MFGP_LIB); its line is marked and is not a headline number")
     a = p.parse_args()
     pre = {"headline": dict(steps=200, warmup=20, full_steps=None, seeds_per_gpu=8, grid=128, nl=1024, nh=1024,
-                            hyp="australia8_mf", dtype="f64"),
+                            hyp="australia8_mf", dtype="f64", sim_iterations=40),
            "configs4": dict(steps=20, warmup=3, full_steps=2, seeds_per_gpu=32, grid=256, nl=4096, nh=4096,
-                            hyp="australia9_mf", dtype="f32")}[a.workload]
+                            hyp="australia9_mf", dtype="f32", sim_iterations=0)}[a.workload]
     for key, v in pre.items():
         if getattr(a, key) is None:
             setattr(a, key, v)
@@ -287,6 +294,62 @@ def cpu_faithful(wl, hyp, XH, yH, reps=3):
                       f"dense psi@beta), median of {reps} updates at the full config"}
 
 
+def simulation_leg(a, world, rank, my_seeds, wls, hyp, dev, backend):
+    """The planners on top of the GP step: this rank's seeds
+    run the reference's Todescato loop (simulator.py:788-954) in lockstep
+    (coverage.run_lockstep: one batched append + predict and one batched cell
+    reduction per iteration, host Voronoi per seed), from the lofi prior of the
+    headline workload (1024 points, shared by all seeds as runner.py:131-132 shares
+    its prior), 8 agents, the headline grid. Timed with a barrier and device
+    synchronisation on both sides, max over ranks; beside it one seed through the
+    drop-in API (coverage.simulate, the reference's one-simulation-per-process
+    model) for a few iterations."""
+    import torch
+    import torch.distributed as dist
+    from mfgp_coverage_amd import coverage, synthetic
+    T = a.sim_iterations
+    w0 = wls[0]
+    truth = np.column_stack([w0.xs, synthetic.field(w0.xs, np.random.default_rng(1234).random((4, 2)))])
+    prior = np.column_stack([w0.XL, w0.yL])
+    stats = coverage.LockstepStats()
+    # one untimed iteration first (first-use kernel loads of the cell reduction)
+    coverage.run_lockstep("todescato", my_seeds[:1], 1, a.agents, truth, 0.1, prior, hyp, log=False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    logs = coverage.run_lockstep("todescato", my_seeds, T, a.agents, truth, 0.1, prior, hyp, stats=stats)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    Td = min(T, 8)
+    t1 = time.perf_counter()
+    coverage.simulate("todescato", my_seeds[0], Td, a.agents, truth, 0.1, prior, hyp)
+    el1 = time.perf_counter() - t1
+    tt = torch.tensor([el, el1], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el, el1 = float(tt[0].item()), float(tt[1].item())
+    total = a.seeds if a.seeds is not None else world * a.seeds_per_gpu
+    it = max(1, stats.iterations)
+    return {
+        "metric": "coverage-simulation iterations/s (Todescato planner, seeds in lockstep)",
+        "value": total * T / el, "unit": "seed-iterations/s", "per_gpu": len(my_seeds) * T / el,
+        "seeds_per_gpu": len(my_seeds), "iterations": T, "agents": a.agents,
+        "ms_per_iteration": el / T * 1e3,
+        "breakdown_ms_per_iteration": {"gp_step_enqueue": 1e3 * stats.gp / it, "voronoi_host": 1e3 * stats.voronoi / it,
+                                       "cell_reduce_and_wait": 1e3 * stats.cells / it,
+                                       "samples_logs_decisions": 1e3 * stats.host / it},
+        "hifi_rows_appended": stats.rows, "seed_steps_without_samples": stats.post_copy,
+        "log_rows": [sum(len(x[j]) for x in logs) for j in range(3)],
+        "workload": f"{a.grid}x{a.grid} grid, australia8_mf, prior = {prior.shape[0]} lofi points, "
+                    f"{a.agents} agents, sigma_n = 0.1, synthetic truth field",
+        "dropin_one_seed": {"value": Td / el1, "unit": "seed-iterations/s", "iterations": Td,
+                            "note": "one seed through SFGP/MFGP + geometry (the reference's process model)"},
+    }
+
+
 def main():
     a = parse()
     plan, arg = launch_plan(a.gpus, os.environ)
@@ -328,7 +391,11 @@ def main():
 
     f32 = a.dtype == "f32"
     dtype = _lib.F32 if f32 else _lib.F64
-    B, G, NL, NH, k = a.seeds_per_gpu, a.grid, a.nl, a.nh, a.agents
+    total_seeds = a.seeds if a.seeds is not None else world * a.seeds_per_gpu
+    if total_seeds < world:
+        sys.exit(f"bench.py: --seeds {total_seeds} leaves a rank without seeds ({world} ranks)")
+    my_seeds = shard_seeds(total_seeds, world, rank)   # contiguous, sizes differ by at most one
+    B, G, NL, NH, k = len(my_seeds), a.grid, a.nl, a.nh, a.agents
     NH0 = NH - k
     W, K = a.warmup, a.steps
     KF = min(a.full_steps, K)
@@ -336,7 +403,7 @@ def main():
     hyp = synthetic.HYP[a.hyp]
     M = G * G
     N = NL + NH
-    wls = [synthetic.Workload(G, NL, NH0, k, total, seed=seed) for seed in shard_seeds(world * B, world, rank)]
+    wls = [synthetic.Workload(G, NL, NH0, k, total, seed=seed) for seed in my_seeds]
     Xnew = torch.from_numpy(np.ascontiguousarray(np.stack([w.Xnew for w in wls], 1).reshape(total, B * k, 2))).to(dev)
     ynew = torch.from_numpy(np.ascontiguousarray(np.stack([w.ynew for w in wls], 1).reshape(total, B * k))).to(dev)
     mu = torch.empty(B * M, dtype=torch.float64, device=dev)
@@ -382,6 +449,7 @@ def main():
         # axis tables, timed as factor work (reported with full_recompute: every
         # refactor of a lattice-eligible model pays it once)
         lat_build_ms = None
+        tw0 = time.perf_counter()
         for s in range(W):
             if s == 0 and incremental:
                 ctx.enable_timing(True)
@@ -392,6 +460,17 @@ def main():
                 ctx.synchronize()
                 lat_build_ms = ctx.timing()["factor_ms"]
                 ctx.enable_timing(False)
+        # a short run (the driver's --steps 20 is ~2 ms of GPU work) would otherwise
+        # time the clock ramp: keep stepping, untimed, on the warm-up inputs (every
+        # step truncates back to the same rows, so any input is a valid step) until
+        # warm_ms of wall time has passed
+        extra = 0
+        ctx.synchronize()
+        while W > 1 and (time.perf_counter() - tw0) * 1e3 < a.warm_ms:
+            for _ in range(16):
+                step(1 + extra % (W - 1))
+                extra += 1
+            ctx.synchronize()
         aggregate(varmax[:W].transpose(0, 1).contiguous())   # first-use kernel loads / communicator setup
         ctx.synchronize()
         # the timed region: exactly K steps, nothing else on the stream (no HIP events)
@@ -445,12 +524,13 @@ def main():
         st = models[0].stats()
         del models
         return {"elapsed": float(el[0].item()), "gather_ms": 1e3 * float(el[1].item()), "tm": tm,
-                "lat_build_ms": lat_build_ms,
+                "lat_build_ms": lat_build_ms, "extra_warmup_steps": extra,
                 "host_ms": 1e3 * float(np.mean(host_t)), "stats": st, "traj": traj.cpu().numpy(), "R": R,
                 "breakdown": {"predict": tb["predict_ms"] / nb_steps, "factor": tb["factor_ms"] / nb_steps}}
 
     inc = run(True, W, K)
     full = None if a.no_full else run(False, W, KF)
+    sim = simulation_leg(a, world, rank, my_seeds, wls, hyp, dev, backend) if a.sim_iterations else None
     if os.environ.get("MFGP_BENCH_DUMP") and rank == 0:
         np.savez(os.environ["MFGP_BENCH_DUMP"], inc=inc["traj"], full=full["traj"] if full else inc["traj"])
     if full is not None and rank == 0 and not diag_lib:
@@ -488,7 +568,7 @@ def main():
         lat_flops = B * (16 * n0 * n0 + 2 * ka * G * n_t + 2 * ka * M * parts * ny8)
         lat_gbs = lat_bytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
         lat_tf = lat_flops / (v_ms * 1e-3) / 1e12 if v_ms > 0 else float("nan")
-        value = world * B * K / elapsed
+        value = total_seeds * K / elapsed
         # SURVEY.md section 8d's algorithmic cost of one update as the reference
         # computes it (refactor + V from scratch): F = N^3/3 + M N^2 + 2 N^2 + 4 M N flop,
         # B_8d = 8 (4M + 3N + 2 N^2) bytes. The incremental path does not do that work
@@ -578,7 +658,7 @@ def main():
                                "reductions in fp64" if f32 else "fp64"),
                 "update": update + "; full_recompute below is the reference's per-update work",
                 "seeds_per_gpu": B, "grid": G, "N_train": N, "N_lofi": NL, "N_hifi": NH, "agents": k,
-                "global_seeds": world * B, "parallelism": f"seed-sharded x{world}, 1 RCCL all_gather",
+                "global_seeds": total_seeds, "parallelism": f"seed-sharded x{world}, 1 RCCL all_gather",
             },
             "roofline": roof,
             "algorithmic_8d": {
@@ -591,6 +671,7 @@ def main():
                         "peak by construction; the roofline above is the kernel's own work",
             },
             "host_enqueue_ms_per_step": inc["host_ms"],
+            "extra_warmup_steps": inc["extra_warmup_steps"],
             "gather_ms": inc["gather_ms"],
             "breakdown_ms_per_step": inc["breakdown"],
         }
@@ -601,7 +682,7 @@ def main():
             achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else float("nan")
             ftraffic, _ = pmc_traffic("k_predict") if default_cfg else (None, None)
             out["full_recompute"] = {
-                "value": world * B * KF / full["elapsed"],
+                "value": total_seeds * KF / full["elapsed"],
                 "steps": KF,
                 "ms_per_step": full["elapsed"] / KF * 1e3,
                 "roofline": {
@@ -615,6 +696,8 @@ def main():
                 "breakdown_ms_per_step": dict(full["breakdown"], **({"lattice_entry": inc["lat_build_ms"]}
                                                               if inc.get("lat_build_ms") else {})),
             }
+        if sim is not None:
+            out["simulation"] = sim
         if world == 1 and not a.no_cpu_baseline:
             if M * N > 16384 * 2048:
                 out["cpu_baseline"] = cpu_baseline_sampled(wls[0], hyp, W, NL, NH0, k)

@@ -158,7 +158,8 @@ int64_t mfgp_model_m(const mfgp_model* m);
  * training rows of the last lattice step (read back from the device; synchronises
  * the context's stream; only when n > 9), lattice steps launched with their
  * descriptors as the kernel argument, lattice steps whose GEMM and cells ran as a
- * second launch (k_lat_gemm2)}. */
+ * second launch (k_lat_gemm2), batch predicts served from the resident posterior
+ * because the model appended nothing (k_post_copy)}; n <= 13. */
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n);
 /* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
 int mfgp_get_factor(mfgp_model* m, double* L_out);
@@ -169,6 +170,11 @@ int mfgp_get_factor(mfgp_model* m, double* L_out);
  * order). One set of launches serves the whole batch. flags: MFGP_ASYNC. */
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y,
                               const int64_t* k, double* mu, double* var, int flags);
+/* A member with k[i] = 0 whose factor and resident posterior are current (it
+ * was predicted before and nothing changed) is not recomputed: its outputs are its
+ * resident posterior (the same bits as its last predict), copied by one launch for
+ * all such members (device outputs; mfgp_model_stats counts them), and the step
+ * runs over the others. */
 /* mfgp_batch_append_predict plus fused reductions of each model's variance:
  * var_max[i] = np.amax of the posterior covariance (its largest diagonal entry,
  * simulator.py:672, 842, 1014) and var_argmax[i] = the first cell attaining it
@@ -219,6 +225,19 @@ int mfgp_nlml(mfgp_model* m, const double* hyp, int nhyp, double* nlml, double* 
 int mfgp_cell_reduce(mfgp_ctx* ctx, const double* grid, int64_t M, int ncells, const int* vstart,
                      const double* verts, const double* seeds, const double* w, const double* f,
                      const double* var, double* out, int64_t* argmax);
+
+/* mfgp_cell_reduce over the partitions of several seeds in one launch (the
+ * lockstep simulations of a seed batch, mfgp_coverage_amd/coverage.py: every
+ * seed's loss partition of its agents and Lloyd partition of its centroids,
+ * simulator.py:895-904). Cell i reads the fields of seed field[i]: w + field[i]*M
+ * and var + field[i]*M (w and var are [nfield][M], e.g. the batch's posterior
+ * means / variances as mfgp_batch_append_predict wrote them); f [M] is shared.
+ * field and vstart are host memory. Same per-cell outputs as mfgp_cell_reduce
+ * (bit for bit: a cell's reduction does not depend on the other cells).
+ * Synchronous. */
+int mfgp_batch_cell_reduce(mfgp_ctx* ctx, const double* grid, int64_t M, int ncells, const int* vstart,
+                           const double* verts, const double* seeds, const int* field, int nfield,
+                           const double* w, const double* f, const double* var, double* out, int64_t* argmax);
 
 const char* mfgp_last_error(void);
 const char* mfgp_version(void);

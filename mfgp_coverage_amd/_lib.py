@@ -43,6 +43,10 @@ SIGNATURES = {
     "mfgp_cell_reduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mfgp_batch_cell_reduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
     "mfgp_sample_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p,
                                           _c_int64_p]),
     "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -335,11 +339,13 @@ class Model:
         device counters hold them (MF: summed over both kernel parts); {lattice_arg}:
         the lattice steps launched with their descriptors by value (k_inc_lat_arg);
         {lattice_g2}: the lattice steps whose GEMM and cells ran as a second launch
-        (k_lat_gemm2)."""
-        out = (ctypes.c_int64 * 12)()
-        check(lib().mfgp_model_stats(self.handle, out, 12))
+        (k_lat_gemm2); {post_copy}: batch predicts served from the resident posterior
+        because the model appended nothing (k_post_copy)."""
+        out = (ctypes.c_int64 * 13)()
+        check(lib().mfgp_model_stats(self.handle, out, 13))
         keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream",
-                "lattice_nx", "lattice_ny", "lattice", "lattice_virtual", "lattice_arg", "lattice_g2")
+                "lattice_nx", "lattice_ny", "lattice", "lattice_virtual", "lattice_arg", "lattice_g2",
+                "post_copy")
         return dict(zip(keys, (int(v) for v in out)))
 
     def sample_points(self, threshold, max_points):
@@ -438,4 +444,44 @@ def cell_reduce(grid, verts, vstart, seeds, w=None, f=None, var=None, ctx=None):
     check(lib().mfgp_cell_reduce(ctx.handle, ptr(g), g.shape[0], n, ctypes.c_void_p(vs.ctypes.data), ptr(v), ptr(sd),
                                  *[ptr(a) for a in arrs], ctypes.c_void_p(out.ctypes.data),
                                  ctypes.c_void_p(am.ctypes.data)))
+    return out[:n], am[:n]
+
+
+def batch_cell_reduce(grid, verts, vstart, seeds, field, nfield, w=None, f=None, var=None, ctx=None, M=None):
+    """mfgp_batch_cell_reduce -> (out [n, 6], argmax [n]). verts / seeds / vstart /
+    field are host arrays; grid a host array [M, 2] or (with M) the integer device
+    address of one; w and var host arrays [nfield, M] or integer device addresses
+    of [nfield * M] float64 (a batch's predict outputs); f a host array [M] or a
+    device address."""
+    ctx = ctx or context()
+    keep = []
+
+    def arg(a):
+        if a is None:
+            return None
+        if isinstance(a, int):
+            return ctypes.c_void_p(a)
+        a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1)
+        keep.append(a)
+        return ptr(a)
+    if isinstance(grid, int):
+        if M is None:
+            raise ValueError("a device grid needs M")
+        g_arg, Mg = ctypes.c_void_p(grid), int(M)
+    else:
+        g = np.ascontiguousarray(grid, dtype=np.float64).reshape(-1, 2)
+        g_arg, Mg = ptr(g), g.shape[0]
+        keep.append(g)
+    v = np.ascontiguousarray(verts, dtype=np.float64).reshape(-1, 2)
+    vs = np.ascontiguousarray(vstart, dtype=np.int32).reshape(-1)
+    fd = np.ascontiguousarray(field, dtype=np.int32).reshape(-1)
+    sd = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 2)
+    n = vs.shape[0] - 1
+    if fd.shape[0] != n:
+        raise ValueError("field needs one entry per cell")
+    out = np.empty((max(n, 1), 6), dtype=np.float64)
+    am = np.empty(max(n, 1), dtype=np.int64)
+    check(lib().mfgp_batch_cell_reduce(ctx.handle, g_arg, Mg, n, ctypes.c_void_p(vs.ctypes.data), ptr(v),
+                                       ptr(sd), ctypes.c_void_p(fd.ctypes.data), int(nfield), arg(w), arg(f), arg(var),
+                                       ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(am.ctypes.data)))
     return out[:n], am[:n]

@@ -171,6 +171,7 @@ struct mfgp_model {
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0, n_lattice = 0;
   int64_t n_lattice_arg = 0;   // lattice steps launched with their descriptors by value (k_inc_lat_arg)
   int64_t n_lattice_g2 = 0;    // lattice steps whose GEMM and cells ran as a second launch (k_lat_gemm2)
+  int64_t n_post_copy = 0;     // batch predicts served from the resident posterior (k_post_copy: nothing appended)
   // state generation: a new factor from scratch, a new grid or new hyperparameters
   // start a new one (the resident posterior, F and the tables belong to one)
   uint64_t gen = 1;
@@ -310,10 +311,10 @@ int ensure_h_status(mfgp_ctx* c, size_t n) {
 int ensure_ws(mfgp_ctx* c, size_t bytes) {
   if (bytes <= c->ws_bytes) return MFGP_OK;
   HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t want = std::max(bytes, c->ws_bytes + c->ws_bytes / 2);
   if (c->ws) HIP_TRY(hipFree(c->ws));
   c->ws = nullptr;
   c->ws_bytes = 0;
-  size_t want = std::max(bytes, c->ws_bytes + c->ws_bytes / 2);
   HIP_TRY(hipMalloc(&c->ws, want));
   c->ws_bytes = want;
   return MFGP_OK;
@@ -908,6 +909,8 @@ struct ViewBuf {
 std::mutex g_view_mu;
 std::vector<ViewBuf> g_view_pool;
 constexpr size_t VIEW_POOL_MAX = 8;
+// bytes of T scratch the recursive-doubling F build may hold in the workspace
+constexpr int64_t TRINV_WS_MAX = int64_t(2) << 30;
 
 int ensure_spec_out(mfgp_model* m) {
   if (m->spec_out && m->spec_cap >= m->M) return MFGP_OK;
@@ -919,23 +922,29 @@ int ensure_spec_out(mfgp_model* m) {
   m->spec_cap = 0;
   m->spec_valid = false;
   {
+    // best fit: the smallest pooled buffer that holds M (a small model does not take
+    // the large buffer another model just returned)
     std::lock_guard<std::mutex> g(g_view_mu);
+    size_t best = g_view_pool.size();
     for (size_t i = 0; i < g_view_pool.size(); ++i)
-      if (g_view_pool[i].cap >= m->M) {
-        // (the pool's buffers are laid out [2][cap]: mu at 0, var at cap)
-        m->spec_out = g_view_pool[i].host;
-        m->spec_cap = g_view_pool[i].cap;
-        g_view_pool.erase(g_view_pool.begin() + (long)i);
-        break;
-      }
+      if (g_view_pool[i].cap >= m->M && (best == g_view_pool.size() || g_view_pool[i].cap < g_view_pool[best].cap))
+        best = i;
+    if (best < g_view_pool.size()) {
+      // (the pool's buffers are laid out [2][cap]: mu at 0, var at cap)
+      m->spec_out = g_view_pool[best].host;
+      m->spec_cap = g_view_pool[best].cap;
+      g_view_pool.erase(g_view_pool.begin() + (long)best);
+    }
   }
+  HIP_TRY(hipSetDevice(c->device));   // the mapping below is the model's device's
   if (m->spec_out) {
     void* dev = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dev, m->spec_out, 0));
     m->spec_out_dev = static_cast<double*>(dev);
     return MFGP_OK;
   }
-  HIP_TRY(hipHostMalloc(&m->spec_out, sizeof(double) * 2 * (size_t)m->M, hipHostMallocMapped));
+  // portable: a pooled buffer may serve a model of a context on another device
+  HIP_TRY(hipHostMalloc(&m->spec_out, sizeof(double) * 2 * (size_t)m->M, hipHostMallocMapped | hipHostMallocPortable));
   void* dev = nullptr;
   HIP_TRY(hipHostGetDevicePointer(&dev, m->spec_out, 0));
   m->spec_out_dev = static_cast<double*>(dev);
@@ -1010,12 +1019,22 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
     // the block-column form (diagnostics)
     const int64_t tstride = trinv_scratch(max_nbr);
     double* tscr = nullptr;
+    // the scratch is bounded (TRINV_WS_MAX, and half the free HBM): a batch that needs
+    // more runs in GP chunks (configs[4]: 32 GPs x 128 MiB at N = 8192 -> chunks of 8)
+    int chunk = count;
     if (!c->trinv_columns) {
-      int rc = ensure_ws(c, sizeof(double) * (size_t)(tstride * count));
+      size_t free_b = 0, total_b = 0;
+      int64_t budget = TRINV_WS_MAX;
+      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+        budget = std::min<int64_t>(budget, (int64_t)((free_b + c->ws_bytes) / 2));
+      const int64_t per_gp = (int64_t)sizeof(double) * tstride;
+      chunk = (int)std::max<int64_t>(1, std::min<int64_t>(count, budget / std::max<int64_t>(per_gp, 1)));
+      int rc = ensure_ws(c, sizeof(double) * (size_t)(tstride * chunk));
       if (rc) return rc;
       tscr = c->ws;
     }
-    HIP_TRY(launch_trinv_f(dd, count, max_nbr, tscr, tstride, c->stream));
+    for (int i0 = 0; i0 < count; i0 += chunk)
+      HIP_TRY(launch_trinv_f(dd + i0, std::min(chunk, count - i0), max_nbr, tscr, tstride, c->stream));
   }
   if (max_rows > 0) HIP_TRY(launch_lat_tables(dd, count, max_rows, c->stream));
   if (max_axw > 0) HIP_TRY(launch_lat_axes(dd, count, max_axw, c->stream));
@@ -1650,7 +1669,7 @@ int mfgp_batch_truncate(mfgp_model** models, int count, int64_t n_keep_hifi) {
 
 static int batch_run(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                      double* mu, double* var, double* vmax, int64_t* vargmax, int flags, bool do_factor,
-                     bool do_predict);
+                     bool do_predict, const int64_t* out_offs = nullptr, const int* vidx = nullptr);
 
 // The speculative form of an eager append (mfgp_append): the bordered append and
 // the one-pass predict as one launch, synchronised (a non-PD step is reported
@@ -1781,10 +1800,10 @@ int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
     if (m->kind == MFGP_MF) HIP_TRY(hipMemcpy(&nv[1], m->zvl + m->zb_rows + 1, sizeof(int), hipMemcpyDeviceToHost));
     virt = (int64_t)nv[0] + nv[1];
   }
-  const int64_t v[12] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+  const int64_t v[13] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
                          m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice, virt,
-                         m->n_lattice_arg, m->n_lattice_g2};
-  for (int i = 0; i < n && i < 12; ++i) out[i] = v[i];
+                         m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy};
+  for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
@@ -1808,15 +1827,17 @@ int mfgp_get_factor(mfgp_model* m, double* L_out) {
 // (do_factor) and predict (do_predict) `count` models with one set of launches
 // per kind: bordered appends (k_inc_factor) and full refactors side by side,
 // then one-pass predicts over the resident V (k_vstream) and full predicts.
+// out_offs / vidx (or null): each model's offset into mu / var and index into
+// vmax / vargmax, when `models` is a subset of the caller's batch (the models left
+// after the unchanged ones took k_post_copy)
 static int batch_run(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                      double* mu, double* var, double* vmax, int64_t* vargmax, int flags, bool do_factor,
-                     bool do_predict) {
+                     bool do_predict, const int64_t* out_offs, const int* vidx) {
   if (!models || count <= 0) return set_err(MFGP_ERR_ARG, "empty batch");
   mfgp_ctx* c = models[0]->ctx;
   int rc = MFGP_OK;
   for (int i = 0; i < count; ++i) {
     if ((rc = check_model(models[i]))) return rc;
-    models[i]->spec_valid = false;
     if (models[i]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
     if (models[i]->dtype != models[0]->dtype)
       return set_err(MFGP_ERR_ARG, "batch models must share one dtype (MFGP_F64 or MFGP_F32)");
@@ -1825,6 +1846,45 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       return set_err(MFGP_ERR_ARG, "model %d has no current factor (call mfgp_batch_append_factor first)", i);
   }
   if (do_predict && (!mu || !var)) return set_err(MFGP_ERR_ARG, "null output");
+  // Members that append nothing to a current factor whose posterior is resident
+  // for its rows (the lockstep simulations: seeds whose agents all exploited this
+  // iteration, sim:872-891) are unchanged: their predict is the resident posterior,
+  // copied into the outputs with its var max / argmax (k_post_copy, one launch),
+  // and the batch step runs over the others -- so a ragged batch keeps its one
+  // fused (or lattice) launch instead of falling back to streaming V for all.
+  if (do_factor && do_predict && !out_offs && c->incremental && is_device_ptr(mu) && is_device_ptr(var)) {
+    const bool rows_given = k && X && y;
+    std::vector<PostCopy> pc;
+    std::vector<mfgp_model*> rest;
+    std::vector<int64_t> rest_k, rest_off;
+    std::vector<int> rest_vidx;
+    int64_t oo = 0;
+    for (int i = 0; i < count; ++i) {
+      mfgp_model* m = models[i];
+      const int64_t ki = rows_given ? k[i] : 0;
+      const int64_t n = m->NL + m->NH;
+      const int b = (ki == 0 && m->M > 0 && factor_current(m) && m->v_n == n) ? res_find(m, n) : -1;
+      if (b >= 0) {
+        pc.push_back({res_mu(m, b), res_var(m, b), mu + oo, var + oo, vmax ? vmax + i : nullptr,
+                      vargmax ? vargmax + i : nullptr, m->M});
+        m->n_post_copy += 1;
+      } else {
+        rest.push_back(m);
+        rest_k.push_back(ki);
+        rest_off.push_back(oo);
+        rest_vidx.push_back(i);
+      }
+      oo += m->M;
+    }
+    if (!pc.empty()) {
+      HIP_TRY(launch_post_copy(pc.data(), (int)pc.size(), c->stream));
+      if (rest.empty()) return (flags & MFGP_ASYNC) ? MFGP_OK : mfgp_ctx_synchronize(c);
+      // (the rows of the unchanged members are none: the others' rows stay contiguous)
+      return batch_run(rest.data(), (int)rest.size(), X, y, rest_k.data(), mu, var, vmax, vargmax, flags, do_factor,
+                       do_predict, rest_off.data(), rest_vidx.data());
+    }
+  }
+  for (int i = 0; i < count; ++i) models[i]->spec_valid = false;
   // append new rows: device-resident sources are copied by one k_append launch
   // per sub-batch (below); host sources by plain copies here
   const bool has_new = do_factor && k && X && y;
@@ -1833,7 +1893,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
   int64_t off = 0, oo = 0;
   for (int i = 0; i < count; ++i) {
     mfgp_model* m = models[i];
-    out_off[i] = oo;
+    out_off[i] = out_offs ? out_offs[i] : oo;
     oo += m->M;
     if (!do_factor) continue;
     const int64_t ki = has_new ? k[i] : 0;
@@ -1926,7 +1986,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         if (i < nv) set_vstream_rows(pd, porder[i]);
         pd.mu = mu + oo_ord[i];
         pd.var = var + oo_ord[i];
-        const int64_t mi = std::find(models + b0, models + b0 + nb, porder[i]) - models;
+        int64_t mi = std::find(models + b0, models + b0 + nb, porder[i]) - models;
+        if (vidx) mi = vidx[mi];
         if (vmax) pd.vmax = vmax + mi;
         if (vargmax) pd.vargmax = vargmax + mi;
       }
@@ -2276,13 +2337,15 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
 
 // Voronoi-cell reductions (simulator.py:194-323) on the device. Inputs may be
 // host or device memory (host ones are staged through the context workspace);
-// outputs likewise. Synchronous.
-int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, const int* vstart, const double* verts,
-                     const double* seeds, const double* w, const double* f, const double* var, double* out,
-                     int64_t* argmax) {
+// outputs likewise. Synchronous. field (host, [ncells]) or null: cell i reads
+// w / var of seed field[i] ([nfield][M] each; the lockstep simulations' batch).
+static int cell_reduce_impl(mfgp_ctx* c, const double* grid, int64_t M, int ncells, const int* vstart,
+                            const double* verts, const double* seeds, const int* field, int nfield, const double* w,
+                            const double* f, const double* var, double* out, int64_t* argmax) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   if (M < 0 || ncells < 0 || (M > 0 && !grid) || (ncells > 0 && (!vstart || !verts || !seeds || !out || !argmax)))
     return set_err(MFGP_ERR_ARG, "bad cell_reduce arguments");
+  if (field && nfield < 1) return set_err(MFGP_ERR_ARG, "nfield must be >= 1");
   if (M == 0 || ncells == 0) {
     for (int i = 0; i < ncells; ++i) {
       for (int j = 0; j < 6; ++j) out[6 * i + j] = (j == 5) ? -HUGE_VAL : 0.0;
@@ -2292,16 +2355,22 @@ int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, con
   }
   // vertex counts (the offsets must be readable on the host)
   if (is_device_ptr(vstart)) return set_err(MFGP_ERR_ARG, "vstart must be host memory");
+  if (field && is_device_ptr(field)) return set_err(MFGP_ERR_ARG, "field must be host memory");
   if (vstart[0] != 0) return set_err(MFGP_ERR_ARG, "vstart[0] must be 0");
-  for (int i = 0; i < ncells; ++i)
+  for (int i = 0; i < ncells; ++i) {
     if (vstart[i + 1] - vstart[i] > 256 || vstart[i + 1] < vstart[i])
       return set_err(MFGP_ERR_ARG, "cell %d: bad vertex count", i);
+    if (field && (field[i] < 0 || field[i] >= nfield)) return set_err(MFGP_ERR_ARG, "cell %d: field out of range", i);
+  }
+  const int64_t nf = field ? nfield : 1;
   const int64_t nv = vstart[ncells];
   const int64_t npart = cell_partial_doubles(M, ncells);
-  // workspace layout (doubles): grid 2M | w M | f M | var M | verts 2nv | seeds 2n | part | out 6n | argmax n | vstart
-  const int64_t off_g = 0, off_w = off_g + 2 * M, off_f = off_w + M, off_v = off_f + M, off_vx = off_v + M;
+  // workspace layout (doubles): grid 2M | w nf M | f M | var nf M | verts 2nv | seeds 2n | part | out 6n |
+  // argmax n | vstart | field
+  const int64_t off_g = 0, off_w = off_g + 2 * M, off_f = off_w + nf * M, off_v = off_f + M, off_vx = off_v + nf * M;
   const int64_t off_s = off_vx + 2 * nv, off_p = off_s + 2 * ncells, off_o = off_p + npart;
-  const int64_t off_a = off_o + 6 * ncells, off_i = off_a + ncells, total = off_i + (ncells + 2) / 2 + 1;
+  const int64_t off_a = off_o + 6 * ncells, off_i = off_a + ncells, off_fd = off_i + (ncells + 2) / 2 + 1;
+  const int64_t total = off_fd + (ncells + 1) / 2 + 1;
   int rc = ensure_ws(c, sizeof(double) * total);
   if (rc) return rc;
   double* ws = c->ws;
@@ -2313,25 +2382,43 @@ int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, con
     return ws + off;
   };
   const double* dg = stage(grid, 2 * M, off_g);
-  const double* dw = stage(w, M, off_w);
+  const double* dw = stage(w, nf * M, off_w);
   const double* df = stage(f, M, off_f);
-  const double* dv = stage(var, M, off_v);
+  const double* dv = stage(var, nf * M, off_v);
   const double* dx = stage(verts, 2 * nv, off_vx);
   const double* ds = stage(seeds, 2 * ncells, off_s);
   if (!dg || !dx || !ds || (w && !dw) || (f && !df) || (var && !dv))
     return set_err(MFGP_ERR_DEVICE, "cell_reduce: staging failed");
   int* dvs = reinterpret_cast<int*>(ws + off_i);
   HIP_TRY(hipMemcpyAsync(dvs, vstart, sizeof(int) * (ncells + 1), hipMemcpyHostToDevice, s));
+  int* dfd = nullptr;
+  if (field) {
+    dfd = reinterpret_cast<int*>(ws + off_fd);
+    HIP_TRY(hipMemcpyAsync(dfd, field, sizeof(int) * ncells, hipMemcpyHostToDevice, s));
+  }
   const bool dev_out = is_device_ptr(out) && is_device_ptr(argmax);
   double* o = dev_out ? out : ws + off_o;
   int64_t* a = dev_out ? argmax : reinterpret_cast<int64_t*>(ws + off_a);
-  HIP_TRY(launch_cell_reduce(dg, M, dx, dvs, ncells, ds, dw, df, dv, ws + off_p, o, a, s));
+  HIP_TRY(launch_cell_reduce(dg, M, dx, dvs, ncells, ds, dw, df, dv, dfd, ws + off_p, o, a, s));
   if (!dev_out) {
     HIP_TRY(hipMemcpyAsync(out, o, sizeof(double) * 6 * ncells, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(argmax, a, sizeof(int64_t) * ncells, hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(hipStreamSynchronize(s));
   return MFGP_OK;
+}
+
+int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, const int* vstart, const double* verts,
+                     const double* seeds, const double* w, const double* f, const double* var, double* out,
+                     int64_t* argmax) {
+  return cell_reduce_impl(c, grid, M, ncells, vstart, verts, seeds, nullptr, 1, w, f, var, out, argmax);
+}
+
+int mfgp_batch_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, const int* vstart,
+                           const double* verts, const double* seeds, const int* field, int nfield, const double* w,
+                           const double* f, const double* var, double* out, int64_t* argmax) {
+  if (!field) return set_err(MFGP_ERR_ARG, "null field");
+  return cell_reduce_impl(c, grid, M, ncells, vstart, verts, seeds, field, nfield, w, f, var, out, argmax);
 }
 
 // likelihood (gp:81-106 / gp:344-385) and its analytic gradient on the device,

@@ -13,6 +13,13 @@
 //
 // k_cell_partial: grid (point tiles, cells); one thread per point per cell.
 // k_cell_final:   one workgroup per cell sums the tile partials in tile order.
+// A batch of partitions (the lockstep simulations of coverage.py: every seed's
+// loss and Lloyd partitions, sim:895-904) is one launch: cell i reads the field
+// w / var of its own seed, w + field[i] * M (field = null: every cell reads w).
+//
+// k_post_copy: the resident posterior of an unchanged model (a batch member that
+// appended no rows) copied into the batch's outputs with its var max / first
+// argmax -- the step's predict for a model whose state did not change.
 #include <climits>
 #include <cstdint>
 #include <hip/hip_runtime.h>
@@ -63,9 +70,15 @@ __global__ __launch_bounds__(CNT) void k_cell_partial(const double* __restrict__
                                                       const int* __restrict__ vstart,
                                                       const double* __restrict__ seeds,
                                                       const double* __restrict__ w, const double* __restrict__ f,
-                                                      const double* __restrict__ var, double* __restrict__ part,
+                                                      const double* __restrict__ var,
+                                                      const int* __restrict__ field, double* __restrict__ part,
                                                       int64_t ntiles) {
   const int cell = blockIdx.y;
+  if (field) {   // this cell's seed's fields
+    const int64_t fo = (int64_t)field[cell] * M;
+    if (w) w += fo;
+    if (var) var += fo;
+  }
   const int64_t tile = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   __shared__ double vx[CMAXV], vy[CMAXV];
@@ -166,15 +179,73 @@ __global__ __launch_bounds__(64) void k_cell_final(const double* __restrict__ pa
 
 hipError_t launch_cell_reduce(const double* grid, int64_t M, const double* verts, const int* vstart, int ncells,
                               const double* seeds, const double* w, const double* f, const double* var,
-                              double* part, double* out, int64_t* argmax, hipStream_t s) {
+                              const int* field, double* part, double* out, int64_t* argmax, hipStream_t s) {
   const int64_t ntiles = (M + CNT - 1) / CNT;
   if (ntiles <= 0 || ncells <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_cell_partial, dim3((unsigned)ntiles, ncells), dim3(CNT), 0, s, grid, M, verts, vstart, seeds,
-                     w, f, var, part, ntiles);
+                     w, f, var, field, part, ntiles);
   hipLaunchKernelGGL(k_cell_final, dim3(ncells), dim3(64), 0, s, part, ntiles, out, argmax);
   return hipGetLastError();
 }
 
 int64_t cell_partial_doubles(int64_t M, int ncells) { return (int64_t)ncells * ((M + CNT - 1) / CNT) * CPART; }
+
+// One workgroup per model: 16-byte loads and stores of mu / var (M even and the
+// buffers 16-byte aligned, else one double at a time), the running (max, first
+// argmax) of var per thread, then a wave reduction and one across the 16 waves.
+constexpr int PCT = 1024;
+__global__ __launch_bounds__(PCT) void k_post_copy(PostArg a) {
+  const PostCopy& p = a.p[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t M = p.M;
+  double bv = -__builtin_inf();
+  int64_t bi = INT64_MAX;
+  const bool vec = (M % 2 == 0) && ((((uintptr_t)p.smu) | ((uintptr_t)p.svar) | ((uintptr_t)p.mu) |
+                                     ((uintptr_t)p.var)) % 16 == 0);
+  if (vec) {
+    const double2* sm = reinterpret_cast<const double2*>(p.smu);
+    const double2* sv = reinterpret_cast<const double2*>(p.svar);
+    double2* dm = reinterpret_cast<double2*>(p.mu);
+    double2* dv = reinterpret_cast<double2*>(p.var);
+    for (int64_t i = tid; i < M / 2; i += PCT) {
+      const double2 m2 = sm[i], v2 = sv[i];
+      dm[i] = m2;
+      dv[i] = v2;
+      amax_pair(bv, bi, v2.x, 2 * i);
+      amax_pair(bv, bi, v2.y, 2 * i + 1);
+    }
+  } else {
+    for (int64_t i = tid; i < M; i += PCT) {
+      const double v = p.svar[i];
+      p.mu[i] = p.smu[i];
+      p.var[i] = v;
+      amax_pair(bv, bi, v, i);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) amax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+  __shared__ double rv[PCT / 64];
+  __shared__ int64_t ri[PCT / 64];
+  if (lane == 0) {
+    rv[wv] = bv;
+    ri[wv] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int k = 1; k < PCT / 64; ++k) amax_pair(bv, bi, rv[k], ri[k]);
+    if (p.vmax) p.vmax[0] = bv;
+    if (p.vargmax) p.vargmax[0] = bi;
+  }
+}
+
+hipError_t launch_post_copy(const PostCopy* h, int count, hipStream_t s) {
+  for (int i0 = 0; i0 < count; i0 += POST_MAX) {
+    PostArg a{};
+    const int n = count - i0 < POST_MAX ? count - i0 : POST_MAX;
+    for (int i = 0; i < n; ++i) a.p[i] = h[i0 + i];
+    hipLaunchKernelGGL(k_post_copy, dim3(n), dim3(PCT), 0, s, a);
+  }
+  return hipGetLastError();
+}
 
 }  // namespace mfgp

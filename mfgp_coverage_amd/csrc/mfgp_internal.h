@@ -222,10 +222,27 @@ hipError_t launch_vstream(const GPDesc* d, int count, int64_t max_ctiles, int vf
 // MFGP_F32 full predict: round the fp64 V that k_predict wrote into d.V (rows [0, N)
 // of every tile) into the resident fp32 V (d.Vf)
 hipError_t launch_vnarrow(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);
+// field: null, or per cell the seed whose w / var it reads (w + field[cell] * M)
 hipError_t launch_cell_reduce(const double* grid, int64_t M, const double* verts, const int* vstart, int ncells,
                               const double* seeds, const double* w, const double* f, const double* var,
-                              double* part, double* out, int64_t* argmax, hipStream_t s);
+                              const int* field, double* part, double* out, int64_t* argmax, hipStream_t s);
 int64_t cell_partial_doubles(int64_t M, int ncells);
+// the resident posterior of an unchanged model into a batch's outputs (k_post_copy):
+// mu / var [M] copied from smu / svar, *vmax = max var, *vargmax = its first cell
+struct PostCopy {
+  const double* smu;
+  const double* svar;
+  double* mu;
+  double* var;
+  double* vmax;        // or null
+  int64_t* vargmax;    // or null
+  int64_t M;
+};
+constexpr int POST_MAX = 32;   // models per k_post_copy launch (descriptors by value)
+struct PostArg {
+  PostCopy p[POST_MAX];
+};
+hipError_t launch_post_copy(const PostCopy* h, int count, hipStream_t s);
 hipError_t launch_nlml_value(const GPDesc* d, int count, double* out, hipStream_t s);
 hipError_t launch_nlml_grad(const GPDesc* d, int64_t N, double* Xi, double* Kv, double* alpha, double* part,
                             hipStream_t s);

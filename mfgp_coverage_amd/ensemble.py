@@ -22,18 +22,30 @@ def shard_seeds(total_seeds: int, world: int, rank: int):
 def gather_trajectories(traj, world: int, group=None):
     """All-gather per-seed trajectories and aggregate them per iteration.
 
-    traj: tensor [seeds_on_this_rank, iterations] (same shape on every rank).
+    traj: tensor [seeds_on_this_rank, iterations]. The seed counts may differ
+    between ranks (``shard_seeds`` of 100 seeds over 8 ranks gives 13 or 12, and a
+    rank may hold none); the iteration count must be the same on every rank.
     Returns (all [total_seeds, iterations] in rank order, mean [iterations],
     std [iterations]) -- the analysis.py:66-73 statistics (pandas' std is the
     sample std, ddof = 1).
+
+    Two collectives: the per-rank seed counts, then the blocks padded to the
+    largest one (all_gather needs equal shapes).
     """
     import torch
     import torch.distributed as dist
 
     if world > 1:
-        parts = [torch.empty_like(traj) for _ in range(world)]
-        dist.all_gather(parts, traj.contiguous(), group=group)
-        allt = torch.cat(parts, 0)
+        n = torch.tensor([traj.shape[0]], dtype=torch.int64, device=traj.device)
+        counts = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(counts, n, group=group)
+        counts = [int(c.item()) for c in counts]
+        rows = max(counts)
+        pad = traj.new_zeros((rows,) + tuple(traj.shape[1:]))
+        pad[:traj.shape[0]] = traj
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        allt = torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
     else:
         allt = traj
     mean = allt.mean(0)

@@ -81,21 +81,43 @@ def _gather_blocks(block, M, world, group):
     return out
 
 
+def _model_device(model):
+    """The device of the model's context (MFGP_DEVICE / _lib.set_device), or None."""
+    dev = getattr(model, "_dev", None)
+    if dev is None:
+        return None
+    return int(dev().ctx.device)
+
+
 def predict_block_device(model, xs_blk, mmax):
     """The posterior of `model` at the cells xs_blk written straight into a device
     tensor [2, mmax] (row 0 mean, row 1 variance; columns past the block zero) by
-    the batched C ABI's device-output path: no host copy of mean / variance."""
+    the batched C ABI's device-output path: no host copy of mean / variance.
+
+    The tensor lives on the model context's device. Its zero fill runs on torch's
+    current stream and the predict on the context's own (non-blocking) stream, so
+    the fill is waited for before the predict is enqueued; the predict itself
+    returns synchronised, so the collective that follows on torch's stream reads
+    finished data."""
     import torch
 
     from . import _lib
 
-    mine = torch.zeros((2, mmax), dtype=torch.float64, device="cuda")
+    dev = torch.device("cuda", _model_device(model))
+    mine = torch.zeros((2, mmax), dtype=torch.float64, device=dev)
     if xs_blk.shape[0]:
+        torch.cuda.current_stream(dev).synchronize()
         model._sync_data()
         model._push_hyp()
         model._grid_to_device(xs_blk)
         _lib.batch_predict([model._dev()], mine[0].data_ptr(), mine[1].data_ptr())
     return mine
+
+
+def _current_cuda_device():
+    import torch
+
+    return torch.cuda.current_device() if torch.cuda.is_available() else None
 
 
 def predict_sharded(model, X_star, world=None, rank=None, group=None):
@@ -123,7 +145,8 @@ def predict_sharded(model, X_star, world=None, rank=None, group=None):
     lo, hi = bounds[rank]
     import torch.distributed as dist
 
-    if hasattr(model, "_dev") and dist.get_backend(group) == "nccl":
+    nccl = dist.get_backend(group) == "nccl"
+    if nccl and hasattr(model, "_dev") and _model_device(model) == _current_cuda_device():
         mmax = max(b - a for a, b in bounds)
         block = {"bounds": bounds, "mine": predict_block_device(model, xs[lo:hi], mmax)}
     else:

@@ -344,6 +344,83 @@ def make_nlml_fixture(gp):
     print("wrote nlml_reference.npz,", len(cases), "cases")
 
 
+SIM_CASES = {
+    # name: (algorithm, data set, fidelity (hyp file), prior file or None, agents, iterations, seeds)
+    "a6_todescato_hmf": ("todescato", "australia6", "mf", "australia6_prior.csv", 4, 14, (0, 1, 2)),
+    "a6_todescato_hsf": ("todescato", "australia6", "sf", "australia6_prior.csv", 4, 14, (0, 1)),
+    "a6_periodic_nmf": ("periodic", "australia6", "mf", None, 4, 14, (0, 1)),
+    "a6_todescato_nsf": ("todescato", "australia6", "sf", None, 3, 12, (3,)),
+}
+
+
+def make_sim_fixture(sim):
+    """7. ``sim_reference.npz``: the reference's own ``todescato`` / ``periodic``
+    (simulator.py:788-954 / 618-785) on its australia6 data (51x51 grid), with its
+    process-global generators replaced by the counter-based per-seed streams of
+    ``mfgp_coverage_amd.coverage.SeedStreams`` (``random.random`` -> the explore
+    stream, sim:943; ``np.random.default_rng()`` -> the noise stream, sim:877; the
+    start positions of run_sim, runner.py:41-43, from the start stream), so the
+    device drivers can replay the same draws. Stored per case and seed: the three
+    logs encoded as float64 columns in the reference's key order
+    (``runner.encode``), and per iteration and agent the gap between the largest
+    and the second largest posterior variance inside the agent's Lloyd cell (the
+    argmax that decides the next explore target: where the gap is below the parity
+    tolerance the choice is decided by rounding, so the tests compare a
+    trajectory only up to the first such iteration)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from mfgp_coverage_amd import runner
+    from mfgp_coverage_amd.coverage import SeedStreams
+    out = {}
+    real_cmv, real_random, real_rng = sim.compute_max_var, sim.random, sim.np.random.default_rng
+    real_arr = sim.np.array
+
+    def arr(x, *a, **k):
+        try:
+            return real_arr(x, *a, **k)
+        except ValueError:
+            return real_arr(x, dtype=object)
+    for name, (algo, data, fid, prior_file, agents, iterations, seeds) in SIM_CASES.items():
+        truth = pd.read_csv(os.path.join(DATA, f"{data}_hifi.csv"))
+        hyp = pd.read_csv(os.path.join(DATA, f"{data}_{fid}_hyp.csv"))
+        prior = pd.read_csv(os.path.join(DATA, prior_file or "null_prior.csv"))
+        out[name + "_truth"] = truth.values.astype(np.float64)
+        out[name + "_hyp"] = hyp.values.astype(np.float64)[0]
+        out[name + "_prior"] = prior.values.astype(np.float64).reshape(-1, 3)
+        out[name + "_meta"] = np.array([agents, iterations, len(seeds)], dtype=np.int64)
+        out[name + "_seeds"] = np.array(seeds, dtype=np.int64)
+        for s in seeds:
+            st = SeedStreams(s)
+            gaps = []
+
+            def cmv(vor, truth_arr, var_star):
+                var = np.diag(var_star)
+                g = []
+                for cell in vor.filtered_regions:
+                    v = vor.vertices[cell, :]
+                    inside = sim.in_polygon(truth_arr[:, 0], truth_arr[:, 1], v[:, 0], v[:, 1])
+                    iv = np.sort(var[inside])
+                    g.append(iv[-1] - iv[-2] if iv.size > 1 else np.inf)
+                gaps.append(g)
+                return real_cmv(vor, truth_arr, var_star)
+            sim.compute_max_var = cmv
+            sim.random = types.SimpleNamespace(random=lambda: float(st.explore.random()))
+            sim.np.random.default_rng = lambda *a, **k: st.noise
+            sim.np.array = arr
+            try:
+                fn = sim.todescato if algo == "todescato" else sim.periodic
+                logs = fn(name, s, iterations, agents, st.start_positions(agents), truth, 0.1, prior, hyp,
+                          False, None, True)
+            finally:
+                sim.compute_max_var, sim.random, sim.np.random.default_rng = real_cmv, real_random, real_rng
+                sim.np.array = real_arr
+            for recs, cols, kind in zip(logs, runner.SCHEMAS, ("loss", "agent", "sample")):
+                out[f"{name}_s{s}_{kind}"] = runner.encode(recs, cols)
+            out[f"{name}_s{s}_gaps"] = np.array(gaps, dtype=np.float64)
+            print(name, "seed", s, "samples", len(logs[2]), "min gap", np.min(gaps))
+    out["cases"] = np.array(list(SIM_CASES))
+    np.savez_compressed(os.path.join(OUT, "sim_reference.npz"), **out)
+
+
 def make_log_headers():
     """6. ``log_headers.json``: the column headers of the reference's own logs
     (Data/atc24_choi_hmf_{loss,agent,sample}.csv), for the runner's CSV schemas."""
@@ -360,6 +437,10 @@ if __name__ == "__main__":
         make_replay_fixtures()
         make_prior_fixtures()
         sys.exit(0)
+    if sys.argv[1:] == ["sims"]:      # only the planner runs (sim_reference.npz)
+        _import_reference()
+        make_sim_fixture(_import_simulator())
+        sys.exit(0)
     gp = _import_reference()
     make_reference_fixture(gp)
     make_replay_fixtures()
@@ -368,3 +449,4 @@ if __name__ == "__main__":
     make_cells_fixture(sim)
     make_nlml_fixture(gp)
     make_log_headers()
+    make_sim_fixture(sim)

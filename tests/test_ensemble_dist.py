@@ -26,12 +26,12 @@ def _traj(seed, T):
     return np.random.default_rng(seed).random(T)
 
 
-def _worker(rank, world, port, T, S_per, out_q):
+def _worker(rank, world, port, T, S, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    seeds = shard_seeds(S_per * world, world, rank)
-    traj = torch.tensor(np.stack([_traj(s, T) for s in seeds]))
+    seeds = shard_seeds(S, world, rank)
+    traj = torch.tensor(np.stack([_traj(s, T) for s in seeds])) if seeds else torch.zeros((0, T), dtype=torch.float64)
     allt, mean, std = gather_trajectories(traj, world)
     if rank == 0:
         out_q.put((allt.numpy(), mean.numpy(), std.numpy()))
@@ -45,20 +45,23 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gather_trajectories_gloo(world):
-    T, S_per = 12, 3
+@pytest.mark.parametrize("world,S", [(2, 6), (3, 7), (8, 100), (3, 2)])
+def test_gather_trajectories_gloo(world, S):
+    """Even and uneven shards: 7 seeds over 3 ranks (3/2/2), the reference's
+    default 100 simulations (runner.py:85) over 8 ranks (13/12), and a rank with
+    no seeds at all (2 over 3)."""
+    T = 12
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, T, S_per, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, T, S, q)) for r in range(world)]
     for p in procs:
         p.start()
     allt, mean, std = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    ref = np.stack([_traj(s, T) for s in range(S_per * world)])
+    ref = np.stack([_traj(s, T) for s in range(S)])
     np.testing.assert_array_equal(allt, ref)
     np.testing.assert_allclose(mean, ref.mean(0), rtol=1e-14)
     np.testing.assert_allclose(std, ref.std(0, ddof=1), rtol=1e-12)

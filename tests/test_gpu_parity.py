@@ -283,7 +283,7 @@ def test_headline_size_vs_oracle(gp):
 
 def test_configs4_size_vs_oracle(gp):
     """BASELINE configs[4] sizes for one GP: 256x256 grid (M = 65536), N = 4096 lofi + 4096 hifi,
-    australia9 MF hyp, at fp64 (the fp32 mode is not built). The full
+    australia9 MF hyp, at fp64 (the fp32 mode of configs[4] is tests/test_gpu_f32.py). The full
     factor + predict, then an 8-row bordered append (the incremental path), each against the
     diag oracle on 4096 sampled cells plus the new samples' cells and the device's argmax
     cell, at the parity tolerance."""
