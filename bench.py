@@ -108,6 +108,8 @@ def parse():
     p.add_argument("--seeds-per-gpu", type=int, default=None)
     p.add_argument("--seeds", type=int, default=None,
                    help="total seeds over all ranks (default gpus x seeds-per-gpu); need not divide evenly")
+    p.add_argument("--streams", type=int, default=None,
+                   help="sub-batches of the rank's seeds stepped concurrently on their own streams")
     p.add_argument("--warm-ms", type=float, default=300.0,
                    help="after the warm-up steps, keep stepping (untimed) until this much wall time has passed")
     p.add_argument("--sim-iterations", type=int, default=None,
@@ -125,9 +127,9 @@ def parse():
                    help="allow a diagnostic library (MFGP_LIB); its line is marked and is not a headline number")
     a = p.parse_args()
     pre = {"headline": dict(steps=200, warmup=20, full_steps=None, seeds_per_gpu=8, grid=128, nl=1024, nh=1024,
-                            hyp="australia8_mf", dtype="f64", sim_iterations=40),
+                            hyp="australia8_mf", dtype="f64", sim_iterations=40, streams=1),
            "configs4": dict(steps=20, warmup=3, full_steps=2, seeds_per_gpu=32, grid=256, nl=4096, nh=4096,
-                            hyp="australia9_mf", dtype="f32", sim_iterations=0)}[a.workload]
+                            hyp="australia9_mf", dtype="f32", sim_iterations=0, streams=1)}[a.workload]
     for key, v in pre.items():
         if getattr(a, key) is None:
             setattr(a, key, v)
@@ -410,33 +412,66 @@ def main():
     var = torch.empty(B * M, dtype=torch.float64, device=dev)
     ks = [k] * B
 
-    def run(incremental, W, K):
+    def run(incremental, W, K, nstreams=1):
         total = W + K
-        ctx = _lib.context() if incremental else _lib.Context(local)
-        ctx.set_stream(stream.cuda_stream)
-        ctx.set_incremental(incremental)
-        # MFGP_FUSED=0: the append and the predict as two launches (diagnostic)
-        ctx.set_fused(FUSED)
-        models = []
-        for wl in wls:
-            mdl = _lib.Model(ctx, _lib.MF, hyp, 1e-8, dtype=dtype)
-            mdl.set_grid(wl.xs)
-            mdl.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
-            models.append(mdl)
-        # the posterior of the base rows (N - k), as the simulator predicts before
-        # every update (sim:885-892); the incremental steps start from it
-        _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
+        # the rank's seeds as `nstreams` contiguous sub-batches, each stepped by its
+        # own context on its own stream (concurrent launches: mfgp_ctx_set_concurrent);
+        # one sub-batch: the library's context on the bench's torch stream
+        NS = max(1, min(nstreams, B))
+        glo = [g * B // NS for g in range(NS + 1)]
+        ctxs = []
+        for g in range(NS):
+            if NS == 1:
+                c = _lib.context() if incremental else _lib.Context(local)
+                c.set_stream(stream.cuda_stream)
+            else:
+                c = _lib.Context(local)
+                c.set_concurrent(True)
+            c.set_incremental(incremental)
+            # MFGP_FUSED=0: the append and the predict as two launches (diagnostic)
+            c.set_fused(FUSED)
+            ctxs.append(c)
+        models, batches = [], []
+        for g in range(NS):
+            mg = []
+            for wl in wls[glo[g]:glo[g + 1]]:
+                mdl = _lib.Model(ctxs[g], _lib.MF, hyp, 1e-8, dtype=dtype)
+                mdl.set_grid(wl.xs)
+                mdl.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
+                mg.append(mdl)
+            models.extend(mg)
+            batches.append(_lib.Batch(mg, ks[glo[g]:glo[g + 1]]))
         varmax = torch.zeros(total, B, dtype=torch.float64, device=dev)
-
-        batch = _lib.Batch(models, ks)
         xp0, yp0, vp0 = Xnew.data_ptr(), ynew.data_ptr(), varmax.data_ptr()
         mup, varp = mu.data_ptr(), var.data_ptr()
+        # the posterior of the base rows (N - k), as the simulator predicts before
+        # every update (sim:885-892); the incremental steps start from it
+        for g in range(NS):
+            _lib.batch_predict(batches[g].models, mup + 8 * glo[g] * M, varp + 8 * glo[g] * M)
+
+        def sync_all():
+            for c in ctxs:
+                c.synchronize()
 
         def step(s):
-            batch.truncate(NH0)
-            # VarMax of every seed (np.amax(cov), simulator.py:1014) fused into the predict epilogue
-            batch.append_predict(xp0 + s * (B * k * 2 * 8), yp0 + s * (B * k * 8), mup, varp, asynchronous=True,
-                                 vmax_ptr=vp0 + s * (B * 8))
+            for g in range(NS):
+                lo = glo[g]
+                batches[g].truncate(NH0)
+                # VarMax of every seed (np.amax(cov), simulator.py:1014) fused into the predict epilogue
+                batches[g].append_predict(xp0 + 8 * (s * B * k * 2 + lo * k * 2), yp0 + 8 * (s * B * k + lo * k),
+                                          mup + 8 * lo * M, varp + 8 * lo * M, asynchronous=True,
+                                          vmax_ptr=vp0 + 8 * (s * B + lo))
+
+        def timing_all():
+            ts = [c.timing() for c in ctxs]
+            return {key: sum(t[key] for t in ts) for key in ts[0]}
+
+        def set_timing(on, predict_only=False):
+            for c in ctxs:
+                c.enable_timing(on, predict_only=predict_only)
+                if on:
+                    c.set_timing_stride(1)
+                    c.reset_timing()
 
         def aggregate(traj):
             if backend != "nccl":
@@ -452,29 +487,27 @@ def main():
         tw0 = time.perf_counter()
         for s in range(W):
             if s == 0 and incremental:
-                ctx.enable_timing(True)
-                ctx.set_timing_stride(1)
-                ctx.reset_timing()
+                set_timing(True)
             step(s)
             if s == 0 and incremental:
-                ctx.synchronize()
-                lat_build_ms = ctx.timing()["factor_ms"]
-                ctx.enable_timing(False)
+                sync_all()
+                lat_build_ms = timing_all()["factor_ms"]
+                set_timing(False)
         # a short run (the driver's --steps 20 is ~2 ms of GPU work) would otherwise
         # time the clock ramp: keep stepping, untimed, on the warm-up inputs (every
         # step truncates back to the same rows, so any input is a valid step) until
         # warm_ms of wall time has passed
         extra = 0
-        ctx.synchronize()
+        sync_all()
         while W > 1 and (time.perf_counter() - tw0) * 1e3 < a.warm_ms:
             for _ in range(16):
                 step(1 + extra % (W - 1))
                 extra += 1
-            ctx.synchronize()
+            sync_all()
         aggregate(varmax[:W].transpose(0, 1).contiguous())   # first-use kernel loads / communicator setup
-        ctx.synchronize()
-        # the timed region: exactly K steps, nothing else on the stream (no HIP events)
-        ctx.enable_timing(False)
+        sync_all()
+        # the timed region: exactly K steps, nothing else on the streams (no HIP events)
+        set_timing(False)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -495,40 +528,37 @@ def main():
         agg = aggregate(traj)
         torch.cuda.synchronize(dev)
         tg1 = time.perf_counter()
-        ctx.synchronize()   # raises LinAlgError if any factor was not positive definite
+        sync_all()   # raises LinAlgError if any factor was not positive definite
         # the kernel's launch time (roofline): R more untimed steps on the same
-        # inputs, HIP events around every launch on the launch stream
+        # inputs, HIP events around every launch on each launch stream
         R = min(K, 50) if incremental else min(K, 3)
-        ctx.enable_timing(True, predict_only=True)
-        ctx.set_timing_stride(1)
-        ctx.reset_timing()
+        set_timing(True, predict_only=True)
         for s in range(W, W + R):
             step(s)
-        ctx.synchronize()
-        tm = ctx.timing()
+        sync_all()
+        tm = timing_all()
         # per-stage breakdown: a few more (untimed) steps with every stage bracketed by events
-        ctx.enable_timing(True)
-        ctx.set_timing_stride(1)
-        ctx.reset_timing()
+        set_timing(True)
         nb_steps = min(5 if incremental else 1, K)
         for s in range(W, W + nb_steps):
             step(s)
-        ctx.synchronize()
-        tb = ctx.timing()
-        ctx.enable_timing(False)
+        sync_all()
+        tb = timing_all()
+        set_timing(False)
         el = torch.tensor([t1 - t0, tg1 - tg0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         if not diag_lib:   # diagnostic library builds compute garbage on purpose
             assert torch.isfinite(agg).all()
         st = models[0].stats()
-        del models
+        del models, batches
         return {"elapsed": float(el[0].item()), "gather_ms": 1e3 * float(el[1].item()), "tm": tm,
-                "lat_build_ms": lat_build_ms, "extra_warmup_steps": extra,
+                "lat_build_ms": lat_build_ms, "extra_warmup_steps": extra, "streams": NS,
+                "gps_per_launch": B / NS,
                 "host_ms": 1e3 * float(np.mean(host_t)), "stats": st, "traj": traj.cpu().numpy(), "R": R,
-                "breakdown": {"predict": tb["predict_ms"] / nb_steps, "factor": tb["factor_ms"] / nb_steps}}
+                "breakdown": {"predict": tb["predict_ms"] / nb_steps / NS, "factor": tb["factor_ms"] / nb_steps / NS}}
 
-    inc = run(True, W, K)
+    inc = run(True, W, K, a.streams)
     full = None if a.no_full else run(False, W, KF)
     sim = simulation_leg(a, world, rank, my_seeds, wls, hyp, dev, backend) if a.sim_iterations else None
     if os.environ.get("MFGP_BENCH_DUMP") and rank == 0:
@@ -551,6 +581,9 @@ def main():
             vbytes = B * (4 * M * (n0 + k) + 32 * M + n0 * (16 * k + 4 * 16 + 8))
         else:
             vbytes = B * 8 * (M * (n0 + k + 4) + n0 * (3 * k + 1))
+        # (sub-batches on concurrent streams: a launch covers B / streams GPs)
+        shr = inc["gps_per_launch"] / B
+        vbytes = vbytes * shr
         v_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
         v_gbs = vbytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
         # the lattice step in axis form (k_inc_lat). Bytes: F's
@@ -564,8 +597,8 @@ def main():
         ny8 = -(-G // 8) * 8
         fbytes = 8 * sum((n0 - 64 * jb) * 64 for jb in range(-(-n0 // 64)))
         zbytes = 8 * parts * ny8 * G * ka * (1 + -(-G // 64))
-        lat_bytes = B * (fbytes + 8 * 6 * M + es * M * k + zbytes)
-        lat_flops = B * (16 * n0 * n0 + 2 * ka * G * n_t + 2 * ka * M * parts * ny8)
+        lat_bytes = B * (fbytes + 8 * 6 * M + es * M * k + zbytes) * shr
+        lat_flops = B * (16 * n0 * n0 + 2 * ka * G * n_t + 2 * ka * M * parts * ny8) * shr
         lat_gbs = lat_bytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
         lat_tf = lat_flops / (v_ms * 1e-3) / 1e12 if v_ms > 0 else float("nan")
         value = total_seeds * K / elapsed
@@ -631,6 +664,11 @@ def main():
                               "region (no events inside the timed region)",
                     "design_bytes_note": f"{es}-byte V: bytes_per_launch = the resident V read once plus the new "
                                          "rows, grid, outputs and per-row L21 / z terms (DESIGN.md section 4)"}
+        # the step's algorithmic bytes over the whole step's wall time (all sub-batches)
+        step_bytes = roof["bytes_per_launch"] / shr
+        roof["streams"] = inc["streams"]
+        roof["step_aggregate_gbs"] = step_bytes / (elapsed / K) / 1e9
+        roof["step_aggregate_frac"] = roof["step_aggregate_gbs"] / PEAK_HBM_GBS
         if default_cfg:
             wl_name = "australia8_mf MFGP seed ensemble (BASELINE configs[3])"
         elif c4_cfg:

@@ -89,6 +89,16 @@ int mfgp_ctx_set_deferred_appends(mfgp_ctx* ctx, int enable);
  * it; 2 = take the lattice step for them too (tests). 0 = always the V stream
  * (k_inc_stream). Same numbers to rounding. */
 int mfgp_ctx_set_lattice(mfgp_ctx* ctx, int enable);
+/* Declare that this context's launches may run concurrently with launches of
+ * other contexts on the same GPU (several streams stepping independent batches
+ * side by side, e.g. a rank's seeds as four sub-batches). Default 0. With it no
+ * launch relies on all of its workgroups being resident at once: the lattice
+ * step always runs its GEMM as the second launch (k_lat_gemm2) rather than as
+ * split-K tiles that wait for each other inside the first. Every other
+ * cross-workgroup wait in the library is on a workgroup with a lower linear id,
+ * dispatched (and so resident) before its waiter, which stays safe when other
+ * kernels share the GPU. */
+int mfgp_ctx_set_concurrent(mfgp_ctx* ctx, int enable);
 /* Kernel timing with HIP events on the launch stream: enable = 1 times every
  * predict-kernel launch (fused predict or one-pass incremental predict) and
  * every factor stage; 2 times the predict launches only (each event pair is a

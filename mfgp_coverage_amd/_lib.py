@@ -35,6 +35,7 @@ SIGNATURES = {
     "mfgp_ctx_set_deferred_appends": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_lattice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_set_timing_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "mfgp_ctx_set_concurrent": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_batch_append_predict_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -179,6 +180,12 @@ class Context:
         GEMM tiles in the batch to fill the GPU), or always the one-pass V stream.
         on="force": also for batches too small to fill the GPU (tests)."""
         check(lib().mfgp_ctx_set_lattice(self.handle, 2 if on == "force" else (1 if on else 0)))
+
+    def set_concurrent(self, on=True):
+        """This context's launches may run beside other contexts' on the same GPU
+        (mfgp_ctx_set_concurrent): no launch relies on all its workgroups being
+        resident at once (the lattice GEMM always as its own launch)."""
+        check(lib().mfgp_ctx_set_concurrent(self.handle, 1 if on else 0))
 
     def enable_timing(self, on=True, predict_only=False):
         """HIP-event timing of the predict launches (and, unless predict_only, the factor stages)."""

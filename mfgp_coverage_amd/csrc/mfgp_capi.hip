@@ -108,6 +108,11 @@ struct mfgp_ctx {
   bool trinv_columns = false;  // F by the block-column k_trinv_f instead of recursive doubling (MFGP_TRINV_COLUMNS)
   int factor_depth = 4;        // 64-column steps per trailing-update pass of the factor (MFGP_FACTOR_DEPTH; 1: one-level)
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
+  // launches of this context may run concurrently with other contexts' (several
+  // streams on one GPU, mfgp_ctx_set_concurrent): no launch may rely on all of its
+  // workgroups being resident at once -- the lattice step's GEMM runs as the second
+  // launch (k_lat_gemm2, no cross-workgroup waits) instead of in-launch split-K tiles
+  bool concurrent = false;
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
                               // (MFGP_DESC_ARG=0: upload them, diagnostics)
@@ -1380,6 +1385,13 @@ int mfgp_ctx_set_lattice(mfgp_ctx* c, int enable) {
   return MFGP_OK;
 }
 
+int mfgp_ctx_set_concurrent(mfgp_ctx* c, int enable) {
+  if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->concurrent = enable != 0;
+  return MFGP_OK;
+}
+
 int mfgp_ctx_enable_timing(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   c->timing = (enable == 2) ? 2 : (enable != 0 ? 1 : 0);
@@ -2031,6 +2043,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         int64_t t2 = 0;
         for (int i = 0; i < ninc; ++i) t2 += lat_tiles2(order[i], ka);
         g2 = c->lat_gemm2 > 0 || (c->lat_gemm2 < 0 && t2 >= c->ncu && t2 <= 2 * (int64_t)c->ncu);
+        // (split-K tiles of one launch wait for each other: they need the whole chip)
+        if (c->concurrent) g2 = true;
       }
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_coverage.py tests/test_gpu_headline.py "tests/test_gpu_incremental.py::test_headline_batch_default_step_vs_full" \
   tests/test_sharded.py tests/test_boundary.py > gpurun_out/r04a_tests.log 2>&1
 rc=$?
