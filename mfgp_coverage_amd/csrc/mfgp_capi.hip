@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdarg>
@@ -113,6 +114,7 @@ struct mfgp_ctx {
   // workgroups being resident at once -- the lattice step's GEMM runs as the second
   // launch (k_lat_gemm2, no cross-workgroup waits) instead of in-launch split-K tiles
   bool concurrent = false;
+  int64_t spin_us = 2000;     // host polling of mapped status words before a synchronise (MFGP_SPIN_US; 0: off)
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
                               // (MFGP_DESC_ARG=0: upload them, diagnostics)
@@ -480,6 +482,10 @@ int release_slot(mfgp_ctx* c, int slot) {
   c->ring_used[slot] = true;
   return MFGP_OK;
 }
+// A slot whose descriptors went into a launch by value (kernel argument: copied at
+// the launch call) and were never uploaded: nothing on the stream reads it, so it
+// needs no event (one hipEventRecord less per step: the drop-in step's host time).
+void release_slot_unread(mfgp_ctx* c, int slot) { c->ring_used[slot] = false; }
 
 constexpr int STATUS_UNSET = INT_MIN + 1;   // status_host before the launch writes it
 
@@ -1262,6 +1268,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   }
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_SPIN_US")) c->spin_us = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("MFGP_LAT_WU")) c->lat_wu = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("MFGP_LAT_SELFG")) c->lat_selfg = std::atoi(e) != 0;
@@ -1327,10 +1334,28 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
   if (rc) return rc;
   // the status words come back through pinned memory with the stream's last copies
   // (or straight from the mapped word the launch itself published them into)
+  bool all_mapped = !c->async_status.empty();
   for (size_t i = 0; i < c->async_status.size(); ++i)
-    if (!c->async_status[i].host)
+    if (!c->async_status[i].host) {
+      all_mapped = false;
       HIP_TRY(hipMemcpyAsync(c->h_status + i, c->async_status[i].dev, sizeof(int), hipMemcpyDeviceToHost,
                              c->stream));
+    }
+  if (all_mapped && c->spin_us > 0) {
+    // launches that publish their status into mapped host memory as their last act
+    // (the one-GP fused step: the drop-in simulator's updt_hifi): poll those words
+    // first, so that the stream synchronisation below starts when the kernel is
+    // about to end and returns within its active-wait phase instead of sleeping
+    // through the kernel and waking late (the outputs are visible only after it)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (size_t i = 0; i < c->async_status.size(); ++i) {
+      const volatile int* w = reinterpret_cast<const volatile int*>(c->async_status[i].host);
+      while (*w == STATUS_UNSET) {
+        __builtin_ia32_pause();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->spin_us)) break;
+      }
+    }
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (size_t i = 0; i < c->async_status.size(); ++i) {
     const auto& as = c->async_status[i];
@@ -1864,7 +1889,10 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
   // copied into the outputs with its var max / argmax (k_post_copy, one launch),
   // and the batch step runs over the others -- so a ragged batch keeps its one
   // fused (or lattice) launch instead of falling back to streaming V for all.
-  if (do_factor && do_predict && !out_offs && c->incremental && is_device_ptr(mu) && is_device_ptr(var)) {
+  bool any_unchanged = false;   // (cheap test first: the pointer queries cost ~1 us each)
+  for (int i = 0; i < count && !any_unchanged; ++i) any_unchanged = !(k && X && y) || k[i] == 0;
+  if (any_unchanged && do_factor && do_predict && !out_offs && c->incremental && is_device_ptr(mu) &&
+      is_device_ptr(var)) {
     const bool rows_given = k && X && y;
     std::vector<PostCopy> pc;
     std::vector<mfgp_model*> rest;
@@ -2187,21 +2215,22 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       HIP_TRY(launch_inc_stream1(hd[0], hd[0].nprod + ntiles_wg(hd[0].M, hd[0].rsplit, hd[0].vf32), hd[0].vf32,
                                  c->stream));
       if ((rc = ev_end(c, ev))) return rc;
-      if ((rc = release_slot(c, slot))) return rc;
+      release_slot_unread(c, slot);
       m->v_n = m->NL + m->NH;
       m->n_vstream += 1;
       if (res_b[0] >= 0) res_tag(m, res_b[0], m->v_n, 0);
       continue;
     }
-    bool lat_arg = false;
+    bool lat_arg = false, by_value = false;
     if (do_factor && lat && nfull == 0 && ninc == nb && np == nv && desc_arg_ok(c, hd, ninc)) {
       // the whole step is one k_inc_lat launch: its descriptors go by value
       if ((rc = enqueue_inc_lat_arg(c, hd, ninc))) return rc;
-      lat_arg = true;
+      lat_arg = by_value = true;
     } else if (do_factor && fuse && !lat && nfull == 0 && ninc == nb && np == nv && c->desc_arg &&
                ninc <= DESC_ARG_MAX) {
       // the whole step is one k_inc_stream launch (append + one-pass predict)
       if ((rc = enqueue_inc_stream_arg(c, hd, ninc))) return rc;
+      by_value = true;
     } else {
     const GPDesc* dd = nullptr;
     if ((rc = upload_slot(c, slot, nb + np, &dd))) return rc;
@@ -2215,7 +2244,11 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     if (nv > 0 && !fuse && (rc = enqueue_vstream(c, dd + nb, hd + nb, nv))) return rc;
     if (np > nv && (rc = enqueue_predict(c, dd + nb + nv, hd + nb + nv, np - nv))) return rc;
     }
-    if ((rc = release_slot(c, slot))) return rc;
+    if (by_value) {
+      release_slot_unread(c, slot);
+    } else if ((rc = release_slot(c, slot))) {
+      return rc;
+    }
     for (int i = 0; i < np; ++i) {
       mfgp_model* m = porder[i];
       m->v_n = m->NL + m->NH;

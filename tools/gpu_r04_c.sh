@@ -18,3 +18,9 @@ for f in ("r04c_bench20", "r04c_bench200"):
     if "simulation" in d:
         print(json.dumps(d["simulation"]))
 PY
+# A/B: the w units gather L21 from V themselves at B = 8 (default: only one GP)
+MFGP_LAT_SELFG=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-full --sim-iterations 0 --diagnostic > gpurun_out/r04c_selfg1.json 2> gpurun_out/r04c_selfg1.err || exit $?
+python -c "import json;d=json.load(open('gpurun_out/r04c_selfg1.json'));print('selfg1', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+timeout -k 10 120 python -u tools/dropin_r04.py > gpurun_out/r04c_dropin.json 2>/dev/null || exit $?
+timeout -k 10 120 python -u tools/dropin_r04.py --timing > gpurun_out/r04c_dropin_t.json 2>/dev/null || exit $?
+cat gpurun_out/r04c_dropin.json gpurun_out/r04c_dropin_t.json
