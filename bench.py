@@ -168,8 +168,9 @@ def pmc_traffic(kernel="k_predict", tag=None):
 
 def pmc_mfma(kernel):
     """MFMA utilisation of `kernel` from the newest committed rocprofv3 summary
-    (profiles/<round>_mfma_util.csv: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per
-    XCD x 1024 SIMDs), with the shader clock it implies)."""
+    (profiles/<round>_mfma_util.csv, tools/summarize_profile.py): the busy cycles over
+    the kernel's own duration at the measured shader clock (mfma_util), and beside it
+    the GRBM-per-XCD form (mfma_util_grbm, unreliable for short dispatches)."""
     import glob
     import csv
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_mfma_util.csv")))
@@ -178,8 +179,11 @@ def pmc_mfma(kernel):
     with open(files[-1]) as f:
         for row in csv.DictReader(f):
             if kernel in row["Name"]:
-                return {"mfma_util": float(row["mfma_util"]), "clock_ghz": float(row["clock_ghz"]),
-                        "source": os.path.relpath(files[-1], ROOT)}
+                out = {"mfma_util": float(row["mfma_util"]), "source": os.path.relpath(files[-1], ROOT)}
+                for k in ("mfma_util_grbm", "sclk_ghz", "clock_ghz"):
+                    if k in row and row[k]:
+                        out[k] = float(row[k])
+                return out
     return None
 
 

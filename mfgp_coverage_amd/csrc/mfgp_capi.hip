@@ -557,6 +557,20 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.hp = d.hf;
 }
 
+// A model's status word to check at the next mfgp_ctx_synchronize. One entry per
+// model: every entry of a model would read the same device word (its value after
+// the model's last launch), so repeated ASYNC steps add no copies to the sync. A
+// model's entry that the one-GP fused launch publishes into mapped memory
+// (host != null) is replaced by the device word when a later step does not.
+void add_async_status(mfgp_ctx* c, mfgp_model* m) {
+  for (auto& a : c->async_status)
+    if (a.m == m) {
+      a.host = nullptr;   // (a later launch of this model may not publish: read the word)
+      return;
+    }
+  c->async_status.push_back({m, m->status, nullptr});
+}
+
 // ---- resident posterior (two buffers, tagged with the rows and generation) ----
 int ensure_res(mfgp_model* m) {
   if (m->res && m->res_M >= m->M) return MFGP_OK;
@@ -2000,7 +2014,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; i < ninc + nfull; ++i) {   // host bookkeeping of the factors enqueued below
         if (i < ninc) mark_inc_factor(order[i]);
         else mark_full_factor(order[i]);
-        c->async_status.push_back({order[i], order[i]->status, nullptr});
+        add_async_status(c, order[i]);
       }
     }
     // predict descriptors (state after the factor step), ordered

@@ -956,6 +956,15 @@ __device__ __forceinline__ void acquire_agent() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
 }
+// The narrow form (MFGP_ACQUIRE_NARROW builds): the acquire
+// is made once per wait by the polling wave, right after it saw the flag, and the
+// workgroup barrier that follows carries it to the other waves (no acquire after
+// the barrier in every wave).
+__device__ __forceinline__ void acquire_poller() {
+#ifdef MFGP_ACQUIRE_NARROW
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
 __device__ __forceinline__ void publish(unsigned* f, unsigned v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -973,6 +982,7 @@ __device__ void wait_flag(const GPDesc& d, const unsigned* f, unsigned v) {
         break;
       }
     }
+    acquire_poller();
   }
   __syncthreads();
   acquire_agent();
@@ -998,6 +1008,7 @@ __device__ void wait_l21(const GPDesc& d) {
         break;
       }
     }
+    acquire_poller();
   }
   __syncthreads();  acquire_agent();
 }
@@ -2005,6 +2016,7 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
           break;
         }
       }
+      acquire_poller();
     }
     __syncthreads();
     acquire_agent();
@@ -2324,6 +2336,7 @@ __device__ __forceinline__ void vstream_wg_f32(const GPDesc& d, int64_t wgt, dou
           break;
         }
       }
+      acquire_poller();
     }
     __syncthreads();
     acquire_agent();

@@ -154,6 +154,7 @@ __device__ void wait_l21_from(const GPDesc& d, int64_t lo) {
         break;
       }
     }
+    acquire_poller();
   }
   __syncthreads();  acquire_agent();
 }
@@ -167,7 +168,9 @@ __device__ __forceinline__ void spin_wave(const GPDesc& d, const unsigned* f, un
       if ((threadIdx.x & 63) == 0) atomicMin(d.status, SYNC_FAIL);
       break;
     }
-  }  acquire_agent();
+  }
+  acquire_poller();   // (this wave is its own poller)
+  acquire_agent();
 }
 
 template <class VT>
@@ -561,6 +564,7 @@ __device__ void wait_flags_all(const GPDesc& d, const unsigned* f, int64_t n, un
         break;
       }
     }
+    acquire_poller();
   }
   __syncthreads();  acquire_agent();
 }
