@@ -1458,7 +1458,15 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
   double* const Fn = Li + KINC * KINC;             // new rows' tables [2][KA][FW]
   double* const amx = Fn + 2 * 16 * (4 + 64);      // the waves' (max, argmax)
   WTRACE2(0);
-  // ---- the cells' inputs (written by the first launch) ----
+#ifndef MFGP_G2_PRIME
+#define MFGP_G2_PRIME 0
+#endif
+  // the cells' inputs (written by the first launch): L22 | z2, the new rows' tables,
+  // then L22^-1 by forward substitution (16 threads). MFGP_G2_PRIME=1 issues the K
+  // loop's first stages before these loads (their latencies overlapped): 92.1-92.7k
+  // vs 92.9-93.1k GP-updates/s without, alternating runs on one box (round 4,
+  // tools/ab_variants.sh) -- within noise, so off
+  auto prologue = [&]() {
   for (int e = tid; e < KINC * KINC + KINC; e += G2NT) {
     const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
     L22[e] = use ? d.l22r[e] : 0.0;
@@ -1485,6 +1493,7 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
       Li[i * KINC + c] = x[i];
     }
   }
+  };
   // ---- the K loop: split s, wave w: tile rows 16 w + r, all 64 columns ----
   // Each split streams its stages through its own LDS ring (buffer_load ... lds,
   // G2NST stages, one s_barrier per stage for the whole workgroup: the four splits
@@ -1535,10 +1544,14 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
   constexpr int CNT = 2;         // DMAs per issued stage (every wave)
   static_assert((D - 1) * CNT <= 12, "vm_wait_bar covers the outstanding DMAs");
   int64_t slot0 = 0;
-  auto pass = [&](int64_t nlist, bool virt) {
+  auto prime = [&](int64_t nlist, bool virt) {   // the pass's first D stages
+    const int64_t hi = s < nlist ? (nlist - s + G2S - 1) / G2S : 0;
+    for (int64_t t = 0; t < D && t < hi; ++t) issue(s + t * G2S, virt, slot0 + t);
+  };
+  auto pass = [&](int64_t nlist, bool virt, bool primed) {
     const int64_t hi = s < nlist ? (nlist - s + G2S - 1) / G2S : 0;   // this split's stages
     const int64_t him = (nlist + G2S - 1) / G2S;                      // split 0's: the most
-    for (int64_t t = 0; t < D && t < hi; ++t) issue(s + t * G2S, virt, slot0 + t);
+    if (!primed) prime(nlist, virt);
     for (int64_t t = 0; t < him; ++t) {
       // this wave's DMA groups issued for stages after t
       const int64_t last = hi < t + D ? hi : t + D;
@@ -1566,10 +1579,18 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
     }
     slot0 += him;
   };
-  pass(NA, false);
+  if (MFGP_G2_PRIME) {
+    prime(NA, false);
+    prologue();   // (its barrier orders the ring's LDS-DMA writes with nothing: the
+                  // stages are waited for with vmcnt in the loop, as before)
+    pass(NA, false, true);
+  } else {
+    prologue();
+    pass(NA, false, false);
+  }
   if (nvs[0] + nvs[1] > 0) {
     __syncthreads();   // the ring's last reads of the axis pass are done
-    pass(nvs[0] + nvs[1], true);
+    pass(nvs[0] + nvs[1], true, false);
   }
   vm_wait_all();
   __syncthreads();   // every ring read is done: the rings become the splits' sums
