@@ -168,8 +168,9 @@ int64_t mfgp_model_m(const mfgp_model* m);
  * training rows of the last lattice step (read back from the device; synchronises
  * the context's stream; only when n > 9), lattice steps launched with their
  * descriptors as the kernel argument, lattice steps whose GEMM and cells ran as a
- * second launch (k_lat_gemm2), batch predicts served from the resident posterior
- * because the model appended nothing (k_post_copy)}; n <= 13. */
+ * second launch (k_lat_gemm2 or k_lat_gemm3), batch predicts served from the
+ * resident posterior because the model appended nothing (k_post_copy), lattice
+ * steps whose second launch built its own Z rows (k_lat_gemm3)}; n <= 14. */
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n);
 /* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
 int mfgp_get_factor(mfgp_model* m, double* L_out);

@@ -114,6 +114,9 @@ struct mfgp_ctx {
   // workgroups being resident at once -- the lattice step's GEMM runs as the second
   // launch (k_lat_gemm2, no cross-workgroup waits) instead of in-launch split-K tiles
   bool concurrent = false;
+  bool lat_g3 = false;        // the two-launch lattice step's second launch builds its own Z rows
+                              // (k_lat_gemm3) where it applies (MFGP_LAT_G3=1; off by default until
+                              // it beats k_lat_gemm2 at the headline)
   int64_t spin_us = 2000;     // host polling of mapped status words before a synchronise (MFGP_SPIN_US; 0: off)
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
@@ -179,6 +182,9 @@ struct mfgp_model {
   int64_t n_lattice_arg = 0;   // lattice steps launched with their descriptors by value (k_inc_lat_arg)
   int64_t n_lattice_g2 = 0;    // lattice steps whose GEMM and cells ran as a second launch (k_lat_gemm2)
   int64_t n_post_copy = 0;     // batch predicts served from the resident posterior (k_post_copy: nothing appended)
+  int64_t n_lattice_g3 = 0;    // two-launch lattice steps whose second launch built its Z rows (k_lat_gemm3)
+  unsigned* csr = nullptr;     // g3 buffer: member lists, places, c w rows (g3_bytes; mfgp_internal.h)
+  int64_t csr_n = 0;           // (bytes)
   // state generation: a new factor from scratch, a new grid or new hyperparameters
   // start a new one (the resident posterior, F and the tables belong to one)
   uint64_t gen = 1;
@@ -552,7 +558,8 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.wcnt = nullptr;
   d.lat_selfg = 0;
   d.lat_g2 = 0;
-  d.pad_g2_ = 0;
+  d.lat_g3 = 0;
+  d.csr = nullptr;
   d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
   d.hp = d.hf;
 }
@@ -733,6 +740,13 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     m->zb_w = tabw;
     m->zb_ka = ka;
   }
+  if (m->csr_n < g3_bytes(tabw, ld)) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (m->csr) HIP_TRY(hipFree(m->csr));
+    m->csr = nullptr;
+    m->csr_n = g3_bytes(tabw, ld);
+    HIP_TRY(hipMalloc(&m->csr, m->csr_n));
+  }
   if (!m->ldone) {
     HIP_TRY(hipMalloc(&m->ldone, sizeof(unsigned) * 4));
     HIP_TRY(hipMemsetAsync(m->ldone, 0, sizeof(unsigned) * 4, s));   // no arrivals; flags below every epoch
@@ -756,6 +770,7 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
   return MFGP_OK;
 }
 void free_lat(mfgp_model* m) {
+  if (m->csr) (void)hipFree(m->csr);
   if (m->F) (void)hipFree(m->F);
   if (m->tab) (void)hipFree(m->tab);
   if (m->wv) (void)hipFree(m->wv);
@@ -1071,7 +1086,8 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
   HIP_TRY(launch_inc_lat(dd, count, max_blocks, hd[0].ka, hd[0].vf32, !hd[0].lat_g2, c->stream));
-  if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2(dd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
+  if (hd[0].lat_g3) HIP_TRY(launch_lat_gemm3(dd, count, max_tiles, hd[0].vf32, c->stream));
+  else if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2(dd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
@@ -1108,7 +1124,8 @@ int enqueue_inc_lat_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
   HIP_TRY(launch_inc_lat_arg(hd, count, max_blocks, hd[0].ka, hd[0].vf32, !hd[0].lat_g2, c->stream));
-  if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2_arg(hd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
+  if (hd[0].lat_g3) HIP_TRY(launch_lat_gemm3_arg(hd, count, max_tiles, hd[0].vf32, c->stream));
+  else if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2_arg(hd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
@@ -1283,6 +1300,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_SPIN_US")) c->spin_us = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("MFGP_LAT_G3")) c->lat_g3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("MFGP_LAT_WU")) c->lat_wu = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("MFGP_LAT_SELFG")) c->lat_selfg = std::atoi(e) != 0;
@@ -1851,10 +1869,10 @@ int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
     if (m->kind == MFGP_MF) HIP_TRY(hipMemcpy(&nv[1], m->zvl + m->zb_rows + 1, sizeof(int), hipMemcpyDeviceToHost));
     virt = (int64_t)nv[0] + nv[1];
   }
-  const int64_t v[13] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+  const int64_t v[14] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
                          m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice, virt,
-                         m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy};
-  for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
+                         m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy, m->n_lattice_g3};
+  for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
@@ -2071,7 +2089,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     res_depth.assign(ninc, 0);
     int ka = 8;
     int64_t tiles_sum = 0, nst_min = INT64_MAX;
-    bool g2 = false;
+    bool g2 = false, g3 = false;
     if (lat) {
       for (int i = 0; i < ninc; ++i) {
         if (order[i]->NL + order[i]->NH - hd[i].n0 > 8) ka = 16;
@@ -2087,6 +2105,14 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         g2 = c->lat_gemm2 > 0 || (c->lat_gemm2 < 0 && t2 >= c->ncu && t2 <= 2 * (int64_t)c->ncu);
         // (split-K tiles of one launch wait for each other: they need the whole chip)
         if (c->concurrent) g2 = true;
+      }
+      // the second launch builds its own Z rows (k_lat_gemm3) where its tiles apply:
+      // KA = 8, 128-wide axis tables (the tile holds all 128 iy), each part's rows
+      // within what a scan unit sorts in LDS
+      g3 = g2 && c->lat_g3 && ka == 8;
+      for (int i = 0; g3 && i < ninc; ++i) {
+        const mfgp_model* m = order[i];
+        g3 = lat_tabw(m) == 128 && hd[i].n0 <= LAT_SCAN_MAX && m->ld <= 65535;
       }
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];
@@ -2153,8 +2179,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
-        const int64_t tiles = g2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
-        const int64_t nzu = lat_nzu(m);
+        const int64_t tiles = g3 ? (m->lat.nx + LAT_G3IX - 1) / LAT_G3IX : (g2 ? lat_tiles2(m, ka) : lat_tiles(m, ka));
+        // g3: one scan unit per part instead of the Z units
+        const int64_t nzu = g3 ? (m->kind == MFGP_SF ? 1 : 2) : lat_nzu(m);
         if ((rc = ensure_lat(m, tiles, S, ka, nzu))) return rc;
         const int bin = res_find(m, fd.n0);
         fd.rmu_in = res_mu(m, bin);
@@ -2194,6 +2221,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.lat_axbuild = m->axt_gen == m->gen ? 0 : 1;
         fd.lat_selfg = selfg;
         fd.lat_g2 = g2 ? 1 : 0;
+        fd.lat_g3 = g3 ? 1 : 0;
+        fd.csr = m->csr;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }
     }
@@ -2272,6 +2301,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         m->n_lattice += 1;
         if (lat_arg) m->n_lattice_arg += 1;
         if (g2) m->n_lattice_g2 += 1;
+        if (g3) m->n_lattice_g3 += 1;
         m->F_n = m->v_n;   // F's new rows and the new rows' tables came with the step
         m->F_gen = m->gen;
         m->tab_n = m->v_n;

@@ -2726,6 +2726,21 @@ hipError_t launch_lat_gemm2_arg(const GPDesc* h, int count, int64_t max_tiles, i
   else hipLaunchKernelGGL((k_lat_gemm2_arg<16, double>), g, dim3(G2NT), 0, s, a);
   return hipGetLastError();
 }
+hipError_t launch_lat_gemm3(const GPDesc* d, int count, int64_t max_tiles, int vf32, hipStream_t s) {
+  const dim3 g(count, (unsigned)max_tiles);
+  if (vf32) hipLaunchKernelGGL((k_lat_gemm3<float>), g, dim3(G3NT), 0, s, d);
+  else hipLaunchKernelGGL((k_lat_gemm3<double>), g, dim3(G3NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_lat_gemm3_arg(const GPDesc* h, int count, int64_t max_tiles, int vf32, hipStream_t s) {
+  if (count < 1 || count > DESC_ARG_MAX) return hipErrorInvalidValue;
+  DescArg a;
+  std::memcpy(a.d, h, sizeof(GPDesc) * count);
+  const dim3 g(count, (unsigned)max_tiles);
+  if (vf32) hipLaunchKernelGGL((k_lat_gemm3_arg<float>), g, dim3(G3NT), 0, s, a);
+  else hipLaunchKernelGGL((k_lat_gemm3_arg<double>), g, dim3(G3NT), 0, s, a);
+  return hipGetLastError();
+}
 hipError_t launch_lat_axes(const GPDesc* d, int count, int64_t max_tabw, hipStream_t s) {
   hipLaunchKernelGGL(k_lat_axes, dim3((unsigned)((4 * (max_tabw + 1) + 3) / 4), count), dim3(NT), 0, s, d);
   return hipGetLastError();

@@ -489,6 +489,13 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   __syncthreads();
   const int nlast = lastm[0];
   if (nlast == 0) return;
+  // g3: the members' c w rows go to their places in the lists (the scan units were
+  // dispatched first and are long done: the wait is one load)
+  const int P = d.hp.kind == 0 ? 1 : 2;
+  if (d.lat_g3) {
+    wait_flag(d, d.zflag, epoch);
+    if (P == 2) wait_flag(d, d.zflag + 1, epoch);
+  }
   // the blocks' w: every contributor's partial in slot order (the same bits whoever
   // is last), stored, then counted into ldone[0] together (one lane each; the Z
   // units wait for all nwb blocks)
@@ -514,6 +521,32 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     double* const wv = d.wv + 64 * jb * KINC;
 #pragma unroll
     for (int m = 0; m < 4; ++m) stx<true>(wv + tid + NT * m, own[m]);
+    if (d.lat_g3) {
+      // element tid + NT m is w[64 jb + (e >> 4)][e & 15]; the A operand's c w: the
+      // product k_lat_gemm3 and the Z units form (the same bits)
+      const Hyp& h = d.hp;
+      const double cL = h.kind == 0 ? h.sL : h.rho * h.sL, cLH = h.rho2 * h.sL;
+      const int* const place = reinterpret_cast<const int*>(d.csr + g3_pos_off(d.tabw, ld));
+      double* const cwb = reinterpret_cast<double*>(d.csr + g3_cw_off(d.tabw, ld));
+      int pl[4][2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int e = tid + NT * m, a = e & 15;
+        const int64_t j = 64 * jb + (e >> 4);
+        pl[m][0] = pl[m][1] = -1;
+        if (a < 8 && j < n0) {
+          pl[m][0] = __hip_atomic_load(place + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (P == 2 && j >= d.NL) pl[m][1] = __hip_atomic_load(place + ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int e = tid + NT * m, a = e & 15;
+        const int64_t j = 64 * jb + (e >> 4);
+        if (pl[m][0] >= 0) cwb[(int64_t)pl[m][0] * 8 + a] = own[m] * (j < d.NL ? cL : cLH);
+        if (pl[m][1] >= 0) cwb[(ld + pl[m][1]) * 8 + a] = own[m] * h.sH;
+      }
+    }
   }
   drain_stores();
   __syncthreads();
@@ -768,7 +801,7 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
         for (int m = 0; m < ZMB; ++m)
           if (m0 + m < nm_all[hh]) {
 #pragma unroll
-            for (int a = 0; a < KA; ++a) acc[hh][a] += cw[(hh * ZMB + m) * KA + a] * ex[hh][m];
+            for (int a = 0; a < KA; ++a) acc[hh][a] = __builtin_fma(cw[(hh * ZMB + m) * KA + a], ex[hh][m], acc[hh][a]);
           }
     }
     WTRACE(4);
@@ -835,6 +868,119 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
     arrive_phase(d.ldone + 2, epoch, d.nzu);
   }
   WTRACE(2);
+}
+
+// g3 (k_lat_gemm3 follows): in place of the Z units, one scan unit per part of the
+// GP lists the part's training rows j < n0 on the lattice by lattice y-row q, in
+// row order within each q -- the order in which a Z unit sums them -- as CSR in
+// d.csr (offsets [ny + 1], then the members (px << 16) | j), and its off-lattice
+// ("virtual") rows in row order in zvl (count, rows, padded to ZKS with the part's
+// first row) as the Z units list them, and each row's place in its list (-1: off the
+// lattice), by which the w units' block reducers store the members' c w rows in list
+// order (g3_cw_off) for the next launch. Nothing here needs w: the units are the
+// launch's first roles and finish while the w units stream F. A stable counting
+// sort: the buckets' sizes (LDS atomics), their offsets (a wave scan), then the
+// rows in chunks of NT in row order, each row's place = its bucket's running
+// offset + the same bucket's rows in the chunk's earlier waves + its rank among
+// its wave's lanes of that bucket (eight ballots). Plain stores: read by the next
+// launch.
+constexpr int SCAN_B = 160;   // buckets held: ny <= 128 lattice rows + the virtual one
+__device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t j_lo = part == 1 ? d.NL : 0;
+  const int n = (int)(d.n0 - j_lo);   // <= LAT_SCAN_MAX (the host's g3 bound)
+  const int ny = d.lat.ny;            // <= 128 (the host's bound: 128-wide tables)
+  int* const lq = reinterpret_cast<int*>(sm);   // [LAT_SCAN_MAX] bucket << 16 | px
+  int* const run = lq + LAT_SCAN_MAX;           // [SCAN_B] the buckets' next places
+  int* const wc = run + SCAN_B;                 // [NT / 64][SCAN_B] this chunk's counts
+  int* const vbase = wc + (NT / 64) * SCAN_B;   // the virtual bucket's first place
+  static_assert((LAT_SCAN_MAX + (1 + NT / 64) * SCAN_B + 2) / 2 <= LAT_LDS, "the scan unit's LDS fits");
+  const int* const lidx = d.lidx + j_lo;
+  for (int b = tid; b < (1 + NT / 64) * SCAN_B; b += NT) run[b] = 0;
+  __syncthreads();
+  constexpr int SU = 8;   // rows loaded ahead per thread
+  for (int e0 = 0; e0 < n; e0 += SU * NT) {
+    int li[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int e = e0 + u * NT + tid;
+      li[u] = e < n ? lidx[e] : -2;
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      if (li[u] == -2) continue;
+      const int b = li[u] >= 0 ? (li[u] >> 16) : ny;
+      lq[e0 + u * NT + tid] = (b << 16) | (li[u] >= 0 ? (li[u] & 0xffff) : 0);
+      __hip_atomic_fetch_add(run + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  unsigned* const off = d.csr + (int64_t)part * (d.tabw + 1 + d.ld);
+  unsigned* const mem = off + d.tabw + 1;
+  if (wv == 0) {   // exclusive offsets of buckets 0 .. ny (ny: the virtual rows)
+    int base = 0;
+    for (int s0 = 0; s0 <= ny; s0 += 64) {
+      const int b = s0 + lane;
+      const int v = b <= ny ? run[b] : 0;
+      int x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+      }
+      if (b <= ny) {
+        run[b] = base + x - v;
+        off[b] = (unsigned)(base + x - v);
+        if (b == ny) *vbase = base + x - v;
+      }
+      base += __shfl(x, 63);
+    }
+  }
+  __syncthreads();
+  int* const zvl = d.zvl + (int64_t)part * (d.zrows + 1);
+  int* const place = reinterpret_cast<int*>(d.csr + g3_pos_off(d.tabw, d.ld)) + (int64_t)part * d.ld;
+  const int vb = *vbase;
+  for (int c0 = 0; c0 < n; c0 += NT) {
+    const int e = c0 + tid;
+    const bool valid = e < n;
+    const int key = valid ? lq[e] : 0;
+    const int b = key >> 16;
+    unsigned long long mask = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const unsigned long long bb = __ballot((b >> bit) & 1);
+      mask &= ((b >> bit) & 1) ? bb : ~bb;
+    }
+    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    if (valid && rank == 0) wc[wv * SCAN_B + b] = __popcll(mask);
+    __syncthreads();
+    if (valid) {
+      int pos = run[b] + rank;
+      for (int w2 = 0; w2 < wv; ++w2) pos += wc[w2 * SCAN_B + b];
+      const int j = (int)j_lo + e;
+      if (b < ny) mem[pos] = ((unsigned)(key & 0xffff) << 16) | (unsigned)j;
+      else zvl[1 + pos - vb] = j;
+      // the row's place for the w units' reducers (read in this launch: write-through)
+      __hip_atomic_store(place + j, b < ny ? pos : -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    for (int bb = tid; bb <= ny; bb += NT) {
+      int t = 0;
+#pragma unroll
+      for (int w2 = 0; w2 < NT / 64; ++w2) {
+        t += wc[w2 * SCAN_B + bb];
+        wc[w2 * SCAN_B + bb] = 0;
+      }
+      run[bb] += t;
+    }
+    __syncthreads();
+  }
+  const int nv = n - vb, nv8 = (nv + ZKS - 1) / ZKS * ZKS;
+  for (int v = nv + tid; v < nv8; v += NT) zvl[1 + v] = (int)j_lo;
+  if (tid == 0) zvl[0] = nv;
+  drain_stores();
+  __syncthreads();
+  if (tid == 0) publish(d.zflag + part, d.epoch);   // the places are stored
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n in [0, 4], then the raw barrier (no
@@ -1339,7 +1485,17 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
   // compiler's waitcnt pass treat every LDS read as aliasing the ring's LDS-DMA
   // writes and drain vmcnt before it (no pipelining)
   __shared__ double sm[LAT_LDS + 16];
-  const int64_t np = d.nprod, role = blockIdx.y;
+  const int64_t np = d.nprod;
+  int64_t role = blockIdx.y;
+  if (d.lat_g3) {
+    // g3: the scan units first (they wait for nothing), then producers and w units
+    if (role < d.nzu) {
+      lat_scan(d, (int)role, sm);
+      return;
+    }
+    role -= d.nzu;
+    if (role >= np + d.nwu) return;
+  }
   if (role < np) {
     inc_producer_role<VT>(d, role, sm, reinterpret_cast<int*>(sm + LAT_LDS),
                           *reinterpret_cast<unsigned*>(sm + LAT_LDS + 8));
@@ -1693,6 +1849,342 @@ __global__ __launch_bounds__(G2NT) void k_lat_gemm2_arg(const DescArg a) {
   (void)a;
   const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
   lat_gemm2<KA, VT>(descs[blockIdx.x], blockIdx.y);
+}
+
+// ---------------------------------------------------------------------------
+// g3: the second launch with its A operand built in the tile (k_lat_gemm3, the
+// default where it applies: KA = 8, 128-wide axis tables, <= LAT_SCAN_MAX rows per
+// part). The first launch then ends when w is stored (no Z units, no Z rows through
+// memory): each tile -- 4 lattice columns x (8 new points) = 32 (a, ix) rows by all
+// 128 iy columns -- sums its own Z rows
+//   Z[part][q][ix][a] = sum_{j on lattice row q, row order} fma(w[j][a] c_j, ex(px_j, ix))
+// from w and the scan units' member lists into LDS (64 KB: every part's rows at
+// once), the same operations in the same order as a Z unit, so the same bits. The K
+// loop then needs no barrier: A from LDS, the axis-table rows (B) loaded into
+// registers six stages ahead. Its sums keep the order of k_lat_gemm2's four K
+// splits -- stage g into accumulator g mod 4, then ((a0 + a1) + a2) + a3 -- so the
+// tile's T~, and with it mu, var and the new V rows, are k_lat_gemm2's bit for bit.
+// Off-lattice ("virtual") training rows are 32-row chunks of the K loop built from
+// their table rows, as the Z units do. One wave per 16 x 16 output tile (16 waves),
+// one workgroup per CU at B = 8 (32 tiles per GP).
+// ---------------------------------------------------------------------------
+constexpr int G3NT = 1024;
+constexpr int G3IX = LAT_G3IX;                   // lattice x columns per tile
+constexpr int G3R = G3IX * 8;                    // (ix, a) rows: 32
+constexpr int G3Y = 128;                         // iy columns (the whole axis)
+constexpr int G3K = 256;                         // lattice K rows at most: parts x round_up(ny, ZKS)
+constexpr int G3FW = G3IX + G3Y;                 // a new row's table columns held for the cells
+constexpr int G3ZS = G3K * G3R;                  // Zs [K][32] (the T~ tile [32][128] aliases it)
+static_assert(G3R * G3Y <= G3ZS, "the T~ tile fits Zs' place");
+static_assert(G3NT == G3R * 32, "a virtual chunk: one element per thread");
+constexpr int G3CH = G3NT;                       // members staged per chunk of the Z build
+constexpr int G3LDS = G3ZS + G3CH * 8 + G3CH / 2 + (KINC * KINC + KINC) + KINC * KINC + 2 * 128 * G3IX + 2 * 16;
+static_assert(2 * 8 * G3FW <= G3CH * 8, "the new rows' tables fit the stage's place");
+constexpr int G3D = 8;                           // K-loop stages of B in flight (a multiple of 4:
+                                                 // stage g's accumulator g % 4 is then b % 4)
+static_assert(G3K / ZKS % G3D == 0, "the K loop's padding stages fit Zs");
+
+template <class VT>
+__device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
+  constexpr int KA = 8;
+  const int k = (int)(d.N - d.n0);
+  if (k <= 0 || k > KA) return;
+  if (d.gate && *d.gate == 0) return;
+  if (tile >= d.lat_tiles) return;   // (the grid is the batch's largest)
+  __shared__ double sm[G3LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wg = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  const GridLattice lat = d.lat;
+  const int64_t ix0 = tile * G3IX;
+  const int64_t tabw = d.tabw, ld = d.ld, zrows = d.zrows, tstride = d.ld * tabw;
+  const Hyp& h = d.hp;
+  const int P = h.kind == 0 ? 1 : 2;
+  const int64_t zq8 = (lat.ny + ZKS - 1) / ZKS * ZKS;
+  const int64_t n0 = d.n0, NL = d.NL;
+  double* const Zs = sm;
+  double* const Sw = sm + G3ZS;                    // the chunk's members' c w rows [8][G3CH]
+                                                   // (then the new rows' tables Fn [2 kinds][KA][G3FW])
+  int* const Spx = reinterpret_cast<int*>(Sw + G3CH * 8);   // their axis columns (part, px)
+  double* const L22 = Sw + G3CH * 8 + G3CH / 2;   // [16][16] | z2 [16]
+  double* const Li = L22 + KINC * KINC + KINC;     // L22^-1
+  double* const AXs = Li + KINC * KINC;            // axis columns ex(px, ix0 + ixl) [parts][128][G3IX]
+  double* const amx = AXs + 2 * 128 * G3IX;        // the waves' (max, argmax)
+  double* const Fn = Sw;
+  WTRACE2(0);
+  // ---- the Z rows' inputs: the members' c w rows in list order (the w units' block
+  // reducers stored them, g3_cw_off) staged through LDS in chunks of G3CH, part 0's
+  // list [0, n0) then part 1's [0, n0 - NL) (the lists' lengths bound by their rows:
+  // no load waits for another); chunk c + 1's loads in flight while c is summed ----
+  const unsigned* const off0 = d.csr;
+  const unsigned* const off1 = d.csr + (tabw + 1 + ld);
+  const unsigned* const mem0 = off0 + tabw + 1;
+  const unsigned* const mem1 = off1 + tabw + 1;
+  const double* const cwb = reinterpret_cast<const double*>(d.csr + g3_cw_off(tabw, ld));
+  const int n0i = (int)n0, n1i = P == 2 ? (int)(n0 - NL) : 0;
+  const int nc0 = (n0i + G3CH - 1) / G3CH, nch = nc0 + (n1i + G3CH - 1) / G3CH;
+  auto ld_chunk = [&](int c, dv2 (&wq)[KA / 2], int& px) {
+    const int pt = c >= nc0 ? 1 : 0;
+    const int m = (pt ? c - nc0 : c) * G3CH + tid;
+    px = 0;
+#pragma unroll
+    for (int h2 = 0; h2 < KA / 2; ++h2) wq[h2] = dv2{0.0, 0.0};
+    if (c < nch && m < (pt ? n1i : n0i)) {   // (past a list's end: stale, never summed)
+      const GLOBAL dv2* src = reinterpret_cast<const GLOBAL dv2*>(gp(cwb) + ((int64_t)pt * ld + m) * 8);
+#pragma unroll
+      for (int h2 = 0; h2 < KA / 2; ++h2) wq[h2] = src[h2];
+      px = (int)((pt ? mem1 : mem0)[m] >> 16);
+    }
+  };
+  dv2 wn[KA / 2];
+  int pxn;
+  ld_chunk(0, wn, pxn);
+  // this thread's Z element (part, q, ixl) and its row's members [m_lo, m_hi) in its list
+  const int zpt = tid / (int)(zq8 * G3IX), zrem = tid % (int)(zq8 * G3IX);
+  const int zqq = zrem / G3IX, zix = zrem % G3IX;
+  const bool zown = zpt < P && zqq < lat.ny && ix0 + zix < lat.nx;
+  int m_lo = 0, m_hi = 0;
+  if (zown) {
+    const unsigned* const o = zpt ? off1 : off0;
+    m_lo = (int)o[zqq];
+    m_hi = (int)o[zqq + 1];
+  }
+  // ---- the cells' inputs (Fn held in registers until the stage is free) and the tile's axis columns ----
+  for (int e = tid; e < KINC * KINC + KINC; e += G3NT) {
+    const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
+    L22[e] = use ? d.l22r[e] : 0.0;
+  }
+  constexpr int FNR = (2 * KA * G3FW + G3NT - 1) / G3NT;
+  double fnr[FNR];
+#pragma unroll
+  for (int u = 0; u < FNR; ++u) {
+    const int e = tid + u * G3NT;
+    fnr[u] = 0.0;
+    if (e < 2 * KA * G3FW) {
+      const int kind2 = e / (KA * G3FW), rem = e % (KA * G3FW);
+      const int a = rem / G3FW, col = rem % G3FW;
+      const bool isx = col < G3IX;
+      const int t = 2 * kind2 + (isx ? 0 : 1);
+      const int64_t idx = isx ? ix0 + col : col - G3IX;
+      if (a < k && idx < tabw) fnr[u] = d.tab[t * tstride + (n0 + a) * tabw + idx];
+    }
+  }
+  for (int e = tid; e < P * 128 * G3IX; e += G3NT) {
+    const int pt = e / (128 * G3IX), rem = e % (128 * G3IX);
+    const int px = rem / G3IX, ixl = rem % G3IX;
+    AXs[e] = (ix0 + ixl < tabw) ? d.axt[(2 * pt) * (tabw + 1) * tabw + px * tabw + ix0 + ixl] : 0.0;
+  }
+  // ---- the tile's Z rows: thread (part, q, ixl), all 8 a, its row's members in row
+  // order: fma(c w, ex(px, ix), acc), a Z unit's operations in a Z unit's order ----
+  double zacc[KA];
+#pragma unroll
+  for (int a = 0; a < KA; ++a) zacc[a] = 0.0;
+  WTRACE2(5);
+  for (int c = 0; c < nch; ++c) {
+    dv2 wq[KA / 2];
+#pragma unroll
+    for (int h2 = 0; h2 < KA / 2; ++h2) wq[h2] = wn[h2];
+    const int pxc = pxn;
+    ld_chunk(c + 1, wn, pxn);
+    asm volatile("" ::: "memory");   // (the next chunk's loads stay here, ahead of this chunk's work)
+    __syncthreads();   // the previous chunk is summed (the first: L22, AXs stored)
+#pragma unroll
+    for (int a = 0; a < KA; ++a) Sw[a * G3CH + tid] = a & 1 ? wq[a >> 1].y : wq[a >> 1].x;
+    Spx[tid] = pxc;
+    __syncthreads();
+    const int pt = c >= nc0 ? 1 : 0, c0 = (pt ? c - nc0 : c) * G3CH;
+    if (zpt == pt) {
+      const int mb = m_lo > c0 ? m_lo : c0, me = m_hi < c0 + G3CH ? m_hi : c0 + G3CH;
+      for (int mm = mb; mm < me; ++mm) {
+        const double ex = AXs[(pt * 128 + Spx[mm - c0]) * G3IX + zix];
+        const double* const cw = Sw + (mm - c0);
+#pragma unroll
+        for (int a = 0; a < KA; ++a) zacc[a] = __builtin_fma(cw[a * G3CH], ex, zacc[a]);
+      }
+    }
+  }
+  WTRACE2(1);
+  if (tid < P * zq8 * G3IX) {
+    double* const zr = Zs + (int64_t)(zpt * zq8 + zqq) * G3R + zix * KA;
+#pragma unroll
+    for (int a = 0; a < KA; ++a) zr[a] = zacc[a];
+  }
+  {
+    // the K loop's padding stages: zero A rows
+    const int z0 = (int)(P * zq8) * G3R;
+    const int z1 = (int)((P * zq8 / ZKS + G3D - 1) / G3D * G3D) * ZKS * G3R;
+    for (int e = z0 + tid; e < z1; e += G3NT) Zs[e] = 0.0;
+  }
+  __syncthreads();   // Zs complete; the stage is free: the new rows' tables take it
+#pragma unroll
+  for (int u = 0; u < FNR; ++u)
+    if (tid + u * G3NT < 2 * KA * G3FW) Fn[tid + u * G3NT] = fnr[u];
+  // the cells use L22^-1's diagonal only: 1 / L22[a][a], the value the forward
+  // substitution of k_lat_gemm2 puts there (t = 1 exactly at i = c)
+  if (tid < KINC) Li[tid * KINC + tid] = tid < k ? 1.0 / L22[tid * KINC + tid] : 0.0;
+  // ---- the K loop: wave wg -> rows 16 rt, columns 16 ct; stage g into acc4[g % 4] ----
+  const int rt = wg >> 3, ct = wg & 7;
+  const int i0 = 16 * rt, iyc = 16 * ct + r;
+  d4 acc4[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc4[s] = d4{0.0, 0.0, 0.0, 0.0};
+  const int NA = (int)(P * zq8 / ZKS);   // lattice stages (8 K rows each)
+  const int NAP = (NA + G3D - 1) / G3D * G3D;   // padded with zero A rows (no branch in the loop)
+  const double* const axb = d.axt + tabw * (tabw + 1);   // part pt's y table: + 2 pt (tabw + 1) tabw
+  static_assert(G3D % 4 == 0, "stage g's accumulator is b % 4");
+  // lane (r, q)'s B element of K row kr + q (kr = 8 g + 4 e): part 1's rows continue part 0's
+  const double* const bb0 = axb + (int64_t)q * tabw + iyc;
+  const double* const bb1 = axb + 2 * (tabw + 1) * tabw + (int64_t)q * tabw + iyc - zq8 * tabw;
+  auto b_ld = [&](int g, int e) -> double {
+    const int kr = g < NA ? ZKS * g + 4 * e : 0;   // (the padding stages: any finite row, times A = 0)
+    return gp((kr >= zq8 ? bb1 : bb0) + (int64_t)kr * tabw)[0];
+  };
+  double bq[G3D][2];
+#pragma unroll
+  for (int b = 0; b < G3D; ++b) {
+    bq[b][0] = b_ld(b, 0);
+    bq[b][1] = b_ld(b, 1);
+    asm volatile("" ::: "memory");   // (in the loop's order: its waits count the same loads)
+  }
+  for (int g0 = 0; g0 < NAP; g0 += G3D) {
+#pragma unroll
+    for (int b = 0; b < G3D; ++b) {
+      const int g = g0 + b;
+      const double a0 = Zs[(ZKS * g + q) * G3R + i0 + r];
+      const double a1 = Zs[(ZKS * g + 4 + q) * G3R + i0 + r];
+      acc4[b & 3] = mfma(a0, bq[b][0], acc4[b & 3]);
+      acc4[b & 3] = mfma(a1, bq[b][1], acc4[b & 3]);
+      bq[b][0] = b_ld(g + G3D, 0);
+      bq[b][1] = b_ld(g + G3D, 1);
+      asm volatile("" ::: "memory");   // (issued here: G3D stages ahead of their use)
+    }
+  }
+  // ---- the virtual rows: chunks of 32 K rows (4 stages) built from their table rows ----
+  int nvr[2] = {0, 0}, nvs[2] = {0, 0};
+  for (int pt = 0; pt < P; ++pt) {
+    nvr[pt] = d.zvl[pt * (zrows + 1)];
+    nvs[pt] = (nvr[pt] + ZKS - 1) / ZKS;
+  }
+  const int NV = nvs[0] + nvs[1];
+  for (int c0 = 0; c0 < NV; c0 += 4) {
+    __syncthreads();   // Zs is free (every wave's reads of the previous stages are done)
+    {
+      const int kr = tid / G3R, col = tid % G3R;   // one element per thread
+      const int gs = c0 + kr / ZKS;
+      double v = 0.0;
+      if (gs < NV) {
+        const int pt = gs < nvs[0] ? 0 : 1;
+        const int vv = ZKS * (gs - (pt ? nvs[0] : 0)) + kr % ZKS;
+        const int ixl = col / KA, a = col % KA;
+        if (vv < nvr[pt] && ix0 + ixl < lat.nx) {
+          const int64_t j = d.zvl[pt * (zrows + 1) + 1 + vv];
+          v = d.wv[j * KINC + a] * d.tab[(2 * pt) * tstride + j * tabw + ix0 + ixl];
+        }
+      }
+      Zs[kr * G3R + col] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {   // stage c0 + s: accumulator (c0 + s) % 4 = s
+      const int gs = c0 + s;
+      if (gs < NV) {
+        const int pt = gs < nvs[0] ? 0 : 1;
+        double bv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int vv = ZKS * (gs - (pt ? nvs[0] : 0)) + 4 * e + q;
+          const int64_t j = d.zvl[pt * (zrows + 1) + 1 + vv];
+          bv[e] = d.tab[(2 * pt + 1) * tstride + j * tabw + iyc];
+        }
+        const double a0 = Zs[(ZKS * s + q) * G3R + i0 + r];
+        const double a1 = Zs[(ZKS * s + 4 + q) * G3R + i0 + r];
+        acc4[s] = mfma(a0, bv[0], acc4[s]);
+        acc4[s] = mfma(a1, bv[1], acc4[s]);
+      }
+    }
+  }
+  __syncthreads();   // every Zs read is done: the place becomes T~
+  WTRACE2(2);
+  double* const Tt = sm;   // [32 (ixl, a)][128 iy]
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    double t = acc4[0][v] + acc4[1][v];
+    t = t + acc4[2][v];
+    t = t + acc4[3][v];
+    Tt[(i0 + q + 4 * v) * G3Y + iyc] = t;
+  }
+  __syncthreads();
+  WTRACE2(3);
+  // ---- cells: thread t < 4 x 128 finishes cell (ix0 + t / 128, t % 128) ----
+  double bv = -__builtin_inf();
+  int64_t bi = INT64_MAX;
+  if (tid < G3IX * G3Y) {
+    const int ixl = tid / G3Y, iyl = tid % G3Y;
+    const int64_t ix = ix0 + ixl, iy = iyl;
+    if (ix < lat.nx && iy < lat.ny) {
+      const int64_t c = ix * lat.sx + iy * lat.sy;
+      const double cov = d.rvar_in[c], com = d.rmu_in[c];
+      VT* const vt = const_cast<VT*>(vres_ptr<VT>(d)) + (c / PBM) * d.vld * PBM + (c % PBM);
+      const double* const Tc = Tt + (ixl * KA) * G3Y + iyl;
+      const int iyc2 = G3IX + iyl;
+      double vn[KA];
+      double vs = 0.0, ms = 0.0;
+#pragma unroll
+      for (int a = 0; a < KA; ++a) {
+        vn[a] = 0.0;
+        if (a < k) {
+          const double* fL = Fn + a * G3FW;
+          const double* fH = Fn + (KA + a) * G3FW;
+          const double pn = fL[ixl] * fL[iyc2] + fH[ixl] * fH[iyc2];
+          double t = pn - Tc[a * G3Y];
+#pragma unroll
+          for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
+          vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
+          vs += vn[a] * vn[a];
+          ms += vn[a] * L22[KINC * KINC + a];
+          __hip_atomic_store(vt + (n0 + a) * PBM, (VT)vn[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      const double vc = cov - vs;
+      const double mc = com + ms;
+      __hip_atomic_store(d.mu + c, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.var + c, vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d.rmu) {
+        __hip_atomic_store(d.rmu + c, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.rvar + c, vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      argmax_pair(bv, bi, vc, c);
+    }
+  }
+  WTRACE2(6);
+  if (d.vmax || d.vargmax || d.status_host) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+    int64_t* const ami = reinterpret_cast<int64_t*>(amx);
+    if (lane == 0) {
+      amx[2 * wg] = bv;
+      ami[2 * wg + 1] = bi;
+    }
+    __syncthreads();
+    if (wg == 0) {
+      bv = amx[0];
+      bi = ami[1];
+      for (int ww = 1; ww < G3NT / 64; ++ww) argmax_pair(bv, bi, amx[2 * ww], ami[2 * ww + 1]);
+      var_argmax_group(d, bv, bi, tile, d.lat_tiles);
+    }
+  }
+  WTRACE2(4);
+}
+
+template <class VT>
+__global__ __launch_bounds__(G3NT) void k_lat_gemm3(const GPDesc* __restrict__ descs) {
+  lat_gemm3<VT>(descs[blockIdx.x], blockIdx.y);
+}
+template <class VT>
+__global__ __launch_bounds__(G3NT) void k_lat_gemm3_arg(const DescArg a) {
+  (void)a;
+  const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
+  lat_gemm3<VT>(descs[blockIdx.x], blockIdx.y);
 }
 
 // The separable tables of rows [tab_lo, n0) (full-path refresh; the step itself
