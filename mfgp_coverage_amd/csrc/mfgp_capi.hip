@@ -651,6 +651,13 @@ bool lat_eligible(const mfgp_model* m, int64_t n0) {
 }
 // F, the tables, w and the flags at the model's leading dimension (contents kept
 // across capacity growth: ensure_cap moves them)
+// Small buffers that every GEMM workgroup of the lattice step reads (the axis
+// tables, the g3 lists): whole 2 MiB units, so that they sit in one large page
+hipError_t hip_malloc_2m(void** p, size_t bytes) {
+  const size_t unit = size_t(2) << 20;
+  return hipMalloc(p, (bytes + unit - 1) / unit * unit);
+}
+
 int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
   hipStream_t s = m->ctx->stream;
   const int64_t ld = m->ld, tabw = lat_tabw(m);
@@ -718,7 +725,7 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     HIP_TRY(hipStreamSynchronize(s));
     if (m->axt) HIP_TRY(hipFree(m->axt));
     m->axt = nullptr;
-    HIP_TRY(hipMalloc(&m->axt, sizeof(double) * 4 * (tabw + 1) * tabw));
+    HIP_TRY(hip_malloc_2m(reinterpret_cast<void**>(&m->axt), sizeof(double) * 4 * (tabw + 1) * tabw));
     m->axt_w = tabw;
     m->axt_gen = UINT64_MAX;   // build before use
   }
@@ -745,7 +752,7 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     if (m->csr) HIP_TRY(hipFree(m->csr));
     m->csr = nullptr;
     m->csr_n = g3_bytes(tabw, ld);
-    HIP_TRY(hipMalloc(&m->csr, m->csr_n));
+    HIP_TRY(hip_malloc_2m(reinterpret_cast<void**>(&m->csr), m->csr_n));
   }
   if (!m->ldone) {
     HIP_TRY(hipMalloc(&m->ldone, sizeof(unsigned) * 4));

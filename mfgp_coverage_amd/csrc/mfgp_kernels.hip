@@ -37,6 +37,17 @@ __device__ long long* g_stamps;
   do {            \
   } while (0)
 #endif
+// k_lat_gemm3's grid: (GPs, tiles); a diagnostic build swaps it to (tiles, GPs) so
+// that a GP's tiles spread over every XCD (MFGP_G3_SWAP; k_lat_gemm2 keeps (GPs, tiles))
+#ifdef MFGP_G3_SWAP
+#define G3_GP blockIdx.y
+#define G3_TILE blockIdx.x
+#define G3_NGP gridDim.y
+#else
+#define G3_GP blockIdx.x
+#define G3_TILE blockIdx.y
+#define G3_NGP gridDim.x
+#endif
 // k_inc_stream timeline stamps (GP 0 only; diagnostic builds)
 #ifdef MFGP_STAMPS
 #define FSTAMP(id)                                                                                 \
@@ -55,11 +66,11 @@ __device__ long long* g_stamps;
                  (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                                \
     }                                                                                                \
   } while (0)
-// the lattice step's second launch (k_lat_gemm2): its workgroups at role 1024 + tile
+// the lattice step's second launch (k_lat_gemm2/3): its workgroups at role 1024 + tile
 #define WTRACE2(slot)                                                                                \
   do {                                                                                               \
     if (threadIdx.x == 0) {                                                                          \
-      long long* wt_ = g_stamps + 64 + 8 * ((1024 + blockIdx.y) * gridDim.x + blockIdx.x);           \
+      long long* wt_ = g_stamps + 64 + 8 * ((1024 + G3_TILE) * G3_NGP + G3_GP);                       \
       wt_[slot] = __builtin_amdgcn_s_memrealtime();                                                  \
       if ((slot) == 0)                                                                               \
         wt_[7] = ((long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |                       \
@@ -2726,8 +2737,13 @@ hipError_t launch_lat_gemm2_arg(const GPDesc* h, int count, int64_t max_tiles, i
   else hipLaunchKernelGGL((k_lat_gemm2_arg<16, double>), g, dim3(G2NT), 0, s, a);
   return hipGetLastError();
 }
+#ifdef MFGP_G3_SWAP
+#define G3_GRID(count, tiles) dim3((unsigned)(tiles), (count))
+#else
+#define G3_GRID(count, tiles) dim3((count), (unsigned)(tiles))
+#endif
 hipError_t launch_lat_gemm3(const GPDesc* d, int count, int64_t max_tiles, int vf32, hipStream_t s) {
-  const dim3 g(count, (unsigned)max_tiles);
+  const dim3 g = G3_GRID(count, max_tiles);
   if (vf32) hipLaunchKernelGGL((k_lat_gemm3<float>), g, dim3(G3NT), 0, s, d);
   else hipLaunchKernelGGL((k_lat_gemm3<double>), g, dim3(G3NT), 0, s, d);
   return hipGetLastError();
@@ -2736,7 +2752,7 @@ hipError_t launch_lat_gemm3_arg(const GPDesc* h, int count, int64_t max_tiles, i
   if (count < 1 || count > DESC_ARG_MAX) return hipErrorInvalidValue;
   DescArg a;
   std::memcpy(a.d, h, sizeof(GPDesc) * count);
-  const dim3 g(count, (unsigned)max_tiles);
+  const dim3 g = G3_GRID(count, max_tiles);
   if (vf32) hipLaunchKernelGGL((k_lat_gemm3_arg<float>), g, dim3(G3NT), 0, s, a);
   else hipLaunchKernelGGL((k_lat_gemm3_arg<double>), g, dim3(G3NT), 0, s, a);
   return hipGetLastError();

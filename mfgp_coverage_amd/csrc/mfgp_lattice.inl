@@ -1878,11 +1878,14 @@ constexpr int G3ZS = G3K * G3R;                  // Zs [K][32] (the T~ tile [32]
 static_assert(G3R * G3Y <= G3ZS, "the T~ tile fits Zs' place");
 static_assert(G3NT == G3R * 32, "a virtual chunk: one element per thread");
 constexpr int G3CH = G3NT;                       // members staged per chunk of the Z build
-constexpr int G3LDS = G3ZS + G3CH * 8 + G3CH / 2 + (KINC * KINC + KINC) + KINC * KINC + 2 * 128 * G3IX + 2 * 16;
-static_assert(2 * 8 * G3FW <= G3CH * 8, "the new rows' tables fit the stage's place");
-constexpr int G3D = 8;                           // K-loop stages of B in flight (a multiple of 4:
-                                                 // stage g's accumulator g % 4 is then b % 4)
-static_assert(G3K / ZKS % G3D == 0, "the K loop's padding stages fit Zs");
+constexpr int G3LDS = G3ZS + G3CH * 8 + (KINC * KINC + KINC) + KINC * KINC + 2 * 128 * G3IX + 2 * 16;
+static_assert(G3IX * G3CH <= G3ZS, "the staged axis values fit Zs' place");
+constexpr int G3D = 8;                           // a wave's K-loop stages of B in flight (even:
+                                                 // its w-th stage's accumulator is then b % 2)
+constexpr int G3P = 2 * G3D;                     // the lattice stages, padded to a multiple of this
+static_assert(G3K / ZKS % G3P == 0, "the K loop's padding stages fit Zs");
+static_assert(G3R * G3Y + 2 * 8 * G3FW <= G3ZS, "T~ and the new rows' tables share Zs' place");
+static_assert(2 * G3R * G3Y <= G3CH * 8, "the K splits' sums fit the stage's place");
 
 template <class VT>
 __device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
@@ -1904,13 +1907,14 @@ __device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
   const int64_t n0 = d.n0, NL = d.NL;
   double* const Zs = sm;
   double* const Sw = sm + G3ZS;                    // the chunk's members' c w rows [8][G3CH]
-                                                   // (then the new rows' tables Fn [2 kinds][KA][G3FW])
-  int* const Spx = reinterpret_cast<int*>(Sw + G3CH * 8);   // their axis columns (part, px)
-  double* const L22 = Sw + G3CH * 8 + G3CH / 2;   // [16][16] | z2 [16]
+                                                   // (then the K splits' sums X23)
+  double* const Sex = Zs;                          // their axis values ex(px, ix0 + ixl) [G3IX][G3CH]
+                                                   // (Zs' place is free until the Z rows are stored)
+  double* const L22 = Sw + G3CH * 8;               // [16][16] | z2 [16]
   double* const Li = L22 + KINC * KINC + KINC;     // L22^-1
   double* const AXs = Li + KINC * KINC;            // axis columns ex(px, ix0 + ixl) [parts][128][G3IX]
   double* const amx = AXs + 2 * 128 * G3IX;        // the waves' (max, argmax)
-  double* const Fn = Sw;
+  double* const Fn = Zs + G3R * G3Y;               // the new rows' tables [2 kinds][KA][G3FW] (after the K loop)
   WTRACE2(0);
   // ---- the Z rows' inputs: the members' c w rows in list order (the w units' block
   // reducers stored them, g3_cw_off) staged through LDS in chunks of G3CH, part 0's
@@ -1988,22 +1992,24 @@ __device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
     ld_chunk(c + 1, wn, pxn);
     asm volatile("" ::: "memory");   // (the next chunk's loads stay here, ahead of this chunk's work)
     __syncthreads();   // the previous chunk is summed (the first: L22, AXs stored)
+    const int pt = c >= nc0 ? 1 : 0, c0 = (pt ? c - nc0 : c) * G3CH;
 #pragma unroll
     for (int a = 0; a < KA; ++a) Sw[a * G3CH + tid] = a & 1 ? wq[a >> 1].y : wq[a >> 1].x;
-    Spx[tid] = pxc;
+#pragma unroll
+    for (int ixl = 0; ixl < G3IX; ++ixl) Sex[ixl * G3CH + tid] = AXs[(pt * 128 + pxc) * G3IX + ixl];
     __syncthreads();
-    const int pt = c >= nc0 ? 1 : 0, c0 = (pt ? c - nc0 : c) * G3CH;
     if (zpt == pt) {
       const int mb = m_lo > c0 ? m_lo : c0, me = m_hi < c0 + G3CH ? m_hi : c0 + G3CH;
+      const double* const ex = Sex + zix * G3CH - c0;
+      const double* const cw = Sw - c0;
+#pragma unroll 4
       for (int mm = mb; mm < me; ++mm) {
-        const double ex = AXs[(pt * 128 + Spx[mm - c0]) * G3IX + zix];
-        const double* const cw = Sw + (mm - c0);
 #pragma unroll
-        for (int a = 0; a < KA; ++a) zacc[a] = __builtin_fma(cw[a * G3CH], ex, zacc[a]);
+        for (int a = 0; a < KA; ++a) zacc[a] = __builtin_fma(cw[a * G3CH + mm], ex[mm], zacc[a]);
       }
     }
   }
-  WTRACE2(1);
+  __syncthreads();   // the last chunk is summed (its axis values sit in Zs' place)
   if (tid < P * zq8 * G3IX) {
     double* const zr = Zs + (int64_t)(zpt * zq8 + zqq) * G3R + zix * KA;
 #pragma unroll
@@ -2012,51 +2018,59 @@ __device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
   {
     // the K loop's padding stages: zero A rows
     const int z0 = (int)(P * zq8) * G3R;
-    const int z1 = (int)((P * zq8 / ZKS + G3D - 1) / G3D * G3D) * ZKS * G3R;
+    const int z1 = (int)((P * zq8 / ZKS + G3P - 1) / G3P * G3P) * ZKS * G3R;
     for (int e = z0 + tid; e < z1; e += G3NT) Zs[e] = 0.0;
   }
-  __syncthreads();   // Zs complete; the stage is free: the new rows' tables take it
-#pragma unroll
-  for (int u = 0; u < FNR; ++u)
-    if (tid + u * G3NT < 2 * KA * G3FW) Fn[tid + u * G3NT] = fnr[u];
+  __syncthreads();   // Zs complete
+  WTRACE2(1);
   // the cells use L22^-1's diagonal only: 1 / L22[a][a], the value the forward
   // substitution of k_lat_gemm2 puts there (t = 1 exactly at i = c)
   if (tid < KINC) Li[tid * KINC + tid] = tid < k ? 1.0 / L22[tid * KINC + tid] : 0.0;
-  // ---- the K loop: wave wg -> rows 16 rt, columns 16 ct; stage g into acc4[g % 4] ----
-  const int rt = wg >> 3, ct = wg & 7;
-  const int i0 = 16 * rt, iyc = 16 * ct + r;
-  d4 acc4[4];
+  // ---- the K loop: wave (kh, ct) -> both 16-row tiles, columns 16 ct, the stages g
+  // with g % 4 in {2 kh, 2 kh + 1} into acc[rt][g % 2] -- k_lat_gemm2's four split
+  // sums, two per wave -- so each B element is loaded once per workgroup ----
+  const int kh = wg >> 3, ct = wg & 7;
+  const int iyc = 16 * ct + r;
+  d4 acc[2][2];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) acc4[s] = d4{0.0, 0.0, 0.0, 0.0};
-  const int NA = (int)(P * zq8 / ZKS);   // lattice stages (8 K rows each)
-  const int NAP = (NA + G3D - 1) / G3D * G3D;   // padded with zero A rows (no branch in the loop)
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) acc[rt][s2] = d4{0.0, 0.0, 0.0, 0.0};
+  const int NA = (int)(P * zq8 / ZKS);          // lattice stages (8 K rows each)
+  const int NAP = (NA + G3P - 1) / G3P * G3P;   // padded with zero A rows (no branch in the loop)
   const double* const axb = d.axt + tabw * (tabw + 1);   // part pt's y table: + 2 pt (tabw + 1) tabw
-  static_assert(G3D % 4 == 0, "stage g's accumulator is b % 4");
   // lane (r, q)'s B element of K row kr + q (kr = 8 g + 4 e): part 1's rows continue part 0's
   const double* const bb0 = axb + (int64_t)q * tabw + iyc;
   const double* const bb1 = axb + 2 * (tabw + 1) * tabw + (int64_t)q * tabw + iyc - zq8 * tabw;
   auto b_ld = [&](int g, int e) -> double {
     const int kr = g < NA ? ZKS * g + 4 * e : 0;   // (the padding stages: any finite row, times A = 0)
+#ifdef MFGP_DIAG_G3NOB   // diagnostic build: B without its loads (timing only, wrong results)
+    return 1.0 + 1e-3 * (kr + q);
+#endif
     return gp((kr >= zq8 ? bb1 : bb0) + (int64_t)kr * tabw)[0];
   };
+  auto gw = [&](int w) { return 4 * (w >> 1) + 2 * kh + (w & 1); };   // this wave's w-th stage
   double bq[G3D][2];
 #pragma unroll
   for (int b = 0; b < G3D; ++b) {
-    bq[b][0] = b_ld(b, 0);
-    bq[b][1] = b_ld(b, 1);
+    bq[b][0] = b_ld(gw(b), 0);
+    bq[b][1] = b_ld(gw(b), 1);
     asm volatile("" ::: "memory");   // (in the loop's order: its waits count the same loads)
   }
-  for (int g0 = 0; g0 < NAP; g0 += G3D) {
+  for (int w0 = 0; w0 < NAP / 2; w0 += G3D) {
 #pragma unroll
     for (int b = 0; b < G3D; ++b) {
-      const int g = g0 + b;
-      const double a0 = Zs[(ZKS * g + q) * G3R + i0 + r];
-      const double a1 = Zs[(ZKS * g + 4 + q) * G3R + i0 + r];
-      acc4[b & 3] = mfma(a0, bq[b][0], acc4[b & 3]);
-      acc4[b & 3] = mfma(a1, bq[b][1], acc4[b & 3]);
-      bq[b][0] = b_ld(g + G3D, 0);
-      bq[b][1] = b_ld(g + G3D, 1);
-      asm volatile("" ::: "memory");   // (issued here: G3D stages ahead of their use)
+      const int g = gw(w0 + b);
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const double a0 = Zs[(ZKS * g + q) * G3R + 16 * rt + r];
+        const double a1 = Zs[(ZKS * g + 4 + q) * G3R + 16 * rt + r];
+        acc[rt][b & 1] = mfma(a0, bq[b][0], acc[rt][b & 1]);
+        acc[rt][b & 1] = mfma(a1, bq[b][1], acc[rt][b & 1]);
+      }
+      bq[b][0] = b_ld(gw(w0 + b + G3D), 0);
+      bq[b][1] = b_ld(gw(w0 + b + G3D), 1);
+      asm volatile("" ::: "memory");   // (issued here: G3D of this wave's stages ahead of their use)
     }
   }
   // ---- the virtual rows: chunks of 32 K rows (4 stages) built from their table rows ----
@@ -2085,8 +2099,8 @@ __device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
     }
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {   // stage c0 + s: accumulator (c0 + s) % 4 = s
-      const int gs = c0 + s;
+    for (int s2 = 0; s2 < 2; ++s2) {   // stage c0 + s (s = 2 kh + s2): accumulator (c0 + s) % 4 = s
+      const int s = 2 * kh + s2, gs = c0 + s;
       if (gs < NV) {
         const int pt = gs < nvs[0] ? 0 : 1;
         double bv[2];
@@ -2096,22 +2110,44 @@ __device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
           const int64_t j = d.zvl[pt * (zrows + 1) + 1 + vv];
           bv[e] = d.tab[(2 * pt + 1) * tstride + j * tabw + iyc];
         }
-        const double a0 = Zs[(ZKS * s + q) * G3R + i0 + r];
-        const double a1 = Zs[(ZKS * s + 4 + q) * G3R + i0 + r];
-        acc4[s] = mfma(a0, bv[0], acc4[s]);
-        acc4[s] = mfma(a1, bv[1], acc4[s]);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const double a0 = Zs[(ZKS * s + q) * G3R + 16 * rt + r];
+          const double a1 = Zs[(ZKS * s + 4 + q) * G3R + 16 * rt + r];
+          acc[rt][s2] = mfma(a0, bv[0], acc[rt][s2]);
+          acc[rt][s2] = mfma(a1, bv[1], acc[rt][s2]);
+        }
       }
     }
   }
-  __syncthreads();   // every Zs read is done: the place becomes T~
+  __syncthreads();   // every Zs read is done: the place becomes T~ and the new rows' tables
   WTRACE2(2);
-  double* const Tt = sm;   // [32 (ixl, a)][128 iy]
+  // the sums of splits 2 and 3 (waves kh = 1) meet those of 0 and 1: ((p0 + p1) + p2) + p3
+  double* const X23 = Sw;   // [2][32][128]
+  if (kh == 1) {
 #pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    double t = acc4[0][v] + acc4[1][v];
-    t = t + acc4[2][v];
-    t = t + acc4[3][v];
-    Tt[(i0 + q + 4 * v) * G3Y + iyc] = t;
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) X23[(s2 * G3R + 16 * rt + q + 4 * v) * G3Y + iyc] = acc[rt][s2][v];
+  }
+#pragma unroll
+  for (int u = 0; u < FNR; ++u)
+    if (tid + u * G3NT < 2 * KA * G3FW) Fn[tid + u * G3NT] = fnr[u];
+  __syncthreads();
+  double* const Tt = sm;   // [32 (ixl, a)][128 iy]
+  if (kh == 0) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = 16 * rt + q + 4 * v;
+        double t = acc[rt][0][v] + acc[rt][1][v];
+        t = t + X23[row * G3Y + iyc];
+        t = t + X23[(G3R + row) * G3Y + iyc];
+        Tt[row * G3Y + iyc] = t;
+      }
   }
   __syncthreads();
   WTRACE2(3);
@@ -2178,13 +2214,13 @@ __device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
 
 template <class VT>
 __global__ __launch_bounds__(G3NT) void k_lat_gemm3(const GPDesc* __restrict__ descs) {
-  lat_gemm3<VT>(descs[blockIdx.x], blockIdx.y);
+  lat_gemm3<VT>(descs[G3_GP], G3_TILE);
 }
 template <class VT>
 __global__ __launch_bounds__(G3NT) void k_lat_gemm3_arg(const DescArg a) {
   (void)a;
   const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
-  lat_gemm3<VT>(descs[blockIdx.x], blockIdx.y);
+  lat_gemm3<VT>(descs[G3_GP], G3_TILE);
 }
 
 // The separable tables of rows [tab_lo, n0) (full-path refresh; the step itself

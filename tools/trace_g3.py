@@ -16,7 +16,8 @@ T = 12
 NH0 = NH - k
 M = G * G
 hyp = synthetic.HYP["australia8_mf"]
-wls = [synthetic.Workload(G, NL, NH0, k, T, seed=s) for s in range(B)]
+SEEDS = [int(v) for v in os.environ.get("TRACE_SEEDS", ",".join(str(s) for s in range(B))).split(",")]
+wls = [synthetic.Workload(G, NL, NH0, k, T, seed=SEEDS[s]) for s in range(B)]
 dev = torch.device("cuda", 0)
 NWG = B * 2048
 st = torch.zeros(64 + 8 * NWG + 64, dtype=torch.int64, device=dev)
@@ -46,6 +47,7 @@ for s in range(T):
                               asynchronous=True)
 ctx.synchronize()
 print(models[0].stats())
+CHECK = os.environ.get("TRACE_NOCHECK") is None
 raw = st.cpu().numpy()[64:64 + 8 * NWG].reshape(NWG, 8)
 tr = raw[:, :7].astype(np.float64)
 used = tr[:, 0] > 0
@@ -58,6 +60,18 @@ gm = (role >= 1024) & used
 print(f"B={B}: launch-1 WGs {l1.sum()}, last stamp {np.nanmax(tr[l1]):.1f}; gemm WGs {gm.sum()}; percentiles 0/10/50/90/100 us")
 for sl in (0, 5, 1, 2, 3, 6, 4):
     print(f"  gemm slot {sl}: {q(tr[gm, sl])}")
-print(f"  prologue (5-0): {q(tr[gm, 5] - tr[gm, 0])}; chunks (1-5): {q(tr[gm, 1] - tr[gm, 5])}")
+print(f"  prologue (5-0): {q(tr[gm, 5] - tr[gm, 0])}; chunks + Z rows (1-5): {q(tr[gm, 1] - tr[gm, 5])}")
 print(f"  K loop (2-1): {q(tr[gm, 2] - tr[gm, 1])}")
 print(f"  T~ (3-2): {q(tr[gm, 3] - tr[gm, 2])}; cells (6-3): {q(tr[gm, 6] - tr[gm, 3])}; argmax (4-6): {q(tr[gm, 4] - tr[gm, 6])}")
+# K-loop duration by XCD, by GP and by tile (which workgroups are slow)
+hw = raw[:, 7]
+xcc = (hw >> 32) & 0xF
+gp_ = np.arange(NWG) % B
+tile = role - 1024
+dur = tr[:, 2] - tr[:, 1]
+for name, key in (("xcc", xcc), ("gp", gp_)):
+    print(f"  K loop by {name}:", {int(v): round(float(np.nanmedian(dur[gm & (key == v)])), 1) for v in np.unique(key[gm])})
+print("  K loop by tile (median over GPs):", [round(float(np.nanmedian(dur[gm & (tile == t)])), 1) for t in range(32)])
+cu = ((hw >> 32) & 0xF) * 1024 + ((hw >> 13) & 0x7) * 64 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xF)
+ucu, cnt = np.unique(cu[gm], return_counts=True)
+print("  gemm WGs per CU:", dict(zip(*np.unique(cnt, return_counts=True))))
