@@ -87,9 +87,14 @@ def voronoi_bounded(points, bounding_box):
     return BoundedVoronoi(vor.vertices, regions, c)
 
 
+def _roll1(a):
+    """np.roll(a, 1) of a 1-D array (the same array, built without np.roll's overhead)."""
+    return np.concatenate((a[-1:], a[:-1]))
+
+
 def poly_area(x, y):
     """sim:127-136 (Shoelace)."""
-    return 0.5 * np.abs(np.dot(x, np.roll(y, 1)) - np.dot(y, np.roll(x, 1)))
+    return 0.5 * np.abs(np.dot(x, _roll1(y)) - np.dot(y, _roll1(x)))
 
 
 def todescato_prob(max_var_t, max_var_0):
@@ -146,9 +151,29 @@ def _prior_arrays(prior):
     return np.empty([0, 2]), np.empty([0, 1])
 
 
-def _sample(truth_arr, x_sample, streams, sigma_n):
+class TruthIndex:
+    """The rows of ``truth_arr`` by exact (x, y): the selection sim:874-877 makes
+    with ``(truth_arr[:, 0] == x) & (truth_arr[:, 1] == y)`` over every row (the
+    same rows in the same order: float keys compare as ``==`` does, 0.0 and -0.0
+    alike), looked up instead of scanned."""
+
+    def __init__(self, truth_arr):
+        self.rows = {}
+        for i, (x, y) in enumerate(zip(truth_arr[:, 0].tolist(), truth_arr[:, 1].tolist())):
+            self.rows.setdefault((x, y), []).append(i)
+        self.none = np.empty(0, dtype=np.int64)
+
+    def __call__(self, x, y):
+        r = self.rows.get((float(x), float(y)))
+        return self.none if r is None else np.asarray(r, dtype=np.int64)
+
+
+def _sample(truth_arr, x_sample, streams, sigma_n, index=None):
     """sim:874-877: the truth at the agent's grid cell plus noise."""
-    sample_idx = np.logical_and(truth_arr[:, 0] == x_sample[0], truth_arr[:, 1] == x_sample[1])
+    if index is None:
+        sample_idx = np.logical_and(truth_arr[:, 0] == x_sample[0], truth_arr[:, 1] == x_sample[1])
+    else:
+        sample_idx = index(x_sample[0], x_sample[1])
     return truth_arr[sample_idx, 2] + streams.sample_noise(sigma_n)
 
 
@@ -222,6 +247,9 @@ def simulate(algo, sim_num, iterations, agents, truth_arr, sigma_n, prior, hyp, 
 
     # 1-3) the empty model's max variance: the normalising constant (sim:827-843)
     truth_arr = np.asarray(truth_arr, dtype=np.float64)
+    tindex = TruthIndex(truth_arr)
+    grid_lo = np.array([x_star[:, 0].min(), x_star[:, 1].min()])   # (the centroids' clamp, sim:276-281)
+    grid_hi = np.array([x_star[:, 0].max(), x_star[:, 1].max()])
     model = init(None)
     x_star = truth_arr[:, [0, 1]]
     bounding_box = np.array([np.amin(x_star[:, 0]), np.amax(x_star[:, 0]),
@@ -248,7 +276,7 @@ def simulate(algo, sim_num, iterations, agents, truth_arr, sigma_n, prior, hyp, 
         for i in range(agents):
             if explore_t[i] == 1:
                 x_sample = positions[i, :]
-                y_sample = _sample(truth_arr, x_sample, streams, sigma_n)
+                y_sample = _sample(truth_arr, x_sample, streams, sigma_n, tindex)
                 x_new = np.vstack((x_new, x_sample))
                 y_new = np.vstack((y_new, y_sample))
                 id_new = np.vstack((id_new, i))
@@ -335,6 +363,9 @@ def run_lockstep(algo, sim_nums, iterations, agents, truth_arr, sigma_n, prior, 
                              np.amin(x_star[:, 1]), np.amax(x_star[:, 1])])
     streams = [SeedStreams(s, key) for s in sims]
     positions = [st.start_positions(agents) for st in streams]
+    tindex = TruthIndex(truth_arr)
+    grid_lo = np.array([x_star[:, 0].min(), x_star[:, 1].min()])   # (the centroids' clamp, sim:276-281)
+    grid_hi = np.array([x_star[:, 0].max(), x_star[:, 1].max()])
     e2, e1 = np.empty((0, 2)), np.empty(0)
     st_ = stats if stats is not None else LockstepStats()
     st_.seeds += B
@@ -384,7 +415,7 @@ def run_lockstep(algo, sim_nums, iterations, agents, truth_arr, sigma_n, prior, 
             for i in range(agents):
                 if explore_t[b][i] == 1:
                     x_sample = positions[b][i, :]
-                    y_sample = _sample(truth_arr, x_sample, streams[b], sigma_n)
+                    y_sample = _sample(truth_arr, x_sample, streams[b], sigma_n, tindex)
                     xb = np.vstack((xb, x_sample))
                     yb = np.vstack((yb, y_sample))
                     ib = np.vstack((ib, i))
@@ -419,6 +450,7 @@ def run_lockstep(algo, sim_nums, iterations, agents, truth_arr, sigma_n, prior, 
         ctx.synchronize()   # LinAlgError here if a seed's factor was not positive definite
         t4 = time.perf_counter()
         c0 = 0
+        lo, hi = grid_lo, grid_hi
         for b in range(B):
             nl = nloss[b]
             ng = len(seeds[b]) - nl
@@ -432,7 +464,6 @@ def run_lockstep(algo, sim_nums, iterations, agents, truth_arr, sigma_n, prior, 
             cen = np.empty((ng, 2))
             amax = np.empty((ng, 2))
             vmax = np.empty((ng, 1))
-            lo, hi = x_star.min(0), x_star.max(0)
             with np.errstate(invalid="ignore", divide="ignore"):
                 for i in range(ng):
                     j = c0 + nl + i

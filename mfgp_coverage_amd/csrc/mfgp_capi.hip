@@ -114,6 +114,8 @@ struct mfgp_ctx {
   // workgroups being resident at once -- the lattice step's GEMM runs as the second
   // launch (k_lat_gemm2, no cross-workgroup waits) instead of in-launch split-K tiles
   bool concurrent = false;
+  bool sync_query = false;    // synchronise by polling hipStreamQuery first (MFGP_SYNC_QUERY)
+  int rsplit_force = 0;       // one-pass predict row splits per cell group (0: the host's rule)
   bool lat_g3 = false;        // the two-launch lattice step's second launch builds its own Z rows
                               // (k_lat_gemm3) where it applies (MFGP_LAT_G3=1; off by default until
                               // it beats k_lat_gemm2 at the headline)
@@ -1146,7 +1148,8 @@ void set_rsplit(const mfgp_ctx* c, GPDesc* hd, int count) {
   }
   int64_t w1 = 0;
   for (int i = 0; i < count; ++i) w1 += ntiles_wg(hd[i].M);
-  const int R = (w1 >= 3 * c->ncu) ? 1 : (2 * w1 >= 3 * c->ncu ? 2 : 4);
+  int R = (w1 >= 3 * c->ncu) ? 1 : (2 * w1 >= 3 * c->ncu ? 2 : 4);
+  if (c->rsplit_force > 0) R = c->rsplit_force;   // (diagnostics: MFGP_RSPLIT)
   for (int i = 0; i < count; ++i) hd[i].rsplit = R;
 }
 
@@ -1307,7 +1310,12 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_SPIN_US")) c->spin_us = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("MFGP_SYNC_QUERY")) c->sync_query = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_G3")) c->lat_g3 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_RSPLIT")) {
+    const int r = std::atoi(e);
+    c->rsplit_force = (r == 1 || r == 2 || r == 4) ? r : 0;
+  }
   if (const char* e = std::getenv("MFGP_LAT_KSPLIT")) c->lat_ksplit = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("MFGP_LAT_WU")) c->lat_wu = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("MFGP_LAT_SELFG")) c->lat_selfg = std::atoi(e) != 0;
@@ -1393,6 +1401,17 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
         __builtin_ia32_pause();
         if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->spin_us)) break;
       }
+    }
+  }
+  if (c->sync_query) {
+    // poll the stream (hipStreamQuery) instead of the runtime's blocking wait, for
+    // up to spin_us; then the blocking wait
+    const auto t0 = std::chrono::steady_clock::now();
+    while (true) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) HIP_TRY(q);
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->spin_us)) break;
     }
   }
   HIP_TRY(hipStreamSynchronize(c->stream));

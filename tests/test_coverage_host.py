@@ -93,3 +93,23 @@ def test_reference_runs_used_the_seed_streams(case):
                 np.testing.assert_allclose(_col(nxt, A, "ProbExplore"), prob[:, 0], rtol=1e-15)
                 u = st.explore_draws(agents)
                 np.testing.assert_array_equal(_col(nxt, A, "Explore"), (u < prob[:, 0]).astype(float))
+
+
+def test_truth_index_selects_the_mask_rows():
+    """TruthIndex picks the rows sim:874-877's exact-equality mask picks: the same
+    rows in the same order, duplicates and a signed zero included, none for a
+    point off the grid."""
+    from mfgp_coverage_amd import coverage as C
+    g = np.linspace(0.0, 1.0, 17)
+    xs = np.array([(a, b) for a in g for b in g])
+    truth = np.column_stack([xs, np.arange(xs.shape[0], dtype=np.float64)])
+    truth = np.vstack([truth, [[0.5, 0.25, -1.0]], [[-0.0, 0.0, -2.0]]])   # a duplicate, a signed zero
+    ti = C.TruthIndex(truth)
+    probes = [xs[i] for i in range(0, xs.shape[0], 7)] + [np.array([0.5, 0.25]), np.array([0.0, -0.0]),
+                                                       np.array([0.5, 0.2500000001])]
+    for p in probes:
+        mask = np.logical_and(truth[:, 0] == p[0], truth[:, 1] == p[1])
+        assert np.array_equal(truth[mask, 2], truth[ti(p[0], p[1]), 2]), p
+        a = C._sample(truth, p, C.SeedStreams(3), 0.1)
+        b = C._sample(truth, p, C.SeedStreams(3), 0.1, ti)
+        assert a.shape == b.shape and np.array_equal(a, b), p

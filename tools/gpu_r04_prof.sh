@@ -17,3 +17,5 @@ PY
 bash tools/profile_round.sh r04 > gpurun_out/r04p_prof.log 2>&1 || exit $?
 python tools/summarize_profile.py gpurun_out/prof_r04 r04 > gpurun_out/r04p_summary.txt 2>&1
 tail -40 gpurun_out/r04p_summary.txt
+# the two-launch step's per-workgroup timeline (stamps build; k_lat_gemm2 by XCD)
+timeout -k 10 200 python -u tools/trace_lat.py tools/diaglib/libmfgp_stamps.so > gpurun_out/r04p_trace_lat.txt 2>&1 || true
