@@ -248,8 +248,6 @@ def simulate(algo, sim_num, iterations, agents, truth_arr, sigma_n, prior, hyp, 
     # 1-3) the empty model's max variance: the normalising constant (sim:827-843)
     truth_arr = np.asarray(truth_arr, dtype=np.float64)
     tindex = TruthIndex(truth_arr)
-    grid_lo = np.array([x_star[:, 0].min(), x_star[:, 1].min()])   # (the centroids' clamp, sim:276-281)
-    grid_hi = np.array([x_star[:, 0].max(), x_star[:, 1].max()])
     model = init(None)
     x_star = truth_arr[:, [0, 1]]
     bounding_box = np.array([np.amin(x_star[:, 0]), np.amax(x_star[:, 0]),

@@ -649,7 +649,14 @@ __device__ __forceinline__ void block_scan(int (&v)[NV], int (&tot)[NV], int* sc
 constexpr int ZR = 8;      // rows per thread per scan batch
 template <int KA>
 __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* sm) {
-  constexpr int ZMB = KA == 8 ? 16 : 6;   // members per row q per load batch
+  // members per row q per load batch: at KA = 8, 8 (two batches for the headline's
+  // ~16 members per row) rather than 16, whose axis values held 64 VGPRs and made
+  // the kernel spill 16 (2 now); the same FMAs in the same order, 0.5-2 % faster
+  // (tools/ab_variants.sh zmb8 zmb12, round 4)
+#ifndef MFGP_ZMB8
+#define MFGP_ZMB8 8
+#endif
+  constexpr int ZMB = KA == 8 ? MFGP_ZMB8 : 6;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Hyp& h = d.hp;

@@ -1,5 +1,5 @@
 """One GP at the headline size (128x128, N = 2048, 8 new rows per step) through the
-batched API on the V stream (k_inc_stream1): steps back to back (asynchronous) and
+batched API on the V stream (k_inc_stream1; argv[2] "lat": the lattice step forced): steps back to back (asynchronous) and
 steps separated by a host pause with a synchronise each (the drop-in simulator's
 pattern), so that rocprofv3's kernel trace can tell the kernel's own duration in
 both. argv: pause in microseconds (0 = back to back)."""
@@ -14,12 +14,13 @@ import torch  # noqa: E402
 from mfgp_coverage_amd import _lib, synthetic  # noqa: E402
 
 PAUSE_US = float(sys.argv[1]) if len(sys.argv) > 1 else 0.0
+LATTICE = len(sys.argv) > 2 and sys.argv[2] == "lat"   # the lattice step forced instead of the V stream
 G, NL, NH, k, S = 128, 1024, 1024, 8, 64
 NH0 = NH - k
 dev = torch.device("cuda", 0)
 wl = synthetic.Workload(G, NL, NH0, k, S, seed=0)
 ctx = _lib.context()
-ctx.set_lattice(False)
+ctx.set_lattice("force" if LATTICE else False)
 m = _lib.Model(ctx, _lib.MF, synthetic.HYP["australia8_mf"], 1e-8)
 m.set_grid(wl.xs)
 m.set_data(wl.XL, wl.yL, wl.XH, wl.yH)
