@@ -233,7 +233,30 @@ __device__ __forceinline__ int64_t wst_first(int64_t C, int64_t nwb, int64_t jb)
   const int64_t K2 = 2 * C - 4 * (nwb - 1);
   return 2 * jb < nwb ? jb * K2 : (nwb - 1 - jb) * K2 + C - 4 * (nwb - 1 - jb);
 }
+#ifndef MFGP_W_SKEW
+#define MFGP_W_SKEW 0
+#endif
+#if MFGP_W_SKEW
+// (diagnostic builds: the first half of the units weigh 1000 + MFGP_W_SKEW, the rest
+// 1000 - MFGP_W_SKEW; unit u's first step and the unit holding step s)
+__device__ __forceinline__ int64_t wst_start(int64_t u, int64_t S, int64_t U) {
+  const int64_t H = U / 2, a = 1000 + MFGP_W_SKEW, b = 1000 - MFGP_W_SKEW;
+  const int64_t cum = u <= H ? u * a : H * a + (u - H) * b;
+  return S * cum / (H * a + (U - H) * b);
+}
+__device__ __forceinline__ int64_t wst_unit(int64_t s, int64_t S, int64_t U) {
+  int64_t lo = 0, hi = U - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) / 2;
+    if (wst_start(mid, S, U) <= s) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+#else
+__device__ __forceinline__ int64_t wst_start(int64_t u, int64_t S, int64_t U) { return u * S / U; }
 __device__ __forceinline__ int64_t wst_unit(int64_t s, int64_t S, int64_t U) { return ((s + 1) * U - 1) / S; }
+#endif
 // block jb's position in the pair order (its partials: slots u + position, distinct
 // since a position's units start where the previous position's end)
 __device__ __forceinline__ int64_t wst_pos(int64_t nwb, int64_t jb) {
@@ -251,6 +274,9 @@ __device__ __forceinline__ int64_t wst_pos(int64_t nwb, int64_t jb) {
 // is), stores the block of w, counts it into ldone[0] (the Z units wait for all
 // nwb blocks) and writes F's new rows for its columns, -L22^-1 w^T (the top
 // block's also the L22^-1 entries).
+#ifndef MFGP_W_PRIO
+#define MFGP_W_PRIO 0
+#endif
 template <class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
   constexpr int DEPTH = MFGP_W_DEPTH;   // steps in flight per wave
@@ -288,7 +314,7 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   const int64_t C = (n0 + 15) / 16;
   const int64_t K2 = 2 * C - 4 * (nwb - 1);
   const int64_t S = (nwb / 2) * K2 + (nwb & 1) * (C - 4 * (nwb / 2));
-  const int64_t s0 = u * S / U, s1 = (u + 1) * S / U;
+  const int64_t s0 = wst_start(u, S, U), s1 = wst_start(u + 1, S, U);
   const int64_t T = s1 - s0;
   // the unit's first step: pair p0, its first (odd0 = 0: block p0) or second block
   // (nwb - 1 - p0), step st0 of it
@@ -450,6 +476,14 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   // compiler's waits at the loop head drain every load in flight; the buffers by
   // compile-time index: registers)
   for (int64_t t0 = 0; t0 < T; t0 += DEPTH) {
+#if MFGP_W_PRIO
+    // priority by progress (2, 1, 0 over the thirds of the unit's steps): the
+    // memory pipe serves a CU's older waves first, so of the two units on a CU the
+    // later-dispatched one streamed 15 % slower; a unit ahead now yields to one behind
+    if (t0 >= (2 * T) / 3) __builtin_amdgcn_s_setprio(0);
+    else if (t0 >= T / 3) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(2);
+#endif
 #pragma unroll
     for (int b = 0; b < DEPTH; ++b) {
       const int64_t t = t0 + b;
@@ -466,6 +500,9 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     }
   }
   WTRACE(3);
+#if MFGP_W_PRIO
+  __builtin_amdgcn_s_setprio(2);   // the count-in and the block reductions are on the step's critical path
+#endif
   // count the unit's partials in (one arrival per block, all at once)
   drain_stores();
   __syncthreads();

@@ -9,3 +9,11 @@ tail -5 gpurun_out/r04_gpu_tests.log
 grep -E "FAILED|ERROR" gpurun_out/r04_gpu_tests.log | head -20
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -2
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r04_final_bench20.json 2> gpurun_out/r04_final_bench20.err || exit 1
+timeout -k 10 300 python -u bench.py > gpurun_out/r04_final_bench.json 2> gpurun_out/r04_final_bench.err || exit 1
+timeout -k 10 200 python -u tools/bench_dropin.py > gpurun_out/r04_dropin.jsonl 2>/dev/null || exit 1
+python3 -c "
+import json
+for f in ('r04_final_bench20', 'r04_final_bench'):
+    d = json.load(open(f'gpurun_out/{f}.json')); print(f, round(d['value']), round(1e3*d['ms_per_step'], 2), d['simulation']['value'] if 'simulation' in d else '')
+print(open('gpurun_out/r04_dropin.jsonl').read()[:300])"

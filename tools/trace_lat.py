@@ -106,3 +106,17 @@ wcu = dict(zip(*np.unique(cu[wsel], return_counts=True)))
 nw = np.array([wcu.get(c, 0) for c in gcu])
 for n in sorted(set(nw)):
     print(f"    GEMM WGs sharing their CU with {n} w units: K-loop {q(dur[nw == n])}")
+# per w unit (index within its GP): start of its F loop, loop duration, end (medians over the GPs)
+wsel_all = (role >= nprod) & (role < nprod + nwu) & used
+uidx = role - nprod
+st_ = {u: [] for u in range(nwu)}
+for i in np.nonzero(wsel_all)[0]:
+    st_[int(uidx[i])].append((tr[i, 1], tr[i, 3] - tr[i, 1], tr[i, 3]))
+rows = []
+for u in range(nwu):
+    if st_[u]:
+        a = np.array(st_[u])
+        rows.append((u, *np.median(a, 0)))
+print("  w unit: index, start, F-loop duration, end (medians over GPs)")
+for r in rows:
+    print("   ", f"{r[0]:3d} {r[1]:6.1f} {r[2]:6.1f} {r[3]:6.1f}")
