@@ -591,7 +591,7 @@ def main():
         v_ms = tm["predict_ms"] / max(1, tm["predict_launches"])
         v_gbs = vbytes / (v_ms * 1e-3) / 1e9 if v_ms > 0 else float("nan")
         # the lattice step in axis form (k_inc_lat). Bytes: F's
-        # lower triangle read once by the w pass (the dominant stream), the resident
+        # lower triangle read once by the w pass (the dominant stream; es bytes per element), the resident
         # posterior in and out plus the caller's mu / var, the new V rows, the Z rows
         # written once and read by every 64-column tile row; flops: the w pass (16 n0^2),
         # the Z sums (2 KA nx n_t) and the K = parts x ny GEMM (2 KA M parts ny8)
@@ -599,7 +599,8 @@ def main():
         parts = 2
         n_t = n0 + (n0 - NL)
         ny8 = -(-G // 8) * 8
-        fbytes = 8 * sum((n0 - 64 * jb) * 64 for jb in range(-(-n0 // 64)))
+        # (F's elements: fp32 for MFGP_F32 models, whose w units stream the rounded copy)
+        fbytes = es * sum((n0 - 64 * jb) * 64 for jb in range(-(-n0 // 64)))
         zbytes = 8 * parts * ny8 * G * ka * (1 + -(-G // 64))
         lat_bytes = B * (fbytes + 8 * 6 * M + es * M * k + zbytes) * shr
         lat_flops = B * (16 * n0 * n0 + 2 * ka * G * n_t + 2 * ka * M * parts * ny8) * shr

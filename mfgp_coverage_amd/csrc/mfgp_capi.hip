@@ -200,6 +200,7 @@ struct mfgp_model {
   uint64_t res_tick[2] = {0, 0}, tick = 0;
   // lattice-separable step state (allocated on first use)
   double* F = nullptr;        // explicit L^-1 [F_ld][F_ld], rows [0, F_n) current for generation F_gen
+  float* Ff = nullptr;        // MFGP_F32: F in fp32 (the rows the lattice steps stream and extend)
   int64_t F_ld = 0, F_n = 0;
   uint64_t F_gen = 0;
   double* tab = nullptr;      // separable tables [4][tab_ld][tabw], rows [0, tab_n)
@@ -371,6 +372,7 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   }
   // the lattice step's F and tables move to the new leading dimension too
   double *F = nullptr, *tab = nullptr;
+  float* Ff = nullptr;
   int* lidx = nullptr;
   if (keep && m->F && m->F_n > 0) {
     HIP_TRY(hipMalloc(&F, sizeof(double) * fblk_size(ld)));
@@ -378,6 +380,13 @@ int ensure_cap(mfgp_model* m, int64_t need) {
     for (int64_t jb = 0; 64 * jb < m->F_n; ++jb)   // each column block's rows [64 jb, F_n)
       HIP_TRY(hipMemcpyAsync(F + fblk_off(jb, ld), m->F + fblk_off(jb, m->F_ld),
                              sizeof(double) * 64 * (m->F_n - 64 * jb), hipMemcpyDeviceToDevice, c->stream));
+    if (m->Ff) {   // (MFGP_F32: the rows past the build live in Ff only)
+      HIP_TRY(hipMalloc(&Ff, sizeof(float) * fblk_size(ld)));
+      HIP_TRY(hipMemsetAsync(Ff, 0, sizeof(float) * fblk_size(ld), c->stream));
+      for (int64_t jb = 0; 64 * jb < m->F_n; ++jb)
+        HIP_TRY(hipMemcpyAsync(Ff + fblk_off(jb, ld), m->Ff + fblk_off(jb, m->F_ld),
+                               sizeof(float) * 64 * (m->F_n - 64 * jb), hipMemcpyDeviceToDevice, c->stream));
+    }
   }
   if (m->tab && m->tab_n > 0) {
     HIP_TRY(hipMalloc(&tab, sizeof(double) * 4 * ld * m->tabw));
@@ -390,10 +399,12 @@ int ensure_cap(mfgp_model* m, int64_t need) {
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (m->F) HIP_TRY(hipFree(m->F));
+  if (m->Ff) HIP_TRY(hipFree(m->Ff));
   if (m->tab) HIP_TRY(hipFree(m->tab));
   if (m->lidx) HIP_TRY(hipFree(m->lidx));
   m->lidx = lidx;
   m->F = F;
+  m->Ff = Ff;
   m->F_ld = F ? ld : 0;
   if (!F) m->F_n = 0;
   m->tab = tab;
@@ -539,6 +550,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.vres = 0;
   d.ablk = m->ablk;
   d.F = nullptr;
+  d.Ff = nullptr;
   d.tab = nullptr;
   d.wv = nullptr;
   d.wflag = nullptr;
@@ -663,12 +675,19 @@ hipError_t hip_malloc_2m(void** p, size_t bytes) {
 int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
   hipStream_t s = m->ctx->stream;
   const int64_t ld = m->ld, tabw = lat_tabw(m);
-  if (!m->F || m->F_ld != ld) {
+  const bool ff = m->dtype == MFGP_F32;   // (F streamed in fp32: DESIGN.md section 2.3)
+  if (!m->F || m->F_ld != ld || (ff && !m->Ff)) {
     HIP_TRY(hipStreamSynchronize(s));
     if (m->F) HIP_TRY(hipFree(m->F));
+    if (m->Ff) HIP_TRY(hipFree(m->Ff));
     m->F = nullptr;
+    m->Ff = nullptr;
     HIP_TRY(hipMalloc(&m->F, sizeof(double) * fblk_size(ld)));
     HIP_TRY(hipMemsetAsync(m->F, 0, sizeof(double) * fblk_size(ld), s));   // F's upper triangle stays zero
+    if (ff) {
+      HIP_TRY(hipMalloc(&m->Ff, sizeof(float) * fblk_size(ld)));
+      HIP_TRY(hipMemsetAsync(m->Ff, 0, sizeof(float) * fblk_size(ld), s));
+    }
     m->F_ld = ld;
     m->F_n = 0;
   }
@@ -781,6 +800,7 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
 void free_lat(mfgp_model* m) {
   if (m->csr) (void)hipFree(m->csr);
   if (m->F) (void)hipFree(m->F);
+  if (m->Ff) (void)hipFree(m->Ff);
   if (m->tab) (void)hipFree(m->tab);
   if (m->wv) (void)hipFree(m->wv);
   if (m->wflag) (void)hipFree(m->wflag);
@@ -1084,6 +1104,13 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
     }
     for (int i0 = 0; i0 < count; i0 += chunk)
       HIP_TRY(launch_trinv_f(dd + i0, std::min(chunk, count - i0), max_nbr, tscr, tstride, c->stream));
+    // MFGP_F32: the copy the lattice step streams, rounded once per build
+    if (hd[0].vf32) {
+      int64_t max_el = 0;
+      for (int i = 0; i < count; ++i)
+        if (hd[i].lat_fbuild) max_el = std::max<int64_t>(max_el, fblk_size(hd[i].ld));
+      HIP_TRY(launch_narrow_f(dd, count, max_el, c->stream));
+    }
   }
   if (max_rows > 0) HIP_TRY(launch_lat_tables(dd, count, max_rows, c->stream));
   if (max_axw > 0) HIP_TRY(launch_lat_axes(dd, count, max_axw, c->stream));
@@ -2217,6 +2244,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         res_b[i] = 1 - bin;
         res_depth[i] = m->res_depth[bin] + 1;
         fd.F = m->F;
+        fd.Ff = m->Ff;
         fd.tab = m->tab;
         fd.tabw = m->tabw;
         fd.wv = m->wv;

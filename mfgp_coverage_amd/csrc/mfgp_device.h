@@ -12,6 +12,7 @@ namespace mfgp {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef float fv2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // Generic -> global address space, so loads/stores through descriptor pointers

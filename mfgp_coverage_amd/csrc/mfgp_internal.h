@@ -99,6 +99,8 @@ struct GPDesc {
   int rsplit;          // one-pass predict: row splits per cell group (1, 2, 4; 128 / rsplit cells per workgroup)
   int vf32;            // 1 = the resident V is Vf (fp32; the one-pass predict streams 256 cells per workgroup)
   // lattice-separable step (k_inc_lat, mfgp_lattice.inl)
+  float* Ff;           // MFGP_F32 models: F rounded to fp32 (the same layout), the copy the w units
+                       // stream and extend (k_trinv_f still builds F in fp64; k_narrow_f rounds it)
   double* F;           // explicit L^-1, lower triangle in 64-column blocks: block jb holds rows
                        // [64 jb, ld) x 64 columns contiguously (F[i][j] at fblk_off(j / 64, ld) +
                        // (i - 64 (j / 64)) * 64 + j % 64); zeros above the diagonal
@@ -216,6 +218,8 @@ __host__ __device__ inline int64_t g3_cw_off(int64_t tabw, int64_t ld) {
 }
 __host__ __device__ inline int64_t g3_bytes(int64_t tabw, int64_t ld) { return 4 * g3_cw_off(tabw, ld) + 8 * 16 * ld; }
 hipError_t launch_lat_gemm3(const GPDesc* d, int count, int64_t max_tiles, int vf32, hipStream_t s);
+// MFGP_F32 models whose F was just built (lat_fbuild): Ff = (float) F over F's storage
+hipError_t launch_narrow_f(const GPDesc* d, int count, int64_t max_elems, hipStream_t s);
 hipError_t launch_lat_gemm3_arg(const GPDesc* h, int count, int64_t max_tiles, int vf32, hipStream_t s);
 // the second launch of a lattice step (lat_g2): its GEMM and cells, max_tiles =
 // max over GPs of lat_tiles

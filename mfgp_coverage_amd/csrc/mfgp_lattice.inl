@@ -360,12 +360,21 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   auto load_f = [&](const Cur& c, dv2 (&f)[2]) {
     const int64_t i = row_of(c);
     const int64_t ii = i < n0 ? i : n0 - 1;
-    const GLOBAL dv2* Fr =
-        reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + fblk_off(c.jb, ld) + (ii - 64 * c.jb) * 64 + 2 * r);
     // plain loads: F stays in the memory-side cache across steps where it fits
     // (tools/probe_wloop.hip: 2 units per CU, plain 25 us vs non-temporal 26-30 us)
-    f[0] = Fr[0];
-    f[1] = Fr[16];
+    if constexpr (sizeof(VT) == 4) {
+      // MFGP_F32: F streamed in fp32 (half the bytes), widened for the f64 MFMA
+      const GLOBAL fv2* Fr =
+          reinterpret_cast<const GLOBAL fv2*>(gp(d.Ff) + fblk_off(c.jb, ld) + (ii - 64 * c.jb) * 64 + 2 * r);
+      const fv2 f0 = Fr[0], f1 = Fr[16];
+      f[0] = dv2{(double)f0.x, (double)f0.y};
+      f[1] = dv2{(double)f1.x, (double)f1.y};
+    } else {
+      const GLOBAL dv2* Fr =
+          reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + fblk_off(c.jb, ld) + (ii - 64 * c.jb) * 64 + 2 * r);
+      f[0] = Fr[0];
+      f[1] = Fr[16];
+    }
   };
   // The A operand L21[r][i]. When every new point is the lattice cell its rounded
   // axis estimate names (the producers' fast-path test, inc_gather_fast; every wave
@@ -605,13 +614,17 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       if (j >= n0) continue;
       double t = 0.0;
       for (int bb = 0; bb <= a; ++bb) t -= Li[a * KINC + bb] * Wh[jl * KINC + bb];
-      d.F[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + jl] = t;
+      if constexpr (sizeof(VT) == 4) d.Ff[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + jl] = (float)t;
+      else d.F[fblk_off(jb, ld) + (n0 + a - 64 * jb) * 64 + jl] = t;
     }
     if (jb == nwb - 1)
       for (int e = tid; e < k * k; e += NT) {
         const int a = e / k, bb = e % k;
         const int64_t j = n0 + bb, jb2 = j / 64;
-        if (bb <= a) d.F[fblk_off(jb2, ld) + (n0 + a - 64 * jb2) * 64 + j % 64] = Li[a * KINC + bb];
+        if (bb <= a) {
+          if constexpr (sizeof(VT) == 4) d.Ff[fblk_off(jb2, ld) + (n0 + a - 64 * jb2) * 64 + j % 64] = (float)Li[a * KINC + bb];
+          else d.F[fblk_off(jb2, ld) + (n0 + a - 64 * jb2) * 64 + j % 64] = Li[a * KINC + bb];
+        }
       }
     __syncthreads();   // Wh is reused by the next block
   }
@@ -2300,4 +2313,26 @@ __global__ __launch_bounds__(NT) void k_lat_axes(const GPDesc* __restrict__ desc
     const int64_t p = rr % (tabw + 1);
     d.axt[rr * tabw + col] = p < tabw ? lat_axis_value(d, t, p, col) : 0.0;
   }
+}
+
+// MFGP_F32: Ff = (float) F over F's storage, for the GPs whose F was just built
+__global__ __launch_bounds__(NT) void k_narrow_f(const GPDesc* __restrict__ descs) {
+  const GPDesc& d = descs[blockIdx.y];
+  if (!d.lat_fbuild || !d.Ff || !d.vf32) return;
+  const int64_t n = fblk_size(d.ld);
+  for (int64_t e = ((int64_t)blockIdx.x * NT + threadIdx.x) * 2; e < n; e += (int64_t)gridDim.x * NT * 2) {
+    if (e + 1 < n) {
+      const dv2 v = *reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + e);
+      *reinterpret_cast<GLOBAL fv2*>(gp(d.Ff) + e) = fv2{(float)v.x, (float)v.y};
+    } else {
+      d.Ff[e] = (float)d.F[e];
+    }
+  }
+}
+
+hipError_t launch_narrow_f(const GPDesc* d, int count, int64_t max_elems, hipStream_t s) {
+  if (count < 1 || max_elems <= 0) return hipSuccess;
+  const int64_t wgs = std::min<int64_t>(1024, (max_elems / 2 + NT - 1) / NT);
+  hipLaunchKernelGGL(k_narrow_f, dim3((unsigned)wgs, count), dim3(NT), 0, s, d);
+  return hipGetLastError();
 }
