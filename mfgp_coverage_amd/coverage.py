@@ -288,7 +288,9 @@ def simulate(algo, sim_num, iterations, agents, truth_arr, sigma_n, prior, hyp, 
         # 9-11) loss, centroids, max variance (sim:894-904)
         loss_vor = voronoi_bounded(positions, bounding_box)
         loss_t = geometry.compute_loss(loss_vor, truth_arr)
-        lloyd_vor = voronoi_bounded(centroids_t, bounding_box)
+        # (every agent exploited: it stands on its centroid, so the two partitions are
+        # of the same points -- the same partition, computed once)
+        lloyd_vor = loss_vor if np.array_equal(positions, centroids_t) else voronoi_bounded(centroids_t, bounding_box)
         centroids_t = geometry.compute_centroids(lloyd_vor, x_star, mu_star)
         argmax_var_t, max_var_t = geometry.compute_max_var(lloyd_vor, truth_arr, var_star)
         if log:
@@ -433,7 +435,9 @@ def run_lockstep(algo, sim_nums, iterations, agents, truth_arr, sigma_n, prior, 
         cells, seeds, field, nloss = [], [], [], []
         for b in range(B):
             lv, lp = _cells_of(voronoi_bounded(positions[b], bounding_box))
-            gv, gp = _cells_of(voronoi_bounded(centroids_t[b], bounding_box))
+            # (a seed whose agents all exploited stands on its centroids: one partition)
+            same = np.array_equal(positions[b], centroids_t[b])
+            gv, gp = (lv, lp) if same else _cells_of(voronoi_bounded(centroids_t[b], bounding_box))
             nloss.append(len(lv))
             cells.extend(lv + gv)
             seeds.append(np.vstack([lp, gp]))
