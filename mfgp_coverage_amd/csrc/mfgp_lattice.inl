@@ -217,6 +217,9 @@ __device__ __forceinline__ double l21c_ld(const double* l21c, int64_t i, int a) 
   }
 }
 
+#ifndef MFGP_W_DEPTH_F
+#define MFGP_W_DEPTH_F 10
+#endif
 #ifndef MFGP_W_DEPTH
 #define MFGP_W_DEPTH 6
 #endif
@@ -279,7 +282,14 @@ __device__ __forceinline__ int64_t wst_pos(int64_t nwb, int64_t jb) {
 #endif
 template <class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
-  constexpr int DEPTH = MFGP_W_DEPTH;   // steps in flight per wave
+  // steps in flight per wave: the loop is latency-bound (each step waits for loads
+  // issued DEPTH - 1 steps earlier), so fp32 F, whose raw 16-byte rows take half the
+  // registers of the widened pairs, keeps more in flight
+  constexpr int DEPTH = sizeof(VT) == 4 ? MFGP_W_DEPTH_F : MFGP_W_DEPTH;
+  // a step's F in registers: two widened pairs (fp64 F) or the raw four floats (fp32)
+  struct FRow {
+    dv2 v[sizeof(VT) == 4 ? 1 : 2];
+  };
   const int64_t n0 = d.n0, ld = d.ld;
   const int nwb = d.nwb;
   const int64_t U = d.nwu;
@@ -357,23 +367,22 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   // 16-byte loads: MFMA 2 hh + 0 takes the even columns, 2 hh + 1 the odd ones. A
   // row past n0 (the block's last step) reloads row n0 - 1 (finite) and is masked.
   auto row_of = [&](const Cur& c) { return 64 * c.jb + 16 * c.st + 4 * w + q; };
-  auto load_f = [&](const Cur& c, dv2 (&f)[2]) {
+  auto load_f = [&](const Cur& c, FRow& f) {
     const int64_t i = row_of(c);
     const int64_t ii = i < n0 ? i : n0 - 1;
     // plain loads: F stays in the memory-side cache across steps where it fits
     // (tools/probe_wloop.hip: 2 units per CU, plain 25 us vs non-temporal 26-30 us)
     if constexpr (sizeof(VT) == 4) {
-      // MFGP_F32: F streamed in fp32 (half the bytes), widened for the f64 MFMA
-      const GLOBAL fv2* Fr =
-          reinterpret_cast<const GLOBAL fv2*>(gp(d.Ff) + fblk_off(c.jb, ld) + (ii - 64 * c.jb) * 64 + 2 * r);
-      const fv2 f0 = Fr[0], f1 = Fr[16];
-      f[0] = dv2{(double)f0.x, (double)f0.y};
-      f[1] = dv2{(double)f1.x, (double)f1.y};
+      // MFGP_F32: F streamed in fp32 (half the bytes), widened for the f64 MFMA; one
+      // 16-byte load per lane: columns 4 r .. 4 r + 3 (acc[j] then holds column 4 r + j;
+      // seg_done stores by that map)
+      // (kept as raw bits in a dv2 slot: widened at compute)
+      f.v[0] = *reinterpret_cast<const GLOBAL dv2*>(gp(d.Ff) + fblk_off(c.jb, ld) + (ii - 64 * c.jb) * 64 + 4 * r);
     } else {
       const GLOBAL dv2* Fr =
           reinterpret_cast<const GLOBAL dv2*>(gp(d.F) + fblk_off(c.jb, ld) + (ii - 64 * c.jb) * 64 + 2 * r);
-      f[0] = Fr[0];
-      f[1] = Fr[16];
+      f.v[0] = Fr[0];
+      f.v[sizeof(VT) == 4 ? 0 : 1] = Fr[16];
     }
   };
   // The A operand L21[r][i]. When every new point is the lattice cell its rounded
@@ -395,8 +404,10 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     const dv2 g = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid))[cr];
     const bool miss = r < k && !(g.x == px && g.y == py);
     selfg = d.lat_selfg && L.nx > 0 && d.vres >= n0 && vres_ptr<VT>(d) != nullptr && __ballot(miss) == 0;
+    // (lanes r >= k carry no point: they read lane 0's element, the same line, so the
+    // compact rows' unused half costs no traffic; their MFMA input is zeroed)
     asrc = selfg ? vres_ptr<VT>(d) + (cr / PBM) * d.vld * PBM + (cr % PBM)
-                 : reinterpret_cast<const VT*>(l21c) + r;
+                 : reinterpret_cast<const VT*>(l21c) + (r < k ? r : 0);
     astr = selfg ? (int64_t)PBM : (int64_t)KINC;
   }
   auto load_a = [&](const Cur& c, double& a) {
@@ -408,8 +419,17 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
 #pragma unroll
   for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
   // (columns a >= k of w are never read: zero)
-  auto compute = [&](const dv2 (&f)[2], double a, bool live) {
+  auto compute = [&](const FRow& fr, double a, bool live) {
     const double av = (live && r < k) ? a : 0.0;
+    dv2 f[2];
+    if constexpr (sizeof(VT) == 4) {
+      const f4 fq = __builtin_bit_cast(f4, fr.v[0]);   // columns 4 r .. 4 r + 3, widened
+      f[0] = dv2{(double)fq.x, (double)fq.y};
+      f[1] = dv2{(double)fq.z, (double)fq.w};
+    } else {
+      f[0] = fr.v[0];
+      f[1] = fr.v[sizeof(VT) == 4 ? 0 : 1];
+    }
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       acc[2 * hh] = mfma(av, f[hh].x, acc[2 * hh]);
@@ -443,8 +463,17 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
     // own[2 hh + m2] is output e = 512 hh + tid + 256 m2 of the block
     double* const part = d.wpart + (u + wst_pos(nwb, jb)) * 1024;
+    if constexpr (sizeof(VT) == 4) {
+      // (the fp32 F's lanes: own[2 hh + m2] is column 4 (jp >> 1) + 2 hh + (jp & 1), row a)
 #pragma unroll
-    for (int m = 0; m < 4; ++m) stx<true>(part + tid + NT * m, own[m]);
+      for (int m = 0; m < 4; ++m) {
+        const int x = tid + NT * (m & 1), jp = x >> 4, a = x & 15, hh = m >> 1;
+        stx<true>(part + (((jp >> 1) << 2) | (hh << 1) | (jp & 1)) * 16 + a, own[m]);
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) stx<true>(part + tid + NT * m, own[m]);
+    }
     if (tid == 0) segs[nseg] = (int)jb;
     ++nseg;
   };
@@ -452,7 +481,7 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   // past the unit's last step reload its last step (unused): a branch around a
   // load would make the compiler's wait for the current step also wait for the
   // loads behind it.
-  dv2 fb[DEPTH][2];
+  FRow fb[DEPTH];
   double ab[DEPTH];
   Cur cl = cur0;   // the next step to load (clamped to the last)
   int64_t tl = 0;
