@@ -116,6 +116,9 @@ struct mfgp_ctx {
   bool concurrent = false;
   bool sync_query = false;    // synchronise by polling hipStreamQuery first (MFGP_SYNC_QUERY)
   int rsplit_force = 0;       // one-pass predict row splits per cell group (0: the host's rule)
+  int lat_zcsr = -1;          // the Z units read member lists built by one scan unit per part
+                              // instead of bucketing every row themselves (-1: where that is
+                              // large; MFGP_LAT_ZCSR=0/1 forces it)
   bool lat_g3 = false;        // the two-launch lattice step's second launch builds its own Z rows
                               // (k_lat_gemm3) where it applies (MFGP_LAT_G3=1; off by default until
                               // it beats k_lat_gemm2 at the headline)
@@ -573,6 +576,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.lat_selfg = 0;
   d.lat_g2 = 0;
   d.lat_g3 = 0;
+  d.lat_zcsr = 0;
   d.csr = nullptr;
   d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
   d.hp = d.hf;
@@ -779,13 +783,13 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     HIP_TRY(hipMalloc(&m->ldone, sizeof(unsigned) * 4));
     HIP_TRY(hipMemsetAsync(m->ldone, 0, sizeof(unsigned) * 4, s));   // no arrivals; flags below every epoch
   }
-  if (m->zflag_n < nzu) {
+  if (m->zflag_n < nzu + 2) {
     HIP_TRY(hipStreamSynchronize(s));
     if (m->zflag) HIP_TRY(hipFree(m->zflag));
     m->zflag = nullptr;
-    HIP_TRY(hipMalloc(&m->zflag, sizeof(unsigned) * nzu));
-    HIP_TRY(hipMemsetAsync(m->zflag, 0, sizeof(unsigned) * nzu, s));   // below every epoch
-    m->zflag_n = nzu;
+    HIP_TRY(hipMalloc(&m->zflag, sizeof(unsigned) * (nzu + 2)));
+    HIP_TRY(hipMemsetAsync(m->zflag, 0, sizeof(unsigned) * (nzu + 2), s));   // below every epoch
+    m->zflag_n = (nzu + 2);
   }
   const size_t need = ksplit > 1 ? (size_t)tiles * ksplit * 8192 : 0;   // LAT_PART doubles per split tile
   if (need > m->gpart_n) {
@@ -1069,7 +1073,7 @@ int enqueue_inc_stream(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int coun
 int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   int64_t max_blocks = 0, max_nbr = 0, max_rows = 0, max_axw = 0, max_tiles = 0;
   for (int i = 0; i < count; ++i) {
-    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu +
+    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu + (hd[i].lat_zcsr ? 2 : 0) +
                                                    (hd[i].lat_g2 ? 0 : (int64_t)hd[i].lat_tiles * hd[i].ksplit));
     max_tiles = std::max<int64_t>(max_tiles, hd[i].lat_tiles);
     if (hd[i].lat_fbuild) max_nbr = std::max(max_nbr, nblocks_rows(hd[i].n0));
@@ -1152,7 +1156,7 @@ int enqueue_inc_stream_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
 int enqueue_inc_lat_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
   int64_t max_blocks = 0, max_tiles = 0;
   for (int i = 0; i < count; ++i) {
-    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu +
+    max_blocks = std::max<int64_t>(max_blocks, hd[i].nprod + hd[i].nwu + hd[i].nzu + (hd[i].lat_zcsr ? 2 : 0) +
                                                    (hd[i].lat_g2 ? 0 : (int64_t)hd[i].lat_tiles * hd[i].ksplit));
     max_tiles = std::max<int64_t>(max_tiles, hd[i].lat_tiles);
   }
@@ -1339,6 +1343,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (const char* e = std::getenv("MFGP_SPIN_US")) c->spin_us = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("MFGP_SYNC_QUERY")) c->sync_query = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_G3")) c->lat_g3 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_LAT_ZCSR")) c->lat_zcsr = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("MFGP_RSPLIT")) {
     const int r = std::atoi(e);
     c->rsplit_force = (r == 1 || r == 2 || r == 4) ? r : 0;
@@ -2276,6 +2281,13 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.lat_selfg = selfg;
         fd.lat_g2 = g2 ? 1 : 0;
         fd.lat_g3 = g3 ? 1 : 0;
+        // Z units reading the scan units' member lists (every lattice row count the scan
+        // units bucket, rows and lattice indices within 16 bits)
+        // -- by default where the Z units' own bucketing is large (every unit scans every
+        // row of its part: nzu x n0 per GP; configs[4] 256 x 8184: 17.8k -> 18.7k
+        // GP-updates/s; the headline's 64 x 2040 is 1 % faster without)
+        const bool zc = c->lat_zcsr > 0 || (c->lat_zcsr < 0 && nzu * fd.n0 >= (int64_t(1) << 20));
+        fd.lat_zcsr = (!g3 && zc && m->lat.ny <= 256 && m->ld <= 65535) ? 1 : 0;
         fd.csr = m->csr;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }

@@ -143,6 +143,8 @@ struct GPDesc {
   int lat_g3;          // 1 = that second launch builds its Z rows itself (k_lat_gemm3; lat_tiles are
                        // its 4-column tiles) from the member lists the scan units of k_inc_lat write
                        // (nzu = parts), instead of reading the Z units' rows
+  int lat_zcsr;        // 1 = one scan unit per part (the launch's first roles) lists the members by
+                       // lattice row in csr, and the Z units read their rows' lists (lat_zunit_csr)
   unsigned* csr;       // g3 member lists, per part [tabw + 1 + ld]: offsets by lattice y-row [ny + 1],
                        // then the members (px << 16) | j in row order, rows ascending; then the
                        // rows' places and the members' c w rows (g3_pos_off, g3_cw_off)

@@ -956,6 +956,163 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
   WTRACE(2);
 }
 
+// A Z unit reading the member lists of the part's scan unit (lat_zcsr: the scan
+// units are the launch's first roles, before the producers): its rows' members are
+// contiguous in the CSR, so the unit reads only them instead of bucketing every
+// row of the part (at configs[4]'s 8,184 rows and 256 units per GP that scan was
+// most of the Z phase). The sums, their order and everything after them are
+// lat_zunit's: the same bits.
+template <int KA>
+__device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, double* sm) {
+  constexpr int ZMB = KA == 8 ? MFGP_ZMB8 : 6;   // members per row q per load batch
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Hyp& h = d.hp;
+  const int P = h.kind == 0 ? 1 : 2;
+  const int64_t tabw = d.tabw;
+  const int ZQ = d.zq;
+  const int ZH = ZQ / 2;
+  const int64_t nu = d.nzu / P;
+  const int part = (int)(zu / nu);
+  const int64_t c = zu % nu;
+  const int64_t ny = d.lat.ny;
+  const int64_t NL = d.NL;
+  const int ql = __builtin_amdgcn_readfirstlane((int)(tid / tabw));
+  const int64_t ix = tid % tabw;
+  const int64_t zq8 = (ny + ZKS - 1) / ZKS * ZKS;
+  const int64_t zrows = d.zrows, tstride = d.ld * tabw;
+  const unsigned epoch = d.epoch;
+  const double* const wv = d.wv;
+  double* const zb = d.zb;
+  const int* const zvl = d.zvl + part * (zrows + 1);
+  const double* const axr = d.axt + (2 * part) * (tabw + 1) * tabw + ix;   // ex(p, ix) at axr[p * tabw]
+  const double cL = h.kind == 0 ? h.sL : h.rho * h.sL, cLH = h.rho2 * h.sL;
+  auto coef = [&](int64_t j) { return part == 1 ? h.sH : (j < NL ? cL : cLH); };
+  double* const cw = sm + w * 2 * ZMB * KA;   // the waves' coefficient batches [4][2][ZMB][KA]
+  static_assert(4 * 2 * ZMB * KA <= LAT_LDS, "the Z unit's LDS fits");
+  WTRACE(0);
+  // the part's lists (the scan unit was dispatched before any producer)
+  wait_flag(d, d.zflag + d.nzu + part, epoch);
+  const unsigned* const off = d.csr + (int64_t)part * (tabw + 1 + d.ld);
+  const unsigned* const mem = off + tabw + 1;
+  auto ldu = [](const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  int lo[2] = {0, 0}, nm[2] = {0, 0};
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int64_t q = c * ZQ + ql + hh * ZH;
+    if (q < ny) {
+      lo[hh] = (int)ldu(off + q);
+      nm[hh] = (int)ldu(off + q + 1) - lo[hh];
+    }
+  }
+  WTRACE(1);
+  double acc[2][KA];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int a = 0; a < KA; ++a) acc[hh][a] = 0.0;
+  const int mmax = nm[0] > nm[1] ? nm[0] : nm[1];
+  double ex[2][ZMB];
+  int jm[2][ZMB];
+  auto load_ex = [&](int m0) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int m = 0; m < ZMB; ++m) {
+        const bool in = m0 + m < nm[hh];
+        const unsigned pk = in ? ldu(mem + (hh ? lo[1] : lo[0]) + m0 + m) : 0u;
+        jm[hh][m] = (int)(pk & 0xffffu);
+        ex[hh][m] = in ? axr[(int64_t)(pk >> 16) * tabw] : 0.0;
+      }
+  };
+  load_ex(0);
+  wait_phase(d, d.ldone, epoch);   // w of every block (every wave: a barrier)
+  WTRACE(3);
+  for (int m0 = 0; m0 < mmax; m0 += ZMB) {
+    if (m0 > 0) load_ex(m0);
+    {
+      // the batch's coefficients w[j][a] c_j into the wave's LDS (the wave's rows
+      // hold the same members in every lane of a group: lane e takes element e)
+      constexpr int NE = (2 * ZMB * KA + 63) / 64;
+      double v[NE];
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = lane + 64 * i;
+        const int hh = e / (ZMB * KA), m = (e / KA) % ZMB, a = e % KA;
+        v[i] = 0.0;
+        if (e < 2 * ZMB * KA && m0 + m < (hh ? nm[1] : nm[0])) {
+          const int64_t j = (int64_t)(ldu(mem + (hh ? lo[1] : lo[0]) + m0 + m) & 0xffffu);
+          v[i] = ldx<true>(&wv[j * KINC + a]) * coef(j);   // L2-served: stored in this launch
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NE; ++i)
+        if (lane + 64 * i < 2 * ZMB * KA) cw[lane + 64 * i] = v[i];
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int m = 0; m < ZMB; ++m)
+        if (m0 + m < nm[hh]) {
+#pragma unroll
+          for (int a = 0; a < KA; ++a) acc[hh][a] = __builtin_fma(cw[(hh * ZMB + m) * KA + a], ex[hh][m], acc[hh][a]);
+        }
+  }
+  (void)jm;
+  WTRACE(4);
+  // this unit's virtual rows (v = c, c + nu, ...; the padding rows up to ZKS: zero):
+  // Z row = w[j][a] (c_j ex_j(ix)), group ql == 0
+  {
+    const int64_t nv = (int64_t)__hip_atomic_load(zvl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t nv8 = (nv + ZKS - 1) / ZKS * ZKS;
+    if (ql == 0)
+      for (int64_t v = c; v < nv8; v += nu) {
+        double* zr = zb + ((part * zrows + zq8 + v) * tabw + ix) * KA;
+        if (v < nv) {
+          const int64_t j = __hip_atomic_load(zvl + 1 + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const double e = d.tab[(2 * part) * tstride + j * tabw + ix];
+#pragma unroll
+          for (int a = 0; a < KA; ++a) stx<true>(zr + a, ldx<true>(&wv[j * KINC + a]) * e);
+        } else {
+#pragma unroll
+          for (int a = 0; a < KA; ++a) stx<true>(zr + a, 0.0);
+        }
+      }
+  }
+  WTRACE(5);
+  // the rows through LDS (512 contiguous bytes per store), as lat_zunit
+  double* const zst = sm;   // [ZH][tabw][KA]
+  static_assert(4096 + 16 <= LAT_LDS, "the Z rows' staging fits");
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < KA; ++a) zst[(ql * tabw + ix) * KA + a] = acc[hh][a];
+    __syncthreads();
+    const int64_t q0 = c * ZQ + hh * ZH;
+    const int64_t nrow = ny - q0 < ZH ? ny - q0 : ZH;
+    double* const zr = zb + (part * zrows + q0) * tabw * KA;
+    if (d.lat_g2) {
+      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) zr[e] = zst[e];
+    } else {
+      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) stx<true>(zr + e, zst[e]);
+    }
+  }
+  if (d.lat_g2) {
+    WTRACE(6);
+    WTRACE(2);
+    return;
+  }
+  drain_stores();
+  __syncthreads();
+  WTRACE(6);
+  if (tid == 0) {
+    publish(d.zflag + zu, epoch);
+    arrive_phase(d.ldone + 2, epoch, d.nzu);
+  }
+  WTRACE(2);
+}
+
 // g3 (k_lat_gemm3 follows): in place of the Z units, one scan unit per part of the
 // GP lists the part's training rows j < n0 on the lattice by lattice y-row q, in
 // row order within each q -- the order in which a Z unit sums them -- as CSR in
@@ -968,20 +1125,22 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
 // sort: the buckets' sizes (LDS atomics), their offsets (a wave scan), then the
 // rows in chunks of NT in row order, each row's place = its bucket's running
 // offset + the same bucket's rows in the chunk's earlier waves + its rank among
-// its wave's lanes of that bucket (eight ballots). Plain stores: read by the next
-// launch.
-constexpr int SCAN_B = 160;   // buckets held: ny <= 128 lattice rows + the virtual one
-__device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm) {
+// its wave's lanes of that bucket (nine ballots). Write-through stores: the Z units
+// of the same launch read the lists (lat_zcsr), or the next launch does (g3).
+constexpr int SCAN_B = 264;   // buckets held: ny <= 256 lattice rows + the virtual one
+// (flag: where the unit publishes that its lists are stored; every output is stored
+// write-through, so the Z units of this launch may read them after the flag)
+__device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm, unsigned* flag) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t j_lo = part == 1 ? d.NL : 0;
-  const int n = (int)(d.n0 - j_lo);   // <= LAT_SCAN_MAX (the host's g3 bound)
-  const int ny = d.lat.ny;            // <= 128 (the host's bound: 128-wide tables)
-  int* const lq = reinterpret_cast<int*>(sm);   // [LAT_SCAN_MAX] bucket << 16 | px
-  int* const run = lq + LAT_SCAN_MAX;           // [SCAN_B] the buckets' next places
+  const int n = (int)(d.n0 - j_lo);
+  const int ny = d.lat.ny;            // <= 256 (the host's bound)
+  int* const run = reinterpret_cast<int*>(sm);  // [SCAN_B] the buckets' next places
   int* const wc = run + SCAN_B;                 // [NT / 64][SCAN_B] this chunk's counts
   int* const vbase = wc + (NT / 64) * SCAN_B;   // the virtual bucket's first place
-  static_assert((LAT_SCAN_MAX + (1 + NT / 64) * SCAN_B + 2) / 2 <= LAT_LDS, "the scan unit's LDS fits");
+  static_assert(((1 + NT / 64) * SCAN_B + 2) / 2 <= LAT_LDS, "the scan unit's LDS fits");
   const int* const lidx = d.lidx + j_lo;
+  auto bucket = [&](int li) { return li >= 0 ? (li >> 16) : ny; };
   for (int b = tid; b < (1 + NT / 64) * SCAN_B; b += NT) run[b] = 0;
   __syncthreads();
   constexpr int SU = 8;   // rows loaded ahead per thread
@@ -993,16 +1152,14 @@ __device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm) 
       li[u] = e < n ? lidx[e] : -2;
     }
 #pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      if (li[u] == -2) continue;
-      const int b = li[u] >= 0 ? (li[u] >> 16) : ny;
-      lq[e0 + u * NT + tid] = (b << 16) | (li[u] >= 0 ? (li[u] & 0xffff) : 0);
-      __hip_atomic_fetch_add(run + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    for (int u = 0; u < SU; ++u)
+      if (li[u] != -2) __hip_atomic_fetch_add(run + bucket(li[u]), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   unsigned* const off = d.csr + (int64_t)part * (d.tabw + 1 + d.ld);
   unsigned* const mem = off + d.tabw + 1;
+  auto st_u = [](unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto st_i = [](int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   if (wv == 0) {   // exclusive offsets of buckets 0 .. ny (ny: the virtual rows)
     int base = 0;
     for (int s0 = 0; s0 <= ny; s0 += 64) {
@@ -1016,7 +1173,7 @@ __device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm) 
       }
       if (b <= ny) {
         run[b] = base + x - v;
-        off[b] = (unsigned)(base + x - v);
+        st_u(off + b, (unsigned)(base + x - v));
         if (b == ny) *vbase = base + x - v;
       }
       base += __shfl(x, 63);
@@ -1029,11 +1186,11 @@ __device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm) 
   for (int c0 = 0; c0 < n; c0 += NT) {
     const int e = c0 + tid;
     const bool valid = e < n;
-    const int key = valid ? lq[e] : 0;
-    const int b = key >> 16;
+    const int li = valid ? lidx[e] : 0;
+    const int b = bucket(li);
     unsigned long long mask = __ballot(valid);
 #pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
+    for (int bit = 0; bit < 9; ++bit) {
       const unsigned long long bb = __ballot((b >> bit) & 1);
       mask &= ((b >> bit) & 1) ? bb : ~bb;
     }
@@ -1044,10 +1201,10 @@ __device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm) 
       int pos = run[b] + rank;
       for (int w2 = 0; w2 < wv; ++w2) pos += wc[w2 * SCAN_B + b];
       const int j = (int)j_lo + e;
-      if (b < ny) mem[pos] = ((unsigned)(key & 0xffff) << 16) | (unsigned)j;
-      else zvl[1 + pos - vb] = j;
-      // the row's place for the w units' reducers (read in this launch: write-through)
-      __hip_atomic_store(place + j, b < ny ? pos : -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (b < ny) st_u(mem + pos, ((unsigned)(li & 0xffff) << 16) | (unsigned)j);
+      else st_i(zvl + 1 + pos - vb, j);
+      // the row's place (the g3 w reducers store its c w row there)
+      st_i(place + j, b < ny ? pos : -1);
     }
     __syncthreads();
     for (int bb = tid; bb <= ny; bb += NT) {
@@ -1062,11 +1219,11 @@ __device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm) 
     __syncthreads();
   }
   const int nv = n - vb, nv8 = (nv + ZKS - 1) / ZKS * ZKS;
-  for (int v = nv + tid; v < nv8; v += NT) zvl[1 + v] = (int)j_lo;
-  if (tid == 0) zvl[0] = nv;
+  for (int v = nv + tid; v < nv8; v += NT) st_i(zvl + 1 + v, (int)j_lo);
+  if (tid == 0) st_i(zvl, nv);
   drain_stores();
   __syncthreads();
-  if (tid == 0) publish(d.zflag + part, d.epoch);   // the places are stored
+  if (tid == 0) publish(flag, d.epoch);   // the lists and places are stored
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n in [0, 4], then the raw barrier (no
@@ -1576,11 +1733,19 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
   if (d.lat_g3) {
     // g3: the scan units first (they wait for nothing), then producers and w units
     if (role < d.nzu) {
-      lat_scan(d, (int)role, sm);
+      lat_scan(d, (int)role, sm, d.zflag + role);
       return;
     }
     role -= d.nzu;
     if (role >= np + d.nwu) return;
+  } else if (d.lat_zcsr) {
+    // the scan units first (they wait for nothing), then the usual roles
+    const int P = d.hp.kind == 0 ? 1 : 2;
+    if (role < P) {
+      lat_scan(d, (int)role, sm, d.zflag + d.nzu + role);
+      return;
+    }
+    role -= P;
   }
   if (role < np) {
     inc_producer_role<VT>(d, role, sm, reinterpret_cast<int*>(sm + LAT_LDS),
@@ -1599,7 +1764,8 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     }
     return;
 #endif
-    lat_zunit<KA>(d, role - np - d.nwu, sm);
+    if (d.lat_zcsr) lat_zunit_csr<KA>(d, role - np - d.nwu, sm);
+    else lat_zunit<KA>(d, role - np - d.nwu, sm);
     return;
   }
 #ifdef MFGP_DIAG_LATNOGEMM   // diagnostic build: producers, w and Z only (timing only)

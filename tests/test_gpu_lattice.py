@@ -511,3 +511,63 @@ def test_lattice_gemm3_equals_gemm2(monkeypatch, dtype):
         for step, (sa, sb) in enumerate(zip(ra, rb)):
             for xa, xb in zip(sa, sb):
                 assert np.array_equal(xa, xb), (B, step)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_lattice_zcsr_equals_zunits(monkeypatch, dtype):
+    """Z units reading the scan units' member lists (MFGP_LAT_ZCSR=1, the default
+    where each Z unit would bucket many rows: configs[4]) against Z units that bucket
+    the rows themselves (MFGP_LAT_ZCSR=0): the same members in the same row order,
+    the same FMAs, so the same bits -- mean, variance, fused max / argmax -- over
+    ragged batches with off-lattice rows (virtual Z rows, their padding) and appends
+    of 8, 3 and 12 rows (KA = 8 and 16), both GEMM forms."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    hyp = _hyp("australia8_mf")
+    G = 64
+    dt = _lib.F32 if dtype == "f32" else _lib.F64
+
+    def run(ctx, B):
+        models, data = [], []
+        for i in range(B):
+            nl, nh = 200 + 11 * i, 260 - 5 * i
+            Xs, X, y = _data(G, nl + nh + 40, seed=290 + i)
+            X[7:12] += 0.27 / (G - 1)   # off-lattice lofi rows
+            X[nl + 2] += 0.31 / (G - 1)   # and a hifi one
+            models.append(_model(ctx, hyp, X[:nl + nh], y[:nl + nh], nl, Xs, dtype=dt))
+            data.append((X, y, nl, nl + nh))
+        M = Xs.shape[0]
+        mu = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        var = torch.empty_like(mu)
+        vmax = torch.empty(B, dtype=torch.float64, device="cuda")
+        vam = torch.empty(B, dtype=torch.int64, device="cuda")
+        _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
+        out = []
+        for k in (8, 3, 12):
+            Xn = np.concatenate([X[n:n + k] for X, _, _, n in data])
+            yn = np.concatenate([y[n:n + k] for _, y, _, n in data])
+            Xt = torch.from_numpy(np.ascontiguousarray(Xn)).cuda()
+            yt = torch.from_numpy(np.ascontiguousarray(yn)).cuda()
+            _lib.batch_append_predict(models, Xt.data_ptr(), yt.data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
+                                      vmax_ptr=vmax.data_ptr(), vargmax_ptr=vam.data_ptr())
+            data = [(X, y, nl, n + k) for X, y, nl, n in data]
+            out.append((mu.cpu().numpy(), var.cpu().numpy(), vmax.cpu().numpy(), vam.cpu().numpy()))
+        assert all(m.stats()["lattice"] == 3 for m in models), [m.stats() for m in models]
+        assert all(m.stats()["lattice_virtual"] > 0 for m in models), [m.stats() for m in models]
+        ctx.synchronize()
+        return out
+
+    for B, g2 in ((1, "0"), (3, "0"), (3, "1")):
+        monkeypatch.setenv("MFGP_LAT_GEMM2", g2)
+        monkeypatch.setenv("MFGP_LAT_ZCSR", "0")
+        a = _lib.Context(0)
+        monkeypatch.setenv("MFGP_LAT_ZCSR", "1")
+        b = _lib.Context(0)
+        monkeypatch.delenv("MFGP_LAT_ZCSR")
+        monkeypatch.delenv("MFGP_LAT_GEMM2")
+        a.set_lattice("force")
+        b.set_lattice("force")
+        ra, rb = run(a, B), run(b, B)
+        for step, (sa, sb) in enumerate(zip(ra, rb)):
+            for xa, xb in zip(sa, sb):
+                assert np.array_equal(xa, xb), (B, g2, step)
