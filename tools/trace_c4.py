@@ -49,7 +49,7 @@ tr = raw[:, :7].astype(np.float64)
 used = tr[:, 0] > 0
 t0 = tr[used, 0].min()
 tr = np.where(tr > 0, (tr - t0) / 100.0, np.nan)
-role = np.arange(NWG) // B
+role = np.arange(NWG) // B - int(os.environ.get("TRACE_ROFF", "2"))   # (the scan units: the first roles)
 n0 = NL + NH0
 nprod = -(-n0 // 128)
 C = -(-n0 // 16)
