@@ -37,8 +37,10 @@ extern "C" {
                                L_hi,rho,noise_lo,noise_hi] (all log-scaled, simulator.py:53-56)     */
 #define MFGP_F64 0
 #define MFGP_F32 1          /* BASELINE configs[4]: the resident V = L^-1 psi^T stored and streamed
-                               in fp32; factor, solves and reductions fp64. Tolerance vs the fp64
-                               oracle: oracle/gp_oracle.py parity_errors_f32 (F32_TOL = 1e-4) */
+                               in fp32, and the lattice step's F = L^-1 streamed in fp32 (built in
+                               fp64, rounded once per build); factor, solves and reductions fp64.
+                               Tolerance vs the fp64 oracle: oracle/gp_oracle.py parity_errors_f32
+                               (F32_TOL = 1e-4) */
 
 #define MFGP_ASYNC 1        /* batch flag: do not synchronise; status via mfgp_ctx_synchronize */
 
