@@ -988,21 +988,30 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
   const double* const axr = d.axt + (2 * part) * (tabw + 1) * tabw + ix;   // ex(p, ix) at axr[p * tabw]
   const double cL = h.kind == 0 ? h.sL : h.rho * h.sL, cLH = h.rho2 * h.sL;
   auto coef = [&](int64_t j) { return part == 1 ? h.sH : (j < NL ? cL : cLH); };
-  double* const cw = sm + w * 2 * ZMB * KA;   // the waves' coefficient batches [4][2][ZMB][KA]
-  static_assert(4 * 2 * ZMB * KA <= LAT_LDS, "the Z unit's LDS fits");
+  // LDS: the unit's members in chunks of ZCH (their rows' lists are contiguous in the
+  // CSR): training row j and axis column px, then (after the w wait) the c w rows
+  constexpr int ZCH = 256;
+  int* const mj = reinterpret_cast<int*>(sm);        // [ZCH]
+  int* const mpx = mj + ZCH;                          // [ZCH]
+  double* const cws = sm + ZCH;                       // [ZCH][KA]
+  static_assert(ZCH + ZCH * KA <= LAT_LDS, "the Z unit's LDS fits");
   WTRACE(0);
   // the part's lists (the scan unit was dispatched before any producer)
   wait_flag(d, d.zflag + d.nzu + part, epoch);
   const unsigned* const off = d.csr + (int64_t)part * (tabw + 1 + d.ld);
   const unsigned* const mem = off + tabw + 1;
   auto ldu = [](const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  int lo[2] = {0, 0}, nm[2] = {0, 0};
+  // the unit's rows c ZQ .. c ZQ + ZQ - 1 (those below ny): members [u_lo, u_hi)
+  const int64_t qa = c * ZQ, qb = qa + ZQ < ny ? qa + ZQ : ny;
+  const int u_lo = qa < ny ? (int)ldu(off + qa) : 0;
+  const int u_hi = qa < ny ? (int)ldu(off + qb) : 0;
+  int lo[2] = {0, 0}, nm[2] = {0, 0};   // this thread group's two rows, relative to u_lo
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int64_t q = c * ZQ + ql + hh * ZH;
     if (q < ny) {
-      lo[hh] = (int)ldu(off + q);
-      nm[hh] = (int)ldu(off + q + 1) - lo[hh];
+      lo[hh] = (int)ldu(off + q) - u_lo;
+      nm[hh] = (int)ldu(off + q + 1) - u_lo - lo[hh];
     }
   }
   WTRACE(1);
@@ -1011,54 +1020,79 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
   for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
     for (int a = 0; a < KA; ++a) acc[hh][a] = 0.0;
-  const int mmax = nm[0] > nm[1] ? nm[0] : nm[1];
-  double ex[2][ZMB];
-  int jm[2][ZMB];
-  auto load_ex = [&](int m0) {
+  bool waited = false;
+  for (int c0 = 0; c0 < u_hi - u_lo; c0 += ZCH) {
+    const int cn = u_hi - u_lo - c0 < ZCH ? u_hi - u_lo - c0 : ZCH;
+    __syncthreads();   // (the previous chunk is summed)
+    for (int e = tid; e < cn; e += NT) {
+      const unsigned pk = ldu(mem + u_lo + c0 + e);
+      mj[e] = (int)(pk & 0xffffu);
+      mpx[e] = (int)(pk >> 16);
+    }
+    __syncthreads();
+    // this thread's members in the chunk, per row: [b0, b1) relative to the chunk
+    int b0[2], b1[2];
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < 2; ++hh) {
+      b0[hh] = lo[hh] - c0 > 0 ? lo[hh] - c0 : 0;
+      const int e1 = lo[hh] + nm[hh] - c0;
+      b1[hh] = e1 < cn ? e1 : cn;
+      if (b1[hh] < b0[hh]) b1[hh] = b0[hh];
+    }
+    const int mmax = (b1[0] - b0[0]) > (b1[1] - b0[1]) ? (b1[0] - b0[0]) : (b1[1] - b0[1]);
+    double ex[2][ZMB];
+    auto load_ex = [&](int m0) {
 #pragma unroll
-      for (int m = 0; m < ZMB; ++m) {
-        const bool in = m0 + m < nm[hh];
-        const unsigned pk = in ? ldu(mem + (hh ? lo[1] : lo[0]) + m0 + m) : 0u;
-        jm[hh][m] = (int)(pk & 0xffffu);
-        ex[hh][m] = in ? axr[(int64_t)(pk >> 16) * tabw] : 0.0;
-      }
-  };
-  load_ex(0);
-  wait_phase(d, d.ldone, epoch);   // w of every block (every wave: a barrier)
-  WTRACE(3);
-  for (int m0 = 0; m0 < mmax; m0 += ZMB) {
-    if (m0 > 0) load_ex(m0);
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int m = 0; m < ZMB; ++m) {
+          const int e = b0[hh] + m0 + m;
+          ex[hh][m] = e < b1[hh] ? axr[(int64_t)mpx[e] * tabw] : 0.0;
+        }
+    };
+    load_ex(0);
+    if (!waited) {
+      wait_phase(d, d.ldone, epoch);   // w of every block (every wave: a barrier)
+      WTRACE(3);
+      waited = true;
+    }
+    // the chunk's c w rows into LDS, one element per thread at a time (all in flight)
     {
-      // the batch's coefficients w[j][a] c_j into the wave's LDS (the wave's rows
-      // hold the same members in every lane of a group: lane e takes element e)
-      constexpr int NE = (2 * ZMB * KA + 63) / 64;
+      constexpr int NE = (ZCH * KA + NT - 1) / NT;
       double v[NE];
 #pragma unroll
-      for (int i = 0; i < NE; ++i) {
-        const int e = lane + 64 * i;
-        const int hh = e / (ZMB * KA), m = (e / KA) % ZMB, a = e % KA;
-        v[i] = 0.0;
-        if (e < 2 * ZMB * KA && m0 + m < (hh ? nm[1] : nm[0])) {
-          const int64_t j = (int64_t)(ldu(mem + (hh ? lo[1] : lo[0]) + m0 + m) & 0xffffu);
-          v[i] = ldx<true>(&wv[j * KINC + a]) * coef(j);   // L2-served: stored in this launch
+      for (int i2 = 0; i2 < NE; ++i2) {
+        const int e = tid + NT * i2, m = e / KA, a = e % KA;
+        v[i2] = 0.0;
+        if (m < cn) {
+          const int64_t j = mj[m];
+          v[i2] = ldx<true>(&wv[j * KINC + a]) * coef(j);   // L2-served: stored in this launch
         }
       }
+      __syncthreads();   // (every thread has read mj: cws may be written)
 #pragma unroll
-      for (int i = 0; i < NE; ++i)
-        if (lane + 64 * i < 2 * ZMB * KA) cw[lane + 64 * i] = v[i];
+      for (int i2 = 0; i2 < NE; ++i2)
+        if (tid + NT * i2 < ZCH * KA) cws[tid + NT * i2] = v[i2];
+      __syncthreads();
     }
+    for (int m0 = 0; m0 < mmax; m0 += ZMB) {
+      if (m0 > 0) load_ex(m0);
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+      for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-      for (int m = 0; m < ZMB; ++m)
-        if (m0 + m < nm[hh]) {
+        for (int m = 0; m < ZMB; ++m) {
+          const int e = b0[hh] + m0 + m;
+          if (e < b1[hh]) {
 #pragma unroll
-          for (int a = 0; a < KA; ++a) acc[hh][a] = __builtin_fma(cw[(hh * ZMB + m) * KA + a], ex[hh][m], acc[hh][a]);
+            for (int a = 0; a < KA; ++a) acc[hh][a] = __builtin_fma(cws[e * KA + a], ex[hh][m], acc[hh][a]);
+          }
         }
+    }
   }
-  (void)jm;
+  if (!waited) {
+    wait_phase(d, d.ldone, epoch);   // (a unit without members still waits: its virtual rows need w)
+    WTRACE(3);
+  }
   WTRACE(4);
   // this unit's virtual rows (v = c, c + nu, ...; the padding rows up to ZKS: zero):
   // Z row = w[j][a] (c_j ex_j(ix)), group ql == 0
