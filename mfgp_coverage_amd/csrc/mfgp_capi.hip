@@ -2287,7 +2287,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         // row of its part: nzu x n0 per GP; configs[4] 256 x 8184: 17.8k -> 18.7k
         // GP-updates/s; the headline's 64 x 2040 is 1 % faster without)
         const bool zc = c->lat_zcsr > 0 || (c->lat_zcsr < 0 && nzu * fd.n0 >= (int64_t(1) << 20));
-        fd.lat_zcsr = (!g3 && zc && m->lat.ny <= 256 && m->ld <= 65535) ? 1 : 0;
+        fd.lat_zcsr = (!g3 && zc && ka == 8 && m->lat.ny <= 256 && m->ld <= 65535) ? 1 : 0;
         fd.csr = m->csr;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }

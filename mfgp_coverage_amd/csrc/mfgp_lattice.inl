@@ -1798,8 +1798,13 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     }
     return;
 #endif
-    if (d.lat_zcsr) lat_zunit_csr<KA>(d, role - np - d.nwu, sm);
-    else lat_zunit<KA>(d, role - np - d.nwu, sm);
+    // (the member-list form at KA = 8 only: at 16 its registers spilled the kernel)
+    if constexpr (KA == 8) {
+      if (d.lat_zcsr) lat_zunit_csr<KA>(d, role - np - d.nwu, sm);
+      else lat_zunit<KA>(d, role - np - d.nwu, sm);
+    } else {
+      lat_zunit<KA>(d, role - np - d.nwu, sm);
+    }
     return;
   }
 #ifdef MFGP_DIAG_LATNOGEMM   // diagnostic build: producers, w and Z only (timing only)
