@@ -116,9 +116,8 @@ struct mfgp_ctx {
   bool concurrent = false;
   bool sync_query = false;    // synchronise by polling hipStreamQuery first (MFGP_SYNC_QUERY)
   int rsplit_force = 0;       // one-pass predict row splits per cell group (0: the host's rule)
-  int lat_zcsr = -1;          // the Z units read member lists built by one scan unit per part
-                              // instead of bucketing every row themselves (-1: where that is
-                              // large; MFGP_LAT_ZCSR=0/1 forces it)
+  int lat_zcsr = 1;           // the Z units read member lists built by one scan unit per part
+                              // instead of bucketing every row themselves (MFGP_LAT_ZCSR=0: off)
   bool lat_g3 = false;        // the two-launch lattice step's second launch builds its own Z rows
                               // (k_lat_gemm3) where it applies (MFGP_LAT_G3=1; off by default until
                               // it beats k_lat_gemm2 at the headline)
@@ -2283,10 +2282,10 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.lat_g3 = g3 ? 1 : 0;
         // Z units reading the scan units' member lists (every lattice row count the scan
         // units bucket, rows and lattice indices within 16 bits)
-        // -- by default where the Z units' own bucketing is large (every unit scans every
-        // row of its part: nzu x n0 per GP; configs[4] 256 x 8184: 17.8k -> 18.7k
-        // GP-updates/s; the headline's 64 x 2040 is 1 % faster without)
-        const bool zc = c->lat_zcsr > 0 || (c->lat_zcsr < 0 && nzu * fd.n0 >= (int64_t(1) << 20));
+        // -- by default (the bucketing Z units scan every row of their part; with the
+        // lists: headline 93.2k -> 95.3k GP-updates/s, configs[4] 17.8k -> 19.3k)
+        const bool zc = c->lat_zcsr != 0;
+        (void)nzu;
         fd.lat_zcsr = (!g3 && zc && ka == 8 && m->lat.ny <= 256 && m->ld <= 65535) ? 1 : 0;
         fd.csr = m->csr;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
