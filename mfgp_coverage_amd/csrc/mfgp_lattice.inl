@@ -965,8 +965,7 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
 template <int KA>
 __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, double* sm) {
   constexpr int ZMB = KA == 8 ? MFGP_ZMB8 : 6;   // members per row q per load batch
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = threadIdx.x;
   const Hyp& h = d.hp;
   const int P = h.kind == 0 ? 1 : 2;
   const int64_t tabw = d.tabw;
