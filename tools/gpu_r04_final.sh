@@ -18,3 +18,6 @@ import json
 for f in ('r04_final_bench20', 'r04_final_bench', 'r04_final_configs4'):
     d = json.load(open(f'gpurun_out/{f}.json')); print(f, round(d['value']), round(1e3*d['ms_per_step'], 2), round(d['roofline']['frac'], 3), d.get('simulation', {}).get('value'))
 print(open('gpurun_out/r04_dropin.jsonl').read()[:200])"
+bash tools/profile_round.sh r04_final > gpurun_out/r04_final_prof.log 2>&1 || exit 1
+timeout -k 10 200 python -u tools/trace_lat.py tools/diaglib/libmfgp_stamps.so > gpurun_out/r04_final_trace_lat.txt 2>&1 || true
+echo profiled
