@@ -64,7 +64,9 @@ wr = nwu
 wch = wr
 _zq = 2 * 256 // (((G + 63) // 64) * 64)
 nzu = 2 * ((G + _zq - 1) // _zq)
-role = np.arange(NWG) // B - int(os.environ.get("TRACE_ROFF", "2"))   # (the two scan units: the first roles)
+role = np.arange(NWG) // B
+# the two scan units are the first roles of launch 1 (k_lat_gemm2's stamps sit at 1024 + tile)
+role = np.where(role >= 1024, role, role - int(os.environ.get("TRACE_ROFF", "2")))
 G2 = bool(used[role >= 1024].any())   # the GEMM as a second launch (k_lat_gemm2): roles 1024 + tile
 q = lambda a: " ".join(f"{np.nanpercentile(a, p):7.1f}" for p in (0, 10, 50, 90, 100)) if np.isfinite(a).any() else "-"
 print(f"B={B} ({nwu} w units, {nzu} Z units per GP): percentiles 0/10/50/90/100 (us from the first WG start); last WG end {np.nanmax(tr):.1f}")
