@@ -108,6 +108,14 @@ struct mfgp_ctx {
                               // tiles); MFGP_LAT_GEMM2, diagnostics and tests
   bool trinv_columns = false;  // F by the block-column k_trinv_f instead of recursive doubling (MFGP_TRINV_COLUMNS)
   int factor_depth = 4;        // 64-column steps per trailing-update pass of the factor (MFGP_FACTOR_DEPTH; 1: one-level)
+  // look-ahead factor (MFGP_FACTOR_LOOKAHEAD=1; off by default: measured no faster,
+  // DESIGN.md §6.2): a group's update of the columns past the next group runs on
+  // `side` while the next group's diagonal / panel chain runs on `stream` (or on
+  // `crit`, CU-masked)
+  bool factor_look = false;
+  hipStream_t side = nullptr, crit = nullptr;
+  int factor_crit_cus = 64;     // CUs of the chain's stream (0: no CU masks)
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
   // launches of this context may run concurrently with other contexts' (several
   // streams on one GPU, mfgp_ctx_set_concurrent): no launch may rely on all of its
@@ -839,27 +847,64 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   // group's FD steps in one pass (k_syrk_blk, FD deep) -- bit-equal to the
   // one-level order, each trailing tile read and written once per group.
   const int FD = std::max(1, c->factor_depth);
+  // Look-ahead (FD > 1): after group g's steps, its update of the next group's
+  // columns runs on the critical stream and its update of every column past that
+  // on c->side, overlapping group g + 1's chain (which touches only its own
+  // columns). Each trailing tile still takes the groups' contributions in group
+  // order -- the side pass of group g - 1 is joined before group g's look-ahead
+  // pass writes the next group's tiles -- so the factor is bit-equal.
+  const bool look = FD > 1 && c->factor_look && c->side;
+  // With CU masks (c->crit, MFGP_FACTOR_CRIT_CUS) the chain runs on its own CUs,
+  // so the side pass's MFMA tiles do not share SIMDs with the latency-bound
+  // diagonal / panel kernels.
+  hipStream_t cs = c->stream;
+  if (look && c->crit) {
+    HIP_TRY(hipEventRecord(c->fork_ev, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->crit, c->fork_ev, 0));
+    cs = c->crit;
+  }
+  bool pending = false;
   for (int64_t K0 = 0; K0 < max_nb; K0 += FD) {
     const int64_t K1 = std::min<int64_t>(K0 + FD, max_nb);
     for (int64_t kb = K0; kb < K1; ++kb) {
-      HIP_TRY(launch_potrf_diag(dd, count, (int)kb, 0, c->stream));
+      HIP_TRY(launch_potrf_diag(dd, count, (int)kb, 0, cs));
       const int64_t below = max_nb - kb - 1;
       if (below <= 0) continue;
-      HIP_TRY(launch_panel(dd, count, (int)kb, below, c->stream));
+      HIP_TRY(launch_panel(dd, count, (int)kb, below, cs));
       const int64_t jmax = std::min<int64_t>(K0 + FD - 1, max_nb - 1);
       if (FD == 1) {
-        HIP_TRY(launch_syrk(dd, count, (int)kb, below * (below + 1) / 2, 0, c->stream));
+        HIP_TRY(launch_syrk(dd, count, (int)kb, below * (below + 1) / 2, 0, cs));
       } else if (jmax >= kb + 1) {
         int64_t tiles = 0;
         for (int64_t j = kb + 1; j <= jmax; ++j) tiles += max_nb - j;
-        HIP_TRY(launch_syrk_blk(dd, count, (int)kb, 1, (int)(kb + 1), (int)jmax, tiles, c->stream));
+        HIP_TRY(launch_syrk_blk(dd, count, (int)kb, 1, (int)(kb + 1), (int)jmax, tiles, cs));
       }
     }
     const int64_t jmin = K0 + FD;
-    if (FD > 1 && jmin < max_nb) {
+    if (look && jmin < max_nb) {
+      if (pending) HIP_TRY(hipStreamWaitEvent(cs, c->join_ev, 0));
+      pending = false;
+      const int64_t j1 = std::min<int64_t>(jmin + FD - 1, max_nb - 1);
+      int64_t tiles = 0;
+      for (int64_t j = jmin; j <= j1; ++j) tiles += max_nb - j;
+      HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)jmin, (int)j1, tiles, cs));
+      if (j1 + 1 < max_nb) {
+        HIP_TRY(hipEventRecord(c->fork_ev, cs));
+        HIP_TRY(hipStreamWaitEvent(c->side, c->fork_ev, 0));
+        const int64_t T = max_nb - (j1 + 1);
+        HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)(j1 + 1), INT32_MAX, T * (T + 1) / 2, c->side));
+        HIP_TRY(hipEventRecord(c->join_ev, c->side));
+        pending = true;
+      }
+    } else if (FD > 1 && jmin < max_nb) {
       const int64_t T = max_nb - jmin;
-      HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)jmin, INT32_MAX, T * (T + 1) / 2, c->stream));
+      HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)jmin, INT32_MAX, T * (T + 1) / 2, cs));
     }
+  }
+  if (pending) HIP_TRY(hipStreamWaitEvent(cs, c->join_ev, 0));
+  if (cs != c->stream) {
+    HIP_TRY(hipEventRecord(c->fork_ev, cs));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->fork_ev, 0));
   }
   int64_t max_n = 0;
   for (int i = 0; i < count; ++i) max_n = std::max(max_n, hd[i].N);
@@ -1353,6 +1398,25 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (const char* e = std::getenv("MFGP_LAT_GEMM2")) c->lat_gemm2 = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("MFGP_TRINV_COLUMNS")) c->trinv_columns = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_FACTOR_DEPTH")) c->factor_depth = std::max(1, std::min(16, std::atoi(e)));
+  if (const char* e = std::getenv("MFGP_FACTOR_LOOKAHEAD")) c->factor_look = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MFGP_FACTOR_CRIT_CUS")) c->factor_crit_cus = std::max(0, std::atoi(e));
+  if (!c->factor_look) {
+    // no extra streams (hardware queues) unless the look-ahead factor is asked for
+  } else if (c->factor_crit_cus > 0 && c->factor_crit_cus < c->ncu) {
+    // every (ncu / crit)-th CU for the chain (spread over the XCDs), the rest for
+    // the side pass
+    const int step = c->ncu / c->factor_crit_cus, nw = (c->ncu + 31) / 32;
+    std::vector<uint32_t> mc(nw, 0u), ms(nw, 0u);
+    for (int i = 0; i < c->ncu; ++i) (i % step == 0 ? mc : ms)[i >> 5] |= 1u << (i & 31);
+    HIP_TRY(hipExtStreamCreateWithCUMask(&c->crit, (uint32_t)nw, mc.data()));
+    HIP_TRY(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)nw, ms.data()));
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  }
+  if (c->factor_look) {
+    HIP_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+  }
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
     const int v = std::atoi(e);
@@ -1376,6 +1440,12 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
   (void)drain_timing(c);
   for (auto e : c->pool) (void)hipEventDestroy(e);
   for (int i = 0; i < RING; ++i) (void)hipEventDestroy(c->ring_ev[i]);
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->crit) (void)hipStreamSynchronize(c->crit);
+  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->crit) (void)hipStreamDestroy(c->crit);
   if (c->ws) (void)hipFree(c->ws);
   if (c->vscr) (void)hipFree(c->vscr);
   if (c->d_ring) (void)hipFree(c->d_ring);
