@@ -138,11 +138,25 @@ def parse():
     return a
 
 
+def source_sha():
+    """sha256 (hex, 16 chars) of the library's sources (mfgp_coverage_amd/csrc/*, the
+    C header): the identity of the build a committed counter summary was collected on
+    (tools/summarize_profile.py writes it to profiles/<tag>_build.json)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "mfgp_coverage_amd", "csrc")
+    for f in sorted(os.listdir(csrc)) + ["../../include/mfgp_hip.h"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(kernel="k_predict", tag=None):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary (profiles/<round>_hbm_traffic.csv, written by tools/summarize_profile.py
-    from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x2 per the gfx950
-    correction of MI355X_MICROARCH.md section HBM)."""
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
+    (profiles/<round>_hbm_traffic.csv, written by tools/summarize_profile.py from
+    separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x2 per the gfx950 correction of
+    MI355X_MICROARCH.md section HBM) collected on THIS build: its profiles/<round>_build.json
+    must hold the current source_sha(). Returns (bytes, source) or (None, reason)."""
     import glob
     import csv
     import re
@@ -151,26 +165,37 @@ def pmc_traffic(kernel="k_predict", tag=None):
     files = [f for f in files if (f"_{tag}_" in os.path.basename(f)) == (tag is not None)
              and (tag is not None or "configs4" not in os.path.basename(f))]
     if not files:
-        return None, None
+        return None, "no committed PMC summary"
+    sha = source_sha()
+    same = []
+    for f in files:
+        bj = f[: -len("_hbm_traffic.csv")] + "_build.json"
+        try:
+            with open(bj) as fh:
+                if json.load(fh).get("src_sha") == sha:
+                    same.append(f)
+        except (OSError, ValueError):
+            pass
+    if not same:
+        return None, f"no PMC summary of this build (sources {sha}); newest: {os.path.relpath(files[-1], ROOT)}"
     # kernel: one name, or several (the launches of one step: their bytes add up)
     names = [kernel] if isinstance(kernel, str) else list(kernel)
     tot, found = 0.0, set()
-    with open(files[-1]) as f:
+    with open(same[-1]) as f:
         for row in csv.DictReader(f):
             for n in names:
                 if n not in found and re.search(rf"::{n}(?![A-Za-z0-9_])", row["Name"]):
                     tot += float(row["fetch_bytes_corrected"]) + float(row["write_bytes"])
                     found.add(n)
     if len(found) != len(names):
-        return None, None
-    return tot, os.path.relpath(files[-1], ROOT)
+        return None, f"{os.path.relpath(same[-1], ROOT)} lacks {sorted(set(names) - found)}"
+    return tot, f"{os.path.relpath(same[-1], ROOT)} (sources {sha})"
 
 
 def pmc_mfma(kernel):
     """MFMA utilisation of `kernel` from the newest committed rocprofv3 summary
     (profiles/<round>_mfma_util.csv, tools/summarize_profile.py): the busy cycles over
-    the kernel's own duration at the measured shader clock (mfma_util), and beside it
-    the GRBM-per-XCD form (mfma_util_grbm, unreliable for short dispatches)."""
+    the kernel's own duration at the measured shader clock."""
     import glob
     import csv
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_mfma_util.csv")))
@@ -180,9 +205,8 @@ def pmc_mfma(kernel):
         for row in csv.DictReader(f):
             if kernel in row["Name"]:
                 out = {"mfma_util": float(row["mfma_util"]), "source": os.path.relpath(files[-1], ROOT)}
-                for k in ("mfma_util_grbm", "sclk_ghz", "clock_ghz"):
-                    if k in row and row[k]:
-                        out[k] = float(row[k])
+                if row.get("sclk_ghz"):
+                    out["sclk_ghz"] = float(row["sclk_ghz"])
                 return out
     return None
 
@@ -672,6 +696,8 @@ def main():
         # the step's algorithmic bytes over the whole step's wall time (all sub-batches)
         step_bytes = roof["bytes_per_launch"] / shr
         roof["streams"] = inc["streams"]
+        if roof.get("traffic"):
+            roof["traffic_over_algorithmic"] = roof["traffic"] / roof["bytes_per_launch"]
         roof["step_aggregate_gbs"] = step_bytes / (elapsed / K) / 1e9
         roof["step_aggregate_frac"] = roof["step_aggregate_gbs"] / PEAK_HBM_GBS
         if default_cfg:

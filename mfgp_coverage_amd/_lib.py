@@ -346,14 +346,13 @@ class Model:
         device counters hold them (MF: summed over both kernel parts); {lattice_arg}:
         the lattice steps launched with their descriptors by value (k_inc_lat_arg);
         {lattice_g2}: the lattice steps whose GEMM and cells ran as a second launch
-        (k_lat_gemm2 or k_lat_gemm3); {post_copy}: batch predicts served from the resident
-        posterior because the model appended nothing (k_post_copy); {lattice_g3}: the
-        two-launch steps whose second launch built its own Z rows (k_lat_gemm3)."""
-        out = (ctypes.c_int64 * 14)()
-        check(lib().mfgp_model_stats(self.handle, out, 14))
+        (k_lat_gemm2); {post_copy}: batch predicts served from the resident posterior
+        because the model appended nothing (k_post_copy)."""
+        out = (ctypes.c_int64 * 13)()
+        check(lib().mfgp_model_stats(self.handle, out, 13))
         keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream",
                 "lattice_nx", "lattice_ny", "lattice", "lattice_virtual", "lattice_arg", "lattice_g2",
-                "post_copy", "lattice_g3")
+                "post_copy")
         return dict(zip(keys, (int(v) for v in out)))
 
     def sample_points(self, threshold, max_points):

@@ -44,6 +44,25 @@ int set_err(int code, const char* fmt, ...) {
                                          hipGetErrorString(e_), __FILE__, __LINE__);       \
   } while (0)
 
+// The context's device for the duration of one entry point, the caller's restored on
+// every return path (an entry point that set the device and left it
+// changed torch.cuda.current_device() in a multi-GPU process). dev < 0: no change.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (dev < 0 || hipGetDevice(&prev) != hipSuccess) {
+      prev = -1;
+      return;
+    }
+    if (prev == dev || hipSetDevice(dev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 constexpr int RING = 64;       // descriptor upload slots
 constexpr int MAXB = 256;      // GPs per launch
 constexpr int64_t MAX_FULL_CAP = 16319;   // largest training capacity the full predict serves (ld <= 16383)
@@ -108,27 +127,15 @@ struct mfgp_ctx {
                               // tiles); MFGP_LAT_GEMM2, diagnostics and tests
   bool trinv_columns = false;  // F by the block-column k_trinv_f instead of recursive doubling (MFGP_TRINV_COLUMNS)
   int factor_depth = 4;        // 64-column steps per trailing-update pass of the factor (MFGP_FACTOR_DEPTH; 1: one-level)
-  // look-ahead factor (MFGP_FACTOR_LOOKAHEAD=1; off by default: measured no faster,
-  // DESIGN.md §6.2): a group's update of the columns past the next group runs on
-  // `side` while the next group's diagonal / panel chain runs on `stream` (or on
-  // `crit`, CU-masked)
-  bool factor_look = false;
-  hipStream_t side = nullptr, crit = nullptr;
-  int factor_crit_cus = 64;     // CUs of the chain's stream (0: no CU masks)
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   bool lat_force = false;     // take it for small batches too (mfgp_ctx_set_lattice(2): tests)
   // launches of this context may run concurrently with other contexts' (several
   // streams on one GPU, mfgp_ctx_set_concurrent): no launch may rely on all of its
   // workgroups being resident at once -- the lattice step's GEMM runs as the second
   // launch (k_lat_gemm2, no cross-workgroup waits) instead of in-launch split-K tiles
   bool concurrent = false;
-  bool sync_query = false;    // synchronise by polling hipStreamQuery first (MFGP_SYNC_QUERY)
   int rsplit_force = 0;       // one-pass predict row splits per cell group (0: the host's rule)
   int lat_zcsr = 1;           // the Z units read member lists built by one scan unit per part
                               // instead of bucketing every row themselves (MFGP_LAT_ZCSR=0: off)
-  bool lat_g3 = false;        // the two-launch lattice step's second launch builds its own Z rows
-                              // (k_lat_gemm3) where it applies (MFGP_LAT_G3=1; off by default until
-                              // it beats k_lat_gemm2 at the headline)
   int64_t spin_us = 2000;     // host polling of mapped status words before a synchronise (MFGP_SPIN_US; 0: off)
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
@@ -194,8 +201,7 @@ struct mfgp_model {
   int64_t n_lattice_arg = 0;   // lattice steps launched with their descriptors by value (k_inc_lat_arg)
   int64_t n_lattice_g2 = 0;    // lattice steps whose GEMM and cells ran as a second launch (k_lat_gemm2)
   int64_t n_post_copy = 0;     // batch predicts served from the resident posterior (k_post_copy: nothing appended)
-  int64_t n_lattice_g3 = 0;    // two-launch lattice steps whose second launch built its Z rows (k_lat_gemm3)
-  unsigned* csr = nullptr;     // g3 buffer: member lists, places, c w rows (g3_bytes; mfgp_internal.h)
+  unsigned* csr = nullptr;     // the scan units' member lists (csr_bytes; mfgp_internal.h)
   int64_t csr_n = 0;           // (bytes)
   // state generation: a new factor from scratch, a new grid or new hyperparameters
   // start a new one (the resident posterior, F and the tables belong to one)
@@ -582,7 +588,6 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.wcnt = nullptr;
   d.lat_selfg = 0;
   d.lat_g2 = 0;
-  d.lat_g3 = 0;
   d.lat_zcsr = 0;
   d.csr = nullptr;
   d.hf = derive_hyp(m->kind, m->hyp, m->jitter);
@@ -677,7 +682,7 @@ bool lat_eligible(const mfgp_model* m, int64_t n0) {
 // F, the tables, w and the flags at the model's leading dimension (contents kept
 // across capacity growth: ensure_cap moves them)
 // Small buffers that every GEMM workgroup of the lattice step reads (the axis
-// tables, the g3 lists): whole 2 MiB units, so that they sit in one large page
+// tables, the member lists): whole 2 MiB units, so that they sit in one large page
 hipError_t hip_malloc_2m(void** p, size_t bytes) {
   const size_t unit = size_t(2) << 20;
   return hipMalloc(p, (bytes + unit - 1) / unit * unit);
@@ -779,11 +784,11 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     m->zb_w = tabw;
     m->zb_ka = ka;
   }
-  if (m->csr_n < g3_bytes(tabw, ld)) {
+  if (m->csr_n < csr_bytes(tabw, ld)) {
     HIP_TRY(hipStreamSynchronize(s));
     if (m->csr) HIP_TRY(hipFree(m->csr));
     m->csr = nullptr;
-    m->csr_n = g3_bytes(tabw, ld);
+    m->csr_n = csr_bytes(tabw, ld);
     HIP_TRY(hip_malloc_2m(reinterpret_cast<void**>(&m->csr), m->csr_n));
   }
   if (!m->ldone) {
@@ -847,23 +852,7 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   // group's FD steps in one pass (k_syrk_blk, FD deep) -- bit-equal to the
   // one-level order, each trailing tile read and written once per group.
   const int FD = std::max(1, c->factor_depth);
-  // Look-ahead (FD > 1): after group g's steps, its update of the next group's
-  // columns runs on the critical stream and its update of every column past that
-  // on c->side, overlapping group g + 1's chain (which touches only its own
-  // columns). Each trailing tile still takes the groups' contributions in group
-  // order -- the side pass of group g - 1 is joined before group g's look-ahead
-  // pass writes the next group's tiles -- so the factor is bit-equal.
-  const bool look = FD > 1 && c->factor_look && c->side;
-  // With CU masks (c->crit, MFGP_FACTOR_CRIT_CUS) the chain runs on its own CUs,
-  // so the side pass's MFMA tiles do not share SIMDs with the latency-bound
-  // diagonal / panel kernels.
   hipStream_t cs = c->stream;
-  if (look && c->crit) {
-    HIP_TRY(hipEventRecord(c->fork_ev, c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->crit, c->fork_ev, 0));
-    cs = c->crit;
-  }
-  bool pending = false;
   for (int64_t K0 = 0; K0 < max_nb; K0 += FD) {
     const int64_t K1 = std::min<int64_t>(K0 + FD, max_nb);
     for (int64_t kb = K0; kb < K1; ++kb) {
@@ -881,30 +870,10 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
       }
     }
     const int64_t jmin = K0 + FD;
-    if (look && jmin < max_nb) {
-      if (pending) HIP_TRY(hipStreamWaitEvent(cs, c->join_ev, 0));
-      pending = false;
-      const int64_t j1 = std::min<int64_t>(jmin + FD - 1, max_nb - 1);
-      int64_t tiles = 0;
-      for (int64_t j = jmin; j <= j1; ++j) tiles += max_nb - j;
-      HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)jmin, (int)j1, tiles, cs));
-      if (j1 + 1 < max_nb) {
-        HIP_TRY(hipEventRecord(c->fork_ev, cs));
-        HIP_TRY(hipStreamWaitEvent(c->side, c->fork_ev, 0));
-        const int64_t T = max_nb - (j1 + 1);
-        HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)(j1 + 1), INT32_MAX, T * (T + 1) / 2, c->side));
-        HIP_TRY(hipEventRecord(c->join_ev, c->side));
-        pending = true;
-      }
-    } else if (FD > 1 && jmin < max_nb) {
+    if (FD > 1 && jmin < max_nb) {
       const int64_t T = max_nb - jmin;
       HIP_TRY(launch_syrk_blk(dd, count, (int)K0, (int)(K1 - K0), (int)jmin, INT32_MAX, T * (T + 1) / 2, cs));
     }
-  }
-  if (pending) HIP_TRY(hipStreamWaitEvent(cs, c->join_ev, 0));
-  if (cs != c->stream) {
-    HIP_TRY(hipEventRecord(c->fork_ev, cs));
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->fork_ev, 0));
   }
   int64_t max_n = 0;
   for (int i = 0; i < count; ++i) max_n = std::max(max_n, hd[i].N);
@@ -1053,7 +1022,6 @@ int ensure_spec_out(mfgp_model* m) {
       g_view_pool.erase(g_view_pool.begin() + (long)best);
     }
   }
-  HIP_TRY(hipSetDevice(c->device));   // the mapping below is the model's device's
   if (m->spec_out) {
     void* dev = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dev, m->spec_out, 0));
@@ -1170,8 +1138,7 @@ int enqueue_inc_lat(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) 
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
   HIP_TRY(launch_inc_lat(dd, count, max_blocks, hd[0].ka, hd[0].vf32, !hd[0].lat_g2, c->stream));
-  if (hd[0].lat_g3) HIP_TRY(launch_lat_gemm3(dd, count, max_tiles, hd[0].vf32, c->stream));
-  else if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2(dd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
+  if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2(dd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
@@ -1208,8 +1175,7 @@ int enqueue_inc_lat_arg(mfgp_ctx* c, const GPDesc* hd, int count) {
   int rc = ev_begin(c, ev, 0);
   if (rc) return rc;
   HIP_TRY(launch_inc_lat_arg(hd, count, max_blocks, hd[0].ka, hd[0].vf32, !hd[0].lat_g2, c->stream));
-  if (hd[0].lat_g3) HIP_TRY(launch_lat_gemm3_arg(hd, count, max_tiles, hd[0].vf32, c->stream));
-  else if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2_arg(hd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
+  if (hd[0].lat_g2) HIP_TRY(launch_lat_gemm2_arg(hd, count, max_tiles, hd[0].ka, hd[0].vf32, c->stream));
   return ev_end(c, ev);
 }
 
@@ -1368,12 +1334,12 @@ int mfgp_debug_set_stamps(void* p) {
 const char* mfgp_version(void) { return "mfgp_hip 0.3 gfx950 f64 f32v"; }
 
 int mfgp_ctx_create(int device, mfgp_ctx** out) {
+  const DeviceGuard dg_(device);
   if (!out) return set_err(MFGP_ERR_ARG, "null out");
   *out = nullptr;
   int n = 0;
   HIP_TRY(hipGetDeviceCount(&n));
   if (device < 0 || device >= n) return set_err(MFGP_ERR_ARG, "device %d out of range (%d devices)", device, n);
-  HIP_TRY(hipSetDevice(device));
   mfgp_ctx* c = new mfgp_ctx();
   c->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
@@ -1385,8 +1351,6 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_SPIN_US")) c->spin_us = std::max(0, std::atoi(e));
-  if (const char* e = std::getenv("MFGP_SYNC_QUERY")) c->sync_query = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MFGP_LAT_G3")) c->lat_g3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_ZCSR")) c->lat_zcsr = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("MFGP_RSPLIT")) {
     const int r = std::atoi(e);
@@ -1398,25 +1362,6 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   if (const char* e = std::getenv("MFGP_LAT_GEMM2")) c->lat_gemm2 = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("MFGP_TRINV_COLUMNS")) c->trinv_columns = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_FACTOR_DEPTH")) c->factor_depth = std::max(1, std::min(16, std::atoi(e)));
-  if (const char* e = std::getenv("MFGP_FACTOR_LOOKAHEAD")) c->factor_look = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MFGP_FACTOR_CRIT_CUS")) c->factor_crit_cus = std::max(0, std::atoi(e));
-  if (!c->factor_look) {
-    // no extra streams (hardware queues) unless the look-ahead factor is asked for
-  } else if (c->factor_crit_cus > 0 && c->factor_crit_cus < c->ncu) {
-    // every (ncu / crit)-th CU for the chain (spread over the XCDs), the rest for
-    // the side pass
-    const int step = c->ncu / c->factor_crit_cus, nw = (c->ncu + 31) / 32;
-    std::vector<uint32_t> mc(nw, 0u), ms(nw, 0u);
-    for (int i = 0; i < c->ncu; ++i) (i % step == 0 ? mc : ms)[i >> 5] |= 1u << (i & 31);
-    HIP_TRY(hipExtStreamCreateWithCUMask(&c->crit, (uint32_t)nw, mc.data()));
-    HIP_TRY(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)nw, ms.data()));
-  } else {
-    HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-  }
-  if (c->factor_look) {
-    HIP_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
-  }
   // A/B runs: MFGP_LATTICE = 0 (V stream only), 1 (default), 2 (lattice without the size gate)
   if (const char* e = std::getenv("MFGP_LATTICE")) {
     const int v = std::atoi(e);
@@ -1434,18 +1379,12 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
 }
 
 void mfgp_ctx_destroy(mfgp_ctx* c) {
+  const DeviceGuard dg_(c ? c->device : -1);
   if (!c) return;
-  (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)drain_timing(c);
   for (auto e : c->pool) (void)hipEventDestroy(e);
   for (int i = 0; i < RING; ++i) (void)hipEventDestroy(c->ring_ev[i]);
-  if (c->side) (void)hipStreamSynchronize(c->side);
-  if (c->crit) (void)hipStreamSynchronize(c->crit);
-  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
-  if (c->side) (void)hipStreamDestroy(c->side);
-  if (c->crit) (void)hipStreamDestroy(c->crit);
   if (c->ws) (void)hipFree(c->ws);
   if (c->vscr) (void)hipFree(c->vscr);
   if (c->d_ring) (void)hipFree(c->d_ring);
@@ -1456,6 +1395,7 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
 }
 
 int mfgp_ctx_trim(mfgp_ctx* c) {
+  const DeviceGuard dg_(c ? c->device : -1);
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->vscr) HIP_TRY(hipFree(c->vscr));
@@ -1477,6 +1417,7 @@ int mfgp_ctx_set_stream(mfgp_ctx* c, void* s) {
 void* mfgp_ctx_get_stream(mfgp_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int mfgp_ctx_synchronize(mfgp_ctx* c) {
+  const DeviceGuard dg_(c ? c->device : -1);
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   int rc = ensure_h_status(c, c->async_status.size());
   if (rc) return rc;
@@ -1502,17 +1443,6 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
         __builtin_ia32_pause();
         if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->spin_us)) break;
       }
-    }
-  }
-  if (c->sync_query) {
-    // poll the stream (hipStreamQuery) instead of the runtime's blocking wait, for
-    // up to spin_us; then the blocking wait
-    const auto t0 = std::chrono::steady_clock::now();
-    while (true) {
-      const hipError_t q = hipStreamQuery(c->stream);
-      if (q == hipSuccess) break;
-      if (q != hipErrorNotReady) HIP_TRY(q);
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->spin_us)) break;
     }
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1611,6 +1541,7 @@ int mfgp_ctx_reset_timing(mfgp_ctx* c) {
 
 int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int nhyp, double jitter,
                       mfgp_model** out) {
+  const DeviceGuard dg_(c ? c->device : -1);
   if (!c || !out) return set_err(MFGP_ERR_ARG, "null ctx/out");
   *out = nullptr;
   if (kind != MFGP_SF && kind != MFGP_MF) return set_err(MFGP_ERR_ARG, "kind must be MFGP_SF or MFGP_MF");
@@ -1618,7 +1549,6 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
   const int want = kind == MFGP_SF ? 4 : 9;
   if (!hyp || nhyp != want)
     return set_err(MFGP_ERR_ARG, "Hyperparameters must be of length 4 (single-fidelity) or 9 (multi-fidelity)");
-  HIP_TRY(hipSetDevice(c->device));
   mfgp_model* m = new mfgp_model();
   m->ctx = c;
   m->kind = kind;
@@ -1637,6 +1567,7 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
 }
 
 void mfgp_model_destroy(mfgp_model* m) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   if (!m) return;
   if (m->ctx) {
     (void)hipStreamSynchronize(m->ctx->stream);
@@ -1663,6 +1594,7 @@ void mfgp_model_destroy(mfgp_model* m) {
 }
 
 int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
+  const DeviceGuard dg_(src ? src->ctx->device : -1);
   int rc = check_model(src);
   if (rc) return rc;
   if (!out) return set_err(MFGP_ERR_ARG, "null out");
@@ -1711,6 +1643,7 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
 }
 
 int mfgp_model_set_hyp(mfgp_model* m, const double* hyp, int nhyp, double jitter) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (!hyp || nhyp != m->nhyp)
@@ -1767,6 +1700,7 @@ GridLattice detect_lattice(const double* g, int64_t M) {
 }
 
 int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (M < 0 || (M > 0 && !xs)) return set_err(MFGP_ERR_ARG, "bad grid");
@@ -1795,6 +1729,7 @@ int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
 
 int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL, const double* XH,
                   const double* yH, int64_t NH) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (NL < 0 || NH < 0) return set_err(MFGP_ERR_ARG, "negative sizes");
@@ -1812,6 +1747,7 @@ int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL,
 int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t k);
 
 int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (k < 0) return set_err(MFGP_ERR_ARG, "negative k");
@@ -1836,6 +1772,7 @@ int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
 }
 
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (n_keep_hifi != m->NH) m->spec_valid = false;
@@ -1855,6 +1792,7 @@ int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
 }
 
 int mfgp_batch_truncate(mfgp_model** models, int count, int64_t n_keep_hifi) {
+  const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
   if (count < 0 || (count > 0 && !models)) return set_err(MFGP_ERR_ARG, "bad batch");
   for (int i = 0; i < count; ++i) {
     const int rc = mfgp_truncate(models[i], n_keep_hifi);
@@ -1885,6 +1823,7 @@ int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t
 }
 
 int mfgp_predict_view(mfgp_model* m, double** mu, double** var, void** view) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (!mu || !var || !view) return set_err(MFGP_ERR_ARG, "null output");
@@ -1923,6 +1862,7 @@ int mfgp_release_view(void* view) {
 }
 
 int mfgp_predict(mfgp_model* m, double* mu, double* var) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   mfgp_ctx* c = m->ctx;
@@ -1996,16 +1936,17 @@ int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
     if (m->kind == MFGP_MF) HIP_TRY(hipMemcpy(&nv[1], m->zvl + m->zb_rows + 1, sizeof(int), hipMemcpyDeviceToHost));
     virt = (int64_t)nv[0] + nv[1];
   }
-  const int64_t v[14] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+  const int64_t v[13] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
                          m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice, virt,
-                         m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy, m->n_lattice_g3};
-  for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
+                         m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy};
+  for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
 int64_t mfgp_model_m(const mfgp_model* m) { return m ? m->M : -1; }
 
 int mfgp_get_factor(mfgp_model* m, double* L_out) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if ((rc = update_factor(m))) return rc;
@@ -2216,7 +2157,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     res_depth.assign(ninc, 0);
     int ka = 8;
     int64_t tiles_sum = 0, nst_min = INT64_MAX;
-    bool g2 = false, g3 = false;
+    bool g2 = false;
     if (lat) {
       for (int i = 0; i < ninc; ++i) {
         if (order[i]->NL + order[i]->NH - hd[i].n0 > 8) ka = 16;
@@ -2232,14 +2173,6 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         g2 = c->lat_gemm2 > 0 || (c->lat_gemm2 < 0 && t2 >= c->ncu && t2 <= 2 * (int64_t)c->ncu);
         // (split-K tiles of one launch wait for each other: they need the whole chip)
         if (c->concurrent) g2 = true;
-      }
-      // the second launch builds its own Z rows (k_lat_gemm3) where its tiles apply:
-      // KA = 8, 128-wide axis tables (the tile holds all 128 iy), each part's rows
-      // within what a scan unit sorts in LDS
-      g3 = g2 && c->lat_g3 && ka == 8;
-      for (int i = 0; g3 && i < ninc; ++i) {
-        const mfgp_model* m = order[i];
-        g3 = lat_tabw(m) == 128 && hd[i].n0 <= LAT_SCAN_MAX && m->ld <= 65535;
       }
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];
@@ -2306,9 +2239,8 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
-        const int64_t tiles = g3 ? (m->lat.nx + LAT_G3IX - 1) / LAT_G3IX : (g2 ? lat_tiles2(m, ka) : lat_tiles(m, ka));
-        // g3: one scan unit per part instead of the Z units
-        const int64_t nzu = g3 ? (m->kind == MFGP_SF ? 1 : 2) : lat_nzu(m);
+        const int64_t tiles = g2 ? lat_tiles2(m, ka) : lat_tiles(m, ka);
+        const int64_t nzu = lat_nzu(m);
         if ((rc = ensure_lat(m, tiles, S, ka, nzu))) return rc;
         const int bin = res_find(m, fd.n0);
         fd.rmu_in = res_mu(m, bin);
@@ -2349,14 +2281,13 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         fd.lat_axbuild = m->axt_gen == m->gen ? 0 : 1;
         fd.lat_selfg = selfg;
         fd.lat_g2 = g2 ? 1 : 0;
-        fd.lat_g3 = g3 ? 1 : 0;
         // Z units reading the scan units' member lists (every lattice row count the scan
         // units bucket, rows and lattice indices within 16 bits)
         // -- by default (the bucketing Z units scan every row of their part; with the
         // lists: headline 93.2k -> 95.3k GP-updates/s, configs[4] 17.8k -> 19.3k)
         const bool zc = c->lat_zcsr != 0;
         (void)nzu;
-        fd.lat_zcsr = (!g3 && zc && ka == 8 && m->lat.ny <= 256 && m->ld <= 65535) ? 1 : 0;
+        fd.lat_zcsr = (zc && ka == 8 && m->lat.ny <= 256 && m->ld <= 65535) ? 1 : 0;
         fd.csr = m->csr;
         fd.tab_lo = (m->tab_gen == m->gen) ? std::min(m->tab_n, fd.n0) : 0;
       }
@@ -2436,7 +2367,6 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
         m->n_lattice += 1;
         if (lat_arg) m->n_lattice_arg += 1;
         if (g2) m->n_lattice_g2 += 1;
-        if (g3) m->n_lattice_g3 += 1;
         m->F_n = m->v_n;   // F's new rows and the new rows' tables came with the step
         m->F_gen = m->gen;
         m->tab_n = m->v_n;
@@ -2456,6 +2386,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
 // the host reads the flag once per chunk and truncates the rows that a stopped
 // loop did not append (the leading rows' factor and V stay valid).
 int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, double* points, int64_t* count) {
+  const DeviceGuard dg_(model ? model->ctx->device : -1);
   int rc = check_model(model);
   if (rc) return rc;
   if (!count || (max_points > 0 && !points)) return set_err(MFGP_ERR_ARG, "null output");
@@ -2592,8 +2523,12 @@ static int cell_reduce_impl(mfgp_ctx* c, const double* grid, int64_t M, int ncel
   const int64_t nv = vstart[ncells];
   const int64_t npart = cell_partial_doubles(M, ncells);
   // workspace layout (doubles): grid 2M | w nf M | f M | var nf M | verts 2nv | seeds 2n | part | out 6n |
-  // argmax n | vstart | field
-  const int64_t off_g = 0, off_w = off_g + 2 * M, off_f = off_w + nf * M, off_v = off_f + M, off_vx = off_v + nf * M;
+  // argmax n | vstart | field; an input already in device memory is read in place and
+  // takes no room (the lockstep driver's w / var at configs[4] scale had
+  // kept ~32 MB of workspace that was never written)
+  auto host_n = [](const double* p, int64_t n) -> int64_t { return (p && !is_device_ptr(p)) ? n : 0; };
+  const int64_t off_g = 0, off_w = off_g + host_n(grid, 2 * M), off_f = off_w + host_n(w, nf * M);
+  const int64_t off_v = off_f + host_n(f, M), off_vx = off_v + host_n(var, nf * M);
   const int64_t off_s = off_vx + 2 * nv, off_p = off_s + 2 * ncells, off_o = off_p + npart;
   const int64_t off_a = off_o + 6 * ncells, off_i = off_a + ncells, off_fd = off_i + (ncells + 2) / 2 + 1;
   const int64_t total = off_fd + (ncells + 1) / 2 + 1;
@@ -2637,12 +2572,14 @@ static int cell_reduce_impl(mfgp_ctx* c, const double* grid, int64_t M, int ncel
 int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, const int* vstart, const double* verts,
                      const double* seeds, const double* w, const double* f, const double* var, double* out,
                      int64_t* argmax) {
+  const DeviceGuard dg_(c ? c->device : -1);
   return cell_reduce_impl(c, grid, M, ncells, vstart, verts, seeds, nullptr, 1, w, f, var, out, argmax);
 }
 
 int mfgp_batch_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, const int* vstart,
                            const double* verts, const double* seeds, const int* field, int nfield, const double* w,
                            const double* f, const double* var, double* out, int64_t* argmax) {
+  const DeviceGuard dg_(c ? c->device : -1);
   if (!field) return set_err(MFGP_ERR_ARG, "null field");
   return cell_reduce_impl(c, grid, M, ncells, vstart, verts, seeds, field, nfield, w, f, var, out, argmax);
 }
@@ -2650,6 +2587,7 @@ int mfgp_batch_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncell
 // likelihood (gp:81-106 / gp:344-385) and its analytic gradient on the device,
 // for the model's data under the given hyperparameters (the model is unchanged).
 int mfgp_nlml(mfgp_model* m, const double* hyp, int nhyp, double* nlml, double* grad) {
+  const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (!hyp || nhyp != m->nhyp)
@@ -2737,12 +2675,14 @@ int mfgp_nlml(mfgp_model* m, const double* hyp, int nhyp, double* nlml, double* 
 
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                               double* mu, double* var, int flags) {
+  const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
   return batch_run(models, count, X, y, k, mu, var, nullptr, nullptr, flags, true, true);
 }
 
 int mfgp_batch_append_predict_ex(mfgp_model** models, int count, const double* X, const double* y,
                                  const int64_t* k, double* mu, double* var, double* var_max, int64_t* var_argmax,
                                  int flags) {
+  const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
   if ((var_max && !is_device_ptr(var_max)) || (var_argmax && !is_device_ptr(var_argmax)))
     return set_err(MFGP_ERR_ARG, "var_max / var_argmax must be device memory");
   return batch_run(models, count, X, y, k, mu, var, var_max, var_argmax, flags, true, true);
@@ -2750,10 +2690,12 @@ int mfgp_batch_append_predict_ex(mfgp_model** models, int count, const double* X
 
 int mfgp_batch_append_factor(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                              int flags) {
+  const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
   return batch_run(models, count, X, y, k, nullptr, nullptr, nullptr, nullptr, flags, true, false);
 }
 
 int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, int flags) {
+  const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
   return batch_run(models, count, nullptr, nullptr, nullptr, mu, var, nullptr, nullptr, flags, false, true);
 }
 

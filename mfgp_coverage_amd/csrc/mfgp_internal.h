@@ -140,14 +140,10 @@ struct GPDesc {
   int lat_selfg;       // k_inc_lat: 1 = the w units gather L21 from V themselves (lattice cells)
   int lat_g2;          // 1 = the GEMM and cells run as a second launch (k_lat_gemm2; lat_tiles are
                        // its 64-row tiles), k_inc_lat has no GEMM roles
-  int lat_g3;          // 1 = that second launch builds its Z rows itself (k_lat_gemm3; lat_tiles are
-                       // its 4-column tiles) from the member lists the scan units of k_inc_lat write
-                       // (nzu = parts), instead of reading the Z units' rows
   int lat_zcsr;        // 1 = one scan unit per part (the launch's first roles) lists the members by
                        // lattice row in csr, and the Z units read their rows' lists (lat_zunit_csr)
-  unsigned* csr;       // g3 member lists, per part [tabw + 1 + ld]: offsets by lattice y-row [ny + 1],
-                       // then the members (px << 16) | j in row order, rows ascending; then the
-                       // rows' places and the members' c w rows (g3_pos_off, g3_cw_off)
+  unsigned* csr;       // member lists, per part [tabw + 1 + ld]: offsets by lattice y-row [ny + 1],
+                       // then the members (px << 16) | j in row order, rows ascending (csr_bytes)
   Hyp hf;              // hyperparameters of the factorisation (updt_info time)
   Hyp hp;              // hyperparameters of predict (predict time)
 };
@@ -206,23 +202,11 @@ hipError_t launch_inc_stream(const GPDesc* d, int count, int64_t max_blocks, int
 hipError_t launch_inc_stream1(const GPDesc& d, int64_t blocks, int vf32, hipStream_t s);
 // the same for count <= DESC_ARG_MAX GPs from host descriptors passed by value
 hipError_t launch_inc_stream_arg(const GPDesc* h, int count, int64_t max_blocks, int vf32, hipStream_t s);
-// g3 (lat_g3): the second launch builds its A operand (the Z rows) from w and the
-// member lists itself; KA = 8, tabw = 128, at most LAT_SCAN_MAX rows per part
-constexpr int LAT_SCAN_MAX = 8192;
-constexpr int LAT_G3IX = 4;   // lattice x columns per k_lat_gemm3 tile (all 128 y columns)
-// The g3 buffer (GPDesc::csr, per model): the member lists [2 parts][tabw + 1 + ld]
-// (unsigned), each row's place in its part's list [2][ld] (int, -1 off the lattice),
-// then, 64-byte aligned, the members' c w rows in list order [2][ld][8] (double;
-// written by the w units' block reducers, read by k_lat_gemm3). Offsets in unsigned.
-__host__ __device__ inline int64_t g3_pos_off(int64_t tabw, int64_t ld) { return 2 * (tabw + 1 + ld); }
-__host__ __device__ inline int64_t g3_cw_off(int64_t tabw, int64_t ld) {
-  return (g3_pos_off(tabw, ld) + 2 * ld + 15) / 16 * 16;
-}
-__host__ __device__ inline int64_t g3_bytes(int64_t tabw, int64_t ld) { return 4 * g3_cw_off(tabw, ld) + 8 * 16 * ld; }
-hipError_t launch_lat_gemm3(const GPDesc* d, int count, int64_t max_tiles, int vf32, hipStream_t s);
+// The member lists of the scan units (GPDesc::csr, per model): [2 parts][tabw + 1 + ld]
+// unsigned (the offsets by lattice y-row, then the members)
+__host__ __device__ inline int64_t csr_bytes(int64_t tabw, int64_t ld) { return 4 * 2 * (tabw + 1 + ld); }
 // MFGP_F32 models whose F was just built (lat_fbuild): Ff = (float) F over F's storage
 hipError_t launch_narrow_f(const GPDesc* d, int count, int64_t max_elems, hipStream_t s);
-hipError_t launch_lat_gemm3_arg(const GPDesc* h, int count, int64_t max_tiles, int vf32, hipStream_t s);
 // the second launch of a lattice step (lat_g2): its GEMM and cells, max_tiles =
 // max over GPs of lat_tiles
 hipError_t launch_lat_gemm2(const GPDesc* d, int count, int64_t max_tiles, int ka, int vf32, hipStream_t s);

@@ -37,17 +37,6 @@ __device__ long long* g_stamps;
   do {            \
   } while (0)
 #endif
-// k_lat_gemm3's grid: (GPs, tiles); a diagnostic build swaps it to (tiles, GPs) so
-// that a GP's tiles spread over every XCD (MFGP_G3_SWAP; k_lat_gemm2 keeps (GPs, tiles))
-#ifdef MFGP_G3_SWAP
-#define G3_GP blockIdx.y
-#define G3_TILE blockIdx.x
-#define G3_NGP gridDim.y
-#else
-#define G3_GP blockIdx.x
-#define G3_TILE blockIdx.y
-#define G3_NGP gridDim.x
-#endif
 // k_inc_stream timeline stamps (GP 0 only; diagnostic builds)
 #ifdef MFGP_STAMPS
 #define FSTAMP(id)                                                                                 \
@@ -70,7 +59,7 @@ __device__ long long* g_stamps;
 #define WTRACE2(slot)                                                                                \
   do {                                                                                               \
     if (threadIdx.x == 0) {                                                                          \
-      long long* wt_ = g_stamps + 64 + 8 * ((1024 + G3_TILE) * G3_NGP + G3_GP);                       \
+      long long* wt_ = g_stamps + 64 + 8 * ((1024 + blockIdx.y) * gridDim.x + blockIdx.x);                       \
       wt_[slot] = __builtin_amdgcn_s_memrealtime();                                                  \
       if ((slot) == 0)                                                                               \
         wt_[7] = ((long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |                       \
@@ -781,9 +770,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
     // acc += L_I,<I V_<I over 16-deep steps; steps s+1, s+2 in flight during step s
     for (int s = 0; s < nk; ++s) {
       const double* cur = lds + (s % NSTAGE) * STAGE;
-#ifndef MFGP_DIAG_NODMA   // diagnostic build: compute on stale LDS (timing only)
       if (s + 2 < nk) dma_step(lds + ((s + 2) % NSTAGE) * STAGE, base, (int64_t)(s + 2) * KS);
-#endif
       main_mma(cur, cur + KS * PW, acc, w, lane);
       if (s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(GLDS_PER_STEP) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -807,9 +794,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
     AccH vh;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
-#ifndef MFGP_DIAG_NODIAG
     half_mma<false>(frag, img, 0, vh, (p16 + 16) / 4, lane);
-#endif
     if (has_b) load_afrag(frag, Amat + fa * NB * ld + fb * NB, ld, p16, lane);   // L_ba
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
@@ -836,9 +821,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int v = 0; v < 4; ++v) th.c[nt][v] = img[swz(64 + p16 + q + 4 * v, nt * 16 + r)];
-#ifndef MFGP_DIAG_NODIAG
       half_mma<true>(frag, img, 0, th, 16, lane);
-#endif
       load_afrag(frag, d.Linv + fb * TILE, NB, p16, lane);   // Linv_b
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
@@ -848,9 +831,7 @@ __global__ __launch_bounds__(PNT, 2) void k_predict(const GPDesc* __restrict__ d
       // V_bot = Linv_b T_bot
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) vh.c[nt] = d4{0.0, 0.0, 0.0, 0.0};
-#ifndef MFGP_DIAG_NODIAG
       half_mma<false>(frag, img, 64, vh, (p16 + 16) / 4, lane);
-#endif
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -1119,11 +1100,7 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
       const int64_t j = 4 * (s0 + NW * u) + q;
       const bool ok = j < j_hi;
       const int64_t jj = ok ? j : j_lo;
-#ifndef MFGP_DIAG_NOGATHER   // diagnostic build: no V-column loads (timing only)
       a[u] = FROMV ? (double)gp(vsrc)[jj * sstride] : ldx<XW>(src + jj * sstride);
-#else
-      a[u] = FROMV ? 1.0 : ldx<XW>(src + jj * sstride);
-#endif
       zz[u] = gp(zv)[jj];
     }
 #pragma unroll
@@ -1134,9 +1111,7 @@ __device__ void inc_schur_partial(const GPDesc& d, const int* cell, int64_t j_lo
       zz[u] = ok ? zz[u] : 0.0;
       if (FROMV && r < k && ok) stx<XW>(&A[j * ld + n0 + r], a[u]);
       // compact rows for the cell tiles: L21 | z1 | zeros
-#ifndef MFGP_DIAG_NOPSTORE   // diagnostic build: no compact-row stores (timing only)
       if (ok) store_l21c<XW, VT>(l21c, j, r, k, a[u], zz[u]);
-#endif
       sacc = mfma(a[u], a[u], sacc);
       uacc = mfma(a[u], zz[u], uacc);
     }
@@ -1676,11 +1651,7 @@ __device__ __forceinline__ void ws_load(WsStage<MODE>& s, const WsSrc<MODE>& src
     const int64_t jj = (!GUARD || j < src.n0) ? j : 0;   // clamped, loads stay unconditional
     // V is read once per update and is far larger than the Infinity Cache
     s.v[u] = __builtin_nontemporal_load(src.vb + jj * (PBM / 2));
-#ifndef MFGP_DIAG_NOL21   // diagnostic build: no L21 loads (timing only)
     if (MODE >= 1) s.a[u] = src.ab[jj * src.astride];
-#else
-    if (MODE >= 1) s.a[u] = 0.5;
-#endif
     if (MODE <= 1) s.z[u] = src.zb[jj];
   }
 }
@@ -1718,12 +1689,8 @@ __device__ __forceinline__ void ws_use(WsStage<MODE>& s, int64_t j0, int64_t n0,
     }
     if (MODE >= 1) {
       const double a = (MODE == 1 && !arow) ? 0.0 : s.a[u];
-#ifndef MFGP_DIAG_NOMMA   // diagnostic build: the stream without its MFMAs (timing only)
       acc[0] = mfma(a, s.v[u].x, acc[0]);
       acc[1] = mfma(a, s.v[u].y, acc[1]);
-#else
-      acc[0][0] += a;
-#endif
     }
   }
 }
@@ -1771,7 +1738,6 @@ __device__ __forceinline__ void ws_stream(const WsSrc<MODE>& src, int q0, bool a
   int64_t t = 0;
   // steady state (sched_barrier keeps each stage's loads ahead of the use after it)
   for (; t + 2 * SS - 1 <= T; t += SS) {
-#ifndef MFGP_WS_NOPRIO
     // the workgroups of a CU stream at unequal rates (the memory pipe favours the
     // oldest waves: 195 / 250 / 309 / 339 us for the four slots of a CU, measured),
     // so priority falls as a wave advances and the waves of a CU finish closer
@@ -1779,7 +1745,6 @@ __device__ __forceinline__ void ws_stream(const WsSrc<MODE>& src, int q0, bool a
     if (t >= (2 * T) / 3) __builtin_amdgcn_s_setprio(0);
     else if (t >= T / 3) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(2);
-#endif
 #pragma unroll
     for (int s = 0; s < SS; ++s) ws_prefetch(pf, t + s, T);
 #pragma unroll
@@ -1920,11 +1885,7 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int a = q + 4 * v;
-#ifdef MFGP_DIAG_NOEPI   // diagnostic build: no psi_new seeds (timing only)
-        if (false) {
-#else
         if (a < k) {
-#endif
           const double tx = Xn[2 * a], ty = Xn[2 * a + 1];
           acc[0][v] = -psi_new(h, d.NL, n0 + a, g0x, g0y, tx, ty);
           acc[1][v] = -psi_new(h, d.NL, n0 + a, g1x, g1y, tx, ty);
@@ -2068,19 +2029,11 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
         msum += vn[a] * L22[KINC * KINC + a];
       }
     }
-#ifdef MFGP_DIAG_NOSTORE   // diagnostic build: no V_new stores (timing only)
-    if (false) {
-#else
     if (live && si == 0 && q < 2 && c < M) {
-#endif
 #pragma unroll
       for (int a = 0; a < KINC; ++a)
         if (a < k) {
-#ifdef MFGP_WS_NTSTORE
-          __builtin_nontemporal_store(vn[a], gp(Vt) + (n0 + a) * PBM + cw + 2 * r + x);
-#else
           gp(Vt)[(n0 + a) * PBM + cw + 2 * r + x] = vn[a];
-#endif
         }
     }
   }
@@ -2212,12 +2165,10 @@ __device__ __forceinline__ void wf_stream(const WfSrc& src, int q0, bool arow, f
     if (s < T) wf_load<MODE, false>(st[s], src, s * RS + q);
   int64_t t = 0;
   for (; t + 2 * SS - 1 <= T; t += SS) {
-#ifndef MFGP_WS_NOPRIO
     // as ws_stream: priority falls as a wave advances
     if (t >= (2 * T) / 3) __builtin_amdgcn_s_setprio(0);
     else if (t >= T / 3) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(2);
-#endif
 #pragma unroll
     for (int s = 0; s < SS; ++s) ws_prefetch(pf, t + s, T);
 #pragma unroll
@@ -2735,26 +2686,6 @@ hipError_t launch_lat_gemm2_arg(const GPDesc* h, int count, int64_t max_tiles, i
   else if (ka == 8) hipLaunchKernelGGL((k_lat_gemm2_arg<8, double>), g, dim3(G2NT), 0, s, a);
   else if (vf32) hipLaunchKernelGGL((k_lat_gemm2_arg<16, float>), g, dim3(G2NT), 0, s, a);
   else hipLaunchKernelGGL((k_lat_gemm2_arg<16, double>), g, dim3(G2NT), 0, s, a);
-  return hipGetLastError();
-}
-#ifdef MFGP_G3_SWAP
-#define G3_GRID(count, tiles) dim3((unsigned)(tiles), (count))
-#else
-#define G3_GRID(count, tiles) dim3((count), (unsigned)(tiles))
-#endif
-hipError_t launch_lat_gemm3(const GPDesc* d, int count, int64_t max_tiles, int vf32, hipStream_t s) {
-  const dim3 g = G3_GRID(count, max_tiles);
-  if (vf32) hipLaunchKernelGGL((k_lat_gemm3<float>), g, dim3(G3NT), 0, s, d);
-  else hipLaunchKernelGGL((k_lat_gemm3<double>), g, dim3(G3NT), 0, s, d);
-  return hipGetLastError();
-}
-hipError_t launch_lat_gemm3_arg(const GPDesc* h, int count, int64_t max_tiles, int vf32, hipStream_t s) {
-  if (count < 1 || count > DESC_ARG_MAX) return hipErrorInvalidValue;
-  DescArg a;
-  std::memcpy(a.d, h, sizeof(GPDesc) * count);
-  const dim3 g = G3_GRID(count, max_tiles);
-  if (vf32) hipLaunchKernelGGL((k_lat_gemm3_arg<float>), g, dim3(G3NT), 0, s, a);
-  else hipLaunchKernelGGL((k_lat_gemm3_arg<double>), g, dim3(G3NT), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_lat_axes(const GPDesc* d, int count, int64_t max_tabw, hipStream_t s) {

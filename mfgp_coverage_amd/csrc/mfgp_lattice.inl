@@ -236,30 +236,8 @@ __device__ __forceinline__ int64_t wst_first(int64_t C, int64_t nwb, int64_t jb)
   const int64_t K2 = 2 * C - 4 * (nwb - 1);
   return 2 * jb < nwb ? jb * K2 : (nwb - 1 - jb) * K2 + C - 4 * (nwb - 1 - jb);
 }
-#ifndef MFGP_W_SKEW
-#define MFGP_W_SKEW 0
-#endif
-#if MFGP_W_SKEW
-// (diagnostic builds: the first half of the units weigh 1000 + MFGP_W_SKEW, the rest
-// 1000 - MFGP_W_SKEW; unit u's first step and the unit holding step s)
-__device__ __forceinline__ int64_t wst_start(int64_t u, int64_t S, int64_t U) {
-  const int64_t H = U / 2, a = 1000 + MFGP_W_SKEW, b = 1000 - MFGP_W_SKEW;
-  const int64_t cum = u <= H ? u * a : H * a + (u - H) * b;
-  return S * cum / (H * a + (U - H) * b);
-}
-__device__ __forceinline__ int64_t wst_unit(int64_t s, int64_t S, int64_t U) {
-  int64_t lo = 0, hi = U - 1;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) / 2;
-    if (wst_start(mid, S, U) <= s) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-#else
 __device__ __forceinline__ int64_t wst_start(int64_t u, int64_t S, int64_t U) { return u * S / U; }
 __device__ __forceinline__ int64_t wst_unit(int64_t s, int64_t S, int64_t U) { return ((s + 1) * U - 1) / S; }
-#endif
 // block jb's position in the pair order (its partials: slots u + position, distinct
 // since a position's units start where the previous position's end)
 __device__ __forceinline__ int64_t wst_pos(int64_t nwb, int64_t jb) {
@@ -277,9 +255,6 @@ __device__ __forceinline__ int64_t wst_pos(int64_t nwb, int64_t jb) {
 // is), stores the block of w, counts it into ldone[0] (the Z units wait for all
 // nwb blocks) and writes F's new rows for its columns, -L22^-1 w^T (the top
 // block's also the L22^-1 entries).
-#ifndef MFGP_W_PRIO
-#define MFGP_W_PRIO 0
-#endif
 template <class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
   // steps in flight per wave: the loop is latency-bound (each step waits for loads
@@ -514,14 +489,6 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   // compiler's waits at the loop head drain every load in flight; the buffers by
   // compile-time index: registers)
   for (int64_t t0 = 0; t0 < T; t0 += DEPTH) {
-#if MFGP_W_PRIO
-    // priority by progress (2, 1, 0 over the thirds of the unit's steps): the
-    // memory pipe serves a CU's older waves first, so of the two units on a CU the
-    // later-dispatched one streamed 15 % slower; a unit ahead now yields to one behind
-    if (t0 >= (2 * T) / 3) __builtin_amdgcn_s_setprio(0);
-    else if (t0 >= T / 3) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(2);
-#endif
 #pragma unroll
     for (int b = 0; b < DEPTH; ++b) {
       const int64_t t = t0 + b;
@@ -538,9 +505,6 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     }
   }
   WTRACE(3);
-#if MFGP_W_PRIO
-  __builtin_amdgcn_s_setprio(2);   // the count-in and the block reductions are on the step's critical path
-#endif
   // count the unit's partials in (one arrival per block, all at once)
   drain_stores();
   __syncthreads();
@@ -564,13 +528,6 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   __syncthreads();
   const int nlast = lastm[0];
   if (nlast == 0) return;
-  // g3: the members' c w rows go to their places in the lists (the scan units were
-  // dispatched first and are long done: the wait is one load)
-  const int P = d.hp.kind == 0 ? 1 : 2;
-  if (d.lat_g3) {
-    wait_flag(d, d.zflag, epoch);
-    if (P == 2) wait_flag(d, d.zflag + 1, epoch);
-  }
   // the blocks' w: every contributor's partial in slot order (the same bits whoever
   // is last), stored, then counted into ldone[0] together (one lane each; the Z
   // units wait for all nwb blocks)
@@ -596,32 +553,6 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     double* const wv = d.wv + 64 * jb * KINC;
 #pragma unroll
     for (int m = 0; m < 4; ++m) stx<true>(wv + tid + NT * m, own[m]);
-    if (d.lat_g3) {
-      // element tid + NT m is w[64 jb + (e >> 4)][e & 15]; the A operand's c w: the
-      // product k_lat_gemm3 and the Z units form (the same bits)
-      const Hyp& h = d.hp;
-      const double cL = h.kind == 0 ? h.sL : h.rho * h.sL, cLH = h.rho2 * h.sL;
-      const int* const place = reinterpret_cast<const int*>(d.csr + g3_pos_off(d.tabw, ld));
-      double* const cwb = reinterpret_cast<double*>(d.csr + g3_cw_off(d.tabw, ld));
-      int pl[4][2];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int e = tid + NT * m, a = e & 15;
-        const int64_t j = 64 * jb + (e >> 4);
-        pl[m][0] = pl[m][1] = -1;
-        if (a < 8 && j < n0) {
-          pl[m][0] = __hip_atomic_load(place + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (P == 2 && j >= d.NL) pl[m][1] = __hip_atomic_load(place + ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int e = tid + NT * m, a = e & 15;
-        const int64_t j = 64 * jb + (e >> 4);
-        if (pl[m][0] >= 0) cwb[(int64_t)pl[m][0] * 8 + a] = own[m] * (j < d.NL ? cL : cLH);
-        if (pl[m][1] >= 0) cwb[(ld + pl[m][1]) * 8 + a] = own[m] * h.sH;
-      }
-    }
   }
   drain_stores();
   __syncthreads();
@@ -1146,20 +1077,17 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
   WTRACE(2);
 }
 
-// g3 (k_lat_gemm3 follows): in place of the Z units, one scan unit per part of the
-// GP lists the part's training rows j < n0 on the lattice by lattice y-row q, in
-// row order within each q -- the order in which a Z unit sums them -- as CSR in
-// d.csr (offsets [ny + 1], then the members (px << 16) | j), and its off-lattice
-// ("virtual") rows in row order in zvl (count, rows, padded to ZKS with the part's
-// first row) as the Z units list them, and each row's place in its list (-1: off the
-// lattice), by which the w units' block reducers store the members' c w rows in list
-// order (g3_cw_off) for the next launch. Nothing here needs w: the units are the
-// launch's first roles and finish while the w units stream F. A stable counting
+// The scan unit of a part (lat_zcsr: the launch's first roles): lists the part's
+// training rows j < n0 on the lattice by lattice y-row q, in row order within each
+// q -- the order in which a Z unit sums them -- as CSR in d.csr (offsets [ny + 1],
+// then the members (px << 16) | j), and its off-lattice ("virtual") rows in row
+// order in zvl (count, rows, padded to ZKS with the part's first row) as the Z units
+// list them. Nothing here needs w: the units finish while the w units stream F. A stable counting
 // sort: the buckets' sizes (LDS atomics), their offsets (a wave scan), then the
 // rows in chunks of NT in row order, each row's place = its bucket's running
 // offset + the same bucket's rows in the chunk's earlier waves + its rank among
 // its wave's lanes of that bucket (nine ballots). Write-through stores: the Z units
-// of the same launch read the lists (lat_zcsr), or the next launch does (g3).
+// of the same launch read the lists.
 constexpr int SCAN_B = 264;   // buckets held: ny <= 256 lattice rows + the virtual one
 // (flag: where the unit publishes that its lists are stored; every output is stored
 // write-through, so the Z units of this launch may read them after the flag)
@@ -1214,7 +1142,6 @@ __device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm, 
   }
   __syncthreads();
   int* const zvl = d.zvl + (int64_t)part * (d.zrows + 1);
-  int* const place = reinterpret_cast<int*>(d.csr + g3_pos_off(d.tabw, d.ld)) + (int64_t)part * d.ld;
   const int vb = *vbase;
   for (int c0 = 0; c0 < n; c0 += NT) {
     const int e = c0 + tid;
@@ -1236,8 +1163,6 @@ __device__ __forceinline__ void lat_scan(const GPDesc& d, int part, double* sm, 
       const int j = (int)j_lo + e;
       if (b < ny) st_u(mem + pos, ((unsigned)(li & 0xffff) << 16) | (unsigned)j);
       else st_i(zvl + 1 + pos - vb, j);
-      // the row's place (the g3 w reducers store its c w row there)
-      st_i(place + j, b < ny ? pos : -1);
     }
     __syncthreads();
     for (int bb = tid; bb <= ny; bb += NT) {
@@ -1290,11 +1215,6 @@ __device__ __forceinline__ void lat_zcompute(const double* slot, d4 (&acc)[2][4]
   __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-#ifdef MFGP_DIAG_LATNOMMA   // diagnostic build: the loop without its MFMAs (timing only)
-    acc[0][0][0] += a[e][0] + b[e][0];
-    acc[1][1][0] += a[e][1] + b[e][1];
-    continue;
-#endif
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       acc[0][n] = mfma(a[e][0], b[e][n], acc[0][n]);
@@ -1689,9 +1609,7 @@ __device__ __forceinline__ void lat_gemm(const GPDesc& d, int64_t tile, int64_t 
     for (int64_t t = 0; t < hi; ++t) {
       const int64_t after = (hi - 1 - t) < (D - 1) ? (hi - 1 - t) : (D - 1);
       vm_wait_bar((int)after * CNT);
-#ifndef MFGP_DIAG_LATNOCOMP   // diagnostic build: the pipeline without its compute (timing only)
       lat_zcompute(sm + ((slot0 + t) % LNST) * LSTG, acc, w, r, q);
-#endif
       // the next DMA after this stage's MFMAs: its wait for a Z unit never holds
       // up a stage that is already here
       if (t + D < hi) issue(s + (t + D) * S, virt, slot0 + t + D);
@@ -1763,15 +1681,7 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
   __shared__ double sm[LAT_LDS + 16];
   const int64_t np = d.nprod;
   int64_t role = blockIdx.y;
-  if (d.lat_g3) {
-    // g3: the scan units first (they wait for nothing), then producers and w units
-    if (role < d.nzu) {
-      lat_scan(d, (int)role, sm, d.zflag + role);
-      return;
-    }
-    role -= d.nzu;
-    if (role >= np + d.nwu) return;
-  } else if (d.lat_zcsr) {
+  if (d.lat_zcsr) {
     // the scan units first (they wait for nothing), then the usual roles
     const int P = d.hp.kind == 0 ? 1 : 2;
     if (role < P) {
@@ -1790,13 +1700,6 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     return;
   }
   if (role < np + d.nwu + d.nzu) {
-#ifdef MFGP_DIAG_LATNOZ   // diagnostic build: Z units count in at once (timing only, wrong results)
-    if (threadIdx.x == 0) {
-      publish(d.zflag + (role - np - d.nwu), d.epoch);
-      arrive_phase(d.ldone + 2, d.epoch, d.nzu);
-    }
-    return;
-#endif
     // (the member-list form at KA = 8 only: at 16 its registers spilled the kernel)
     if constexpr (KA == 8) {
       if (d.lat_zcsr) lat_zunit_csr<KA>(d, role - np - d.nwu, sm);
@@ -1806,9 +1709,6 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     }
     return;
   }
-#ifdef MFGP_DIAG_LATNOGEMM   // diagnostic build: producers, w and Z only (timing only)
-  return;
-#endif
   if constexpr (G1) {
     const int64_t g = role - np - d.nwu - d.nzu;
     if (d.lat_g2 || g >= (int64_t)d.lat_tiles * d.ksplit) return;
@@ -1904,14 +1804,10 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
   double* const Fn = Li + KINC * KINC;             // new rows' tables [2][KA][FW]
   double* const amx = Fn + 2 * 16 * (4 + 64);      // the waves' (max, argmax)
   WTRACE2(0);
-#ifndef MFGP_G2_PRIME
-#define MFGP_G2_PRIME 0
-#endif
   // the cells' inputs (written by the first launch): L22 | z2, the new rows' tables,
-  // then L22^-1 by forward substitution (16 threads). MFGP_G2_PRIME=1 issues the K
-  // loop's first stages before these loads (their latencies overlapped): 92.1-92.7k
-  // vs 92.9-93.1k GP-updates/s without, alternating runs on one box (round 4,
-  // tools/ab_variants.sh) -- within noise, so off
+  // then L22^-1 by forward substitution (16 threads). (Issuing the K loop's first
+  // stages before these loads, their latencies overlapped: 92.1-92.7k vs 92.9-93.1k
+  // GP-updates/s without, alternating runs on one box, round 4 -- within noise)
   auto prologue = [&]() {
   for (int e = tid; e < KINC * KINC + KINC; e += G2NT) {
     const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
@@ -2025,15 +1921,8 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
     }
     slot0 += him;
   };
-  if (MFGP_G2_PRIME) {
-    prime(NA, false);
-    prologue();   // (its barrier orders the ring's LDS-DMA writes with nothing: the
-                  // stages are waited for with vmcnt in the loop, as before)
-    pass(NA, false, true);
-  } else {
-    prologue();
-    pass(NA, false, false);
-  }
+  prologue();
+  pass(NA, false, false);
   if (nvs[0] + nvs[1] > 0) {
     __syncthreads();   // the ring's last reads of the axis pass are done
     pass(nvs[0] + nvs[1], true, false);
@@ -2139,378 +2028,6 @@ __global__ __launch_bounds__(G2NT) void k_lat_gemm2_arg(const DescArg a) {
   (void)a;
   const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
   lat_gemm2<KA, VT>(descs[blockIdx.x], blockIdx.y);
-}
-
-// ---------------------------------------------------------------------------
-// g3: the second launch with its A operand built in the tile (k_lat_gemm3, the
-// default where it applies: KA = 8, 128-wide axis tables, <= LAT_SCAN_MAX rows per
-// part). The first launch then ends when w is stored (no Z units, no Z rows through
-// memory): each tile -- 4 lattice columns x (8 new points) = 32 (a, ix) rows by all
-// 128 iy columns -- sums its own Z rows
-//   Z[part][q][ix][a] = sum_{j on lattice row q, row order} fma(w[j][a] c_j, ex(px_j, ix))
-// from w and the scan units' member lists into LDS (64 KB: every part's rows at
-// once), the same operations in the same order as a Z unit, so the same bits. The K
-// loop then needs no barrier: A from LDS, the axis-table rows (B) loaded into
-// registers six stages ahead. Its sums keep the order of k_lat_gemm2's four K
-// splits -- stage g into accumulator g mod 4, then ((a0 + a1) + a2) + a3 -- so the
-// tile's T~, and with it mu, var and the new V rows, are k_lat_gemm2's bit for bit.
-// Off-lattice ("virtual") training rows are 32-row chunks of the K loop built from
-// their table rows, as the Z units do. One wave per 16 x 16 output tile (16 waves),
-// one workgroup per CU at B = 8 (32 tiles per GP).
-// ---------------------------------------------------------------------------
-constexpr int G3NT = 1024;
-constexpr int G3IX = LAT_G3IX;                   // lattice x columns per tile
-constexpr int G3R = G3IX * 8;                    // (ix, a) rows: 32
-constexpr int G3Y = 128;                         // iy columns (the whole axis)
-constexpr int G3K = 256;                         // lattice K rows at most: parts x round_up(ny, ZKS)
-constexpr int G3FW = G3IX + G3Y;                 // a new row's table columns held for the cells
-constexpr int G3ZS = G3K * G3R;                  // Zs [K][32] (the T~ tile [32][128] aliases it)
-static_assert(G3R * G3Y <= G3ZS, "the T~ tile fits Zs' place");
-static_assert(G3NT == G3R * 32, "a virtual chunk: one element per thread");
-constexpr int G3CH = G3NT;                       // members staged per chunk of the Z build
-constexpr int G3LDS = G3ZS + G3CH * 8 + (KINC * KINC + KINC) + KINC * KINC + 2 * 128 * G3IX + 2 * 16;
-static_assert(G3IX * G3CH <= G3ZS, "the staged axis values fit Zs' place");
-constexpr int G3D = 8;                           // a wave's K-loop stages of B in flight (even:
-                                                 // its w-th stage's accumulator is then b % 2)
-constexpr int G3P = 2 * G3D;                     // the lattice stages, padded to a multiple of this
-static_assert(G3K / ZKS % G3P == 0, "the K loop's padding stages fit Zs");
-static_assert(G3R * G3Y + 2 * 8 * G3FW <= G3ZS, "T~ and the new rows' tables share Zs' place");
-static_assert(2 * G3R * G3Y <= G3CH * 8, "the K splits' sums fit the stage's place");
-
-template <class VT>
-__device__ __forceinline__ void lat_gemm3(const GPDesc& d, int64_t tile) {
-  constexpr int KA = 8;
-  const int k = (int)(d.N - d.n0);
-  if (k <= 0 || k > KA) return;
-  if (d.gate && *d.gate == 0) return;
-  if (tile >= d.lat_tiles) return;   // (the grid is the batch's largest)
-  __shared__ double sm[G3LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wg = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 15, q = lane >> 4;
-  const GridLattice lat = d.lat;
-  const int64_t ix0 = tile * G3IX;
-  const int64_t tabw = d.tabw, ld = d.ld, zrows = d.zrows, tstride = d.ld * tabw;
-  const Hyp& h = d.hp;
-  const int P = h.kind == 0 ? 1 : 2;
-  const int64_t zq8 = (lat.ny + ZKS - 1) / ZKS * ZKS;
-  const int64_t n0 = d.n0, NL = d.NL;
-  double* const Zs = sm;
-  double* const Sw = sm + G3ZS;                    // the chunk's members' c w rows [8][G3CH]
-                                                   // (then the K splits' sums X23)
-  double* const Sex = Zs;                          // their axis values ex(px, ix0 + ixl) [G3IX][G3CH]
-                                                   // (Zs' place is free until the Z rows are stored)
-  double* const L22 = Sw + G3CH * 8;               // [16][16] | z2 [16]
-  double* const Li = L22 + KINC * KINC + KINC;     // L22^-1
-  double* const AXs = Li + KINC * KINC;            // axis columns ex(px, ix0 + ixl) [parts][128][G3IX]
-  double* const amx = AXs + 2 * 128 * G3IX;        // the waves' (max, argmax)
-  double* const Fn = Zs + G3R * G3Y;               // the new rows' tables [2 kinds][KA][G3FW] (after the K loop)
-  WTRACE2(0);
-  // ---- the Z rows' inputs: the members' c w rows in list order (the w units' block
-  // reducers stored them, g3_cw_off) staged through LDS in chunks of G3CH, part 0's
-  // list [0, n0) then part 1's [0, n0 - NL) (the lists' lengths bound by their rows:
-  // no load waits for another); chunk c + 1's loads in flight while c is summed ----
-  const unsigned* const off0 = d.csr;
-  const unsigned* const off1 = d.csr + (tabw + 1 + ld);
-  const unsigned* const mem0 = off0 + tabw + 1;
-  const unsigned* const mem1 = off1 + tabw + 1;
-  const double* const cwb = reinterpret_cast<const double*>(d.csr + g3_cw_off(tabw, ld));
-  const int n0i = (int)n0, n1i = P == 2 ? (int)(n0 - NL) : 0;
-  const int nc0 = (n0i + G3CH - 1) / G3CH, nch = nc0 + (n1i + G3CH - 1) / G3CH;
-  auto ld_chunk = [&](int c, dv2 (&wq)[KA / 2], int& px) {
-    const int pt = c >= nc0 ? 1 : 0;
-    const int m = (pt ? c - nc0 : c) * G3CH + tid;
-    px = 0;
-#pragma unroll
-    for (int h2 = 0; h2 < KA / 2; ++h2) wq[h2] = dv2{0.0, 0.0};
-    if (c < nch && m < (pt ? n1i : n0i)) {   // (past a list's end: stale, never summed)
-      const GLOBAL dv2* src = reinterpret_cast<const GLOBAL dv2*>(gp(cwb) + ((int64_t)pt * ld + m) * 8);
-#pragma unroll
-      for (int h2 = 0; h2 < KA / 2; ++h2) wq[h2] = src[h2];
-      px = (int)((pt ? mem1 : mem0)[m] >> 16);
-    }
-  };
-  dv2 wn[KA / 2];
-  int pxn;
-  ld_chunk(0, wn, pxn);
-  // this thread's Z element (part, q, ixl) and its row's members [m_lo, m_hi) in its list
-  const int zpt = tid / (int)(zq8 * G3IX), zrem = tid % (int)(zq8 * G3IX);
-  const int zqq = zrem / G3IX, zix = zrem % G3IX;
-  const bool zown = zpt < P && zqq < lat.ny && ix0 + zix < lat.nx;
-  int m_lo = 0, m_hi = 0;
-  if (zown) {
-    const unsigned* const o = zpt ? off1 : off0;
-    m_lo = (int)o[zqq];
-    m_hi = (int)o[zqq + 1];
-  }
-  // ---- the cells' inputs (Fn held in registers until the stage is free) and the tile's axis columns ----
-  for (int e = tid; e < KINC * KINC + KINC; e += G3NT) {
-    const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);
-    L22[e] = use ? d.l22r[e] : 0.0;
-  }
-  constexpr int FNR = (2 * KA * G3FW + G3NT - 1) / G3NT;
-  double fnr[FNR];
-#pragma unroll
-  for (int u = 0; u < FNR; ++u) {
-    const int e = tid + u * G3NT;
-    fnr[u] = 0.0;
-    if (e < 2 * KA * G3FW) {
-      const int kind2 = e / (KA * G3FW), rem = e % (KA * G3FW);
-      const int a = rem / G3FW, col = rem % G3FW;
-      const bool isx = col < G3IX;
-      const int t = 2 * kind2 + (isx ? 0 : 1);
-      const int64_t idx = isx ? ix0 + col : col - G3IX;
-      if (a < k && idx < tabw) fnr[u] = d.tab[t * tstride + (n0 + a) * tabw + idx];
-    }
-  }
-  for (int e = tid; e < P * 128 * G3IX; e += G3NT) {
-    const int pt = e / (128 * G3IX), rem = e % (128 * G3IX);
-    const int px = rem / G3IX, ixl = rem % G3IX;
-    AXs[e] = (ix0 + ixl < tabw) ? d.axt[(2 * pt) * (tabw + 1) * tabw + px * tabw + ix0 + ixl] : 0.0;
-  }
-  // ---- the tile's Z rows: thread (part, q, ixl), all 8 a, its row's members in row
-  // order: fma(c w, ex(px, ix), acc), a Z unit's operations in a Z unit's order ----
-  double zacc[KA];
-#pragma unroll
-  for (int a = 0; a < KA; ++a) zacc[a] = 0.0;
-  WTRACE2(5);
-  for (int c = 0; c < nch; ++c) {
-    dv2 wq[KA / 2];
-#pragma unroll
-    for (int h2 = 0; h2 < KA / 2; ++h2) wq[h2] = wn[h2];
-    const int pxc = pxn;
-    ld_chunk(c + 1, wn, pxn);
-    asm volatile("" ::: "memory");   // (the next chunk's loads stay here, ahead of this chunk's work)
-    __syncthreads();   // the previous chunk is summed (the first: L22, AXs stored)
-    const int pt = c >= nc0 ? 1 : 0, c0 = (pt ? c - nc0 : c) * G3CH;
-#pragma unroll
-    for (int a = 0; a < KA; ++a) Sw[a * G3CH + tid] = a & 1 ? wq[a >> 1].y : wq[a >> 1].x;
-#pragma unroll
-    for (int ixl = 0; ixl < G3IX; ++ixl) Sex[ixl * G3CH + tid] = AXs[(pt * 128 + pxc) * G3IX + ixl];
-    __syncthreads();
-    if (zpt == pt) {
-      const int mb = m_lo > c0 ? m_lo : c0, me = m_hi < c0 + G3CH ? m_hi : c0 + G3CH;
-      const double* const ex = Sex + zix * G3CH - c0;
-      const double* const cw = Sw - c0;
-#pragma unroll 4
-      for (int mm = mb; mm < me; ++mm) {
-#pragma unroll
-        for (int a = 0; a < KA; ++a) zacc[a] = __builtin_fma(cw[a * G3CH + mm], ex[mm], zacc[a]);
-      }
-    }
-  }
-  __syncthreads();   // the last chunk is summed (its axis values sit in Zs' place)
-  if (tid < P * zq8 * G3IX) {
-    double* const zr = Zs + (int64_t)(zpt * zq8 + zqq) * G3R + zix * KA;
-#pragma unroll
-    for (int a = 0; a < KA; ++a) zr[a] = zacc[a];
-  }
-  {
-    // the K loop's padding stages: zero A rows
-    const int z0 = (int)(P * zq8) * G3R;
-    const int z1 = (int)((P * zq8 / ZKS + G3P - 1) / G3P * G3P) * ZKS * G3R;
-    for (int e = z0 + tid; e < z1; e += G3NT) Zs[e] = 0.0;
-  }
-  __syncthreads();   // Zs complete
-  WTRACE2(1);
-  // the cells use L22^-1's diagonal only: 1 / L22[a][a], the value the forward
-  // substitution of k_lat_gemm2 puts there (t = 1 exactly at i = c)
-  if (tid < KINC) Li[tid * KINC + tid] = tid < k ? 1.0 / L22[tid * KINC + tid] : 0.0;
-  // ---- the K loop: wave (kh, ct) -> both 16-row tiles, columns 16 ct, the stages g
-  // with g % 4 in {2 kh, 2 kh + 1} into acc[rt][g % 2] -- k_lat_gemm2's four split
-  // sums, two per wave -- so each B element is loaded once per workgroup ----
-  const int kh = wg >> 3, ct = wg & 7;
-  const int iyc = 16 * ct + r;
-  d4 acc[2][2];
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) acc[rt][s2] = d4{0.0, 0.0, 0.0, 0.0};
-  const int NA = (int)(P * zq8 / ZKS);          // lattice stages (8 K rows each)
-  const int NAP = (NA + G3P - 1) / G3P * G3P;   // padded with zero A rows (no branch in the loop)
-  const double* const axb = d.axt + tabw * (tabw + 1);   // part pt's y table: + 2 pt (tabw + 1) tabw
-  // lane (r, q)'s B element of K row kr + q (kr = 8 g + 4 e): part 1's rows continue part 0's
-  const double* const bb0 = axb + (int64_t)q * tabw + iyc;
-  const double* const bb1 = axb + 2 * (tabw + 1) * tabw + (int64_t)q * tabw + iyc - zq8 * tabw;
-  auto b_ld = [&](int g, int e) -> double {
-    const int kr = g < NA ? ZKS * g + 4 * e : 0;   // (the padding stages: any finite row, times A = 0)
-#ifdef MFGP_DIAG_G3NOB   // diagnostic build: B without its loads (timing only, wrong results)
-    return 1.0 + 1e-3 * (kr + q);
-#endif
-    return gp((kr >= zq8 ? bb1 : bb0) + (int64_t)kr * tabw)[0];
-  };
-  auto gw = [&](int w) { return 4 * (w >> 1) + 2 * kh + (w & 1); };   // this wave's w-th stage
-  double bq[G3D][2];
-#pragma unroll
-  for (int b = 0; b < G3D; ++b) {
-    bq[b][0] = b_ld(gw(b), 0);
-    bq[b][1] = b_ld(gw(b), 1);
-    asm volatile("" ::: "memory");   // (in the loop's order: its waits count the same loads)
-  }
-  for (int w0 = 0; w0 < NAP / 2; w0 += G3D) {
-#pragma unroll
-    for (int b = 0; b < G3D; ++b) {
-      const int g = gw(w0 + b);
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const double a0 = Zs[(ZKS * g + q) * G3R + 16 * rt + r];
-        const double a1 = Zs[(ZKS * g + 4 + q) * G3R + 16 * rt + r];
-        acc[rt][b & 1] = mfma(a0, bq[b][0], acc[rt][b & 1]);
-        acc[rt][b & 1] = mfma(a1, bq[b][1], acc[rt][b & 1]);
-      }
-      bq[b][0] = b_ld(gw(w0 + b + G3D), 0);
-      bq[b][1] = b_ld(gw(w0 + b + G3D), 1);
-      asm volatile("" ::: "memory");   // (issued here: G3D of this wave's stages ahead of their use)
-    }
-  }
-  // ---- the virtual rows: chunks of 32 K rows (4 stages) built from their table rows ----
-  int nvr[2] = {0, 0}, nvs[2] = {0, 0};
-  for (int pt = 0; pt < P; ++pt) {
-    nvr[pt] = d.zvl[pt * (zrows + 1)];
-    nvs[pt] = (nvr[pt] + ZKS - 1) / ZKS;
-  }
-  const int NV = nvs[0] + nvs[1];
-  for (int c0 = 0; c0 < NV; c0 += 4) {
-    __syncthreads();   // Zs is free (every wave's reads of the previous stages are done)
-    {
-      const int kr = tid / G3R, col = tid % G3R;   // one element per thread
-      const int gs = c0 + kr / ZKS;
-      double v = 0.0;
-      if (gs < NV) {
-        const int pt = gs < nvs[0] ? 0 : 1;
-        const int vv = ZKS * (gs - (pt ? nvs[0] : 0)) + kr % ZKS;
-        const int ixl = col / KA, a = col % KA;
-        if (vv < nvr[pt] && ix0 + ixl < lat.nx) {
-          const int64_t j = d.zvl[pt * (zrows + 1) + 1 + vv];
-          v = d.wv[j * KINC + a] * d.tab[(2 * pt) * tstride + j * tabw + ix0 + ixl];
-        }
-      }
-      Zs[kr * G3R + col] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {   // stage c0 + s (s = 2 kh + s2): accumulator (c0 + s) % 4 = s
-      const int s = 2 * kh + s2, gs = c0 + s;
-      if (gs < NV) {
-        const int pt = gs < nvs[0] ? 0 : 1;
-        double bv[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int vv = ZKS * (gs - (pt ? nvs[0] : 0)) + 4 * e + q;
-          const int64_t j = d.zvl[pt * (zrows + 1) + 1 + vv];
-          bv[e] = d.tab[(2 * pt + 1) * tstride + j * tabw + iyc];
-        }
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          const double a0 = Zs[(ZKS * s + q) * G3R + 16 * rt + r];
-          const double a1 = Zs[(ZKS * s + 4 + q) * G3R + 16 * rt + r];
-          acc[rt][s2] = mfma(a0, bv[0], acc[rt][s2]);
-          acc[rt][s2] = mfma(a1, bv[1], acc[rt][s2]);
-        }
-      }
-    }
-  }
-  __syncthreads();   // every Zs read is done: the place becomes T~ and the new rows' tables
-  WTRACE2(2);
-  // the sums of splits 2 and 3 (waves kh = 1) meet those of 0 and 1: ((p0 + p1) + p2) + p3
-  double* const X23 = Sw;   // [2][32][128]
-  if (kh == 1) {
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) X23[(s2 * G3R + 16 * rt + q + 4 * v) * G3Y + iyc] = acc[rt][s2][v];
-  }
-#pragma unroll
-  for (int u = 0; u < FNR; ++u)
-    if (tid + u * G3NT < 2 * KA * G3FW) Fn[tid + u * G3NT] = fnr[u];
-  __syncthreads();
-  double* const Tt = sm;   // [32 (ixl, a)][128 iy]
-  if (kh == 0) {
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = 16 * rt + q + 4 * v;
-        double t = acc[rt][0][v] + acc[rt][1][v];
-        t = t + X23[row * G3Y + iyc];
-        t = t + X23[(G3R + row) * G3Y + iyc];
-        Tt[row * G3Y + iyc] = t;
-      }
-  }
-  __syncthreads();
-  WTRACE2(3);
-  // ---- cells: thread t < 4 x 128 finishes cell (ix0 + t / 128, t % 128) ----
-  double bv = -__builtin_inf();
-  int64_t bi = INT64_MAX;
-  if (tid < G3IX * G3Y) {
-    const int ixl = tid / G3Y, iyl = tid % G3Y;
-    const int64_t ix = ix0 + ixl, iy = iyl;
-    if (ix < lat.nx && iy < lat.ny) {
-      const int64_t c = ix * lat.sx + iy * lat.sy;
-      const double cov = d.rvar_in[c], com = d.rmu_in[c];
-      VT* const vt = const_cast<VT*>(vres_ptr<VT>(d)) + (c / PBM) * d.vld * PBM + (c % PBM);
-      const double* const Tc = Tt + (ixl * KA) * G3Y + iyl;
-      const int iyc2 = G3IX + iyl;
-      double vn[KA];
-      double vs = 0.0, ms = 0.0;
-#pragma unroll
-      for (int a = 0; a < KA; ++a) {
-        vn[a] = 0.0;
-        if (a < k) {
-          const double* fL = Fn + a * G3FW;
-          const double* fH = Fn + (KA + a) * G3FW;
-          const double pn = fL[ixl] * fL[iyc2] + fH[ixl] * fH[iyc2];
-          double t = pn - Tc[a * G3Y];
-#pragma unroll
-          for (int b = 0; b < a; ++b) t -= L22[a * KINC + b] * vn[b];
-          vn[a] = t * Li[a * KINC + a];   // 1 / L22[a][a]
-          vs += vn[a] * vn[a];
-          ms += vn[a] * L22[KINC * KINC + a];
-          __hip_atomic_store(vt + (n0 + a) * PBM, (VT)vn[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      const double vc = cov - vs;
-      const double mc = com + ms;
-      __hip_atomic_store(d.mu + c, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(d.var + c, vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d.rmu) {
-        __hip_atomic_store(d.rmu + c, mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d.rvar + c, vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      argmax_pair(bv, bi, vc, c);
-    }
-  }
-  WTRACE2(6);
-  if (d.vmax || d.vargmax || d.status_host) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) argmax_pair(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
-    int64_t* const ami = reinterpret_cast<int64_t*>(amx);
-    if (lane == 0) {
-      amx[2 * wg] = bv;
-      ami[2 * wg + 1] = bi;
-    }
-    __syncthreads();
-    if (wg == 0) {
-      bv = amx[0];
-      bi = ami[1];
-      for (int ww = 1; ww < G3NT / 64; ++ww) argmax_pair(bv, bi, amx[2 * ww], ami[2 * ww + 1]);
-      var_argmax_group(d, bv, bi, tile, d.lat_tiles);
-    }
-  }
-  WTRACE2(4);
-}
-
-template <class VT>
-__global__ __launch_bounds__(G3NT) void k_lat_gemm3(const GPDesc* __restrict__ descs) {
-  lat_gemm3<VT>(descs[G3_GP], G3_TILE);
-}
-template <class VT>
-__global__ __launch_bounds__(G3NT) void k_lat_gemm3_arg(const DescArg a) {
-  (void)a;
-  const GPDesc* descs = (const GPDesc*)__builtin_amdgcn_kernarg_segment_ptr();
-  lat_gemm3<VT>(descs[G3_GP], G3_TILE);
 }
 
 // The separable tables of rows [tab_lo, n0) (full-path refresh; the step itself

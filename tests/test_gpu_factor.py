@@ -3,10 +3,7 @@
 - Two-level blocked Cholesky (mfgp_capi.hip enqueue_factor, k_syrk_blk): the
   trailing matrix takes a group of 64-column steps in one pass. The MFMA
   sequence per tile is the one-level factor's, so L, mu and var must be
-  bit-equal to MFGP_FACTOR_DEPTH=1 for every group depth, on a ragged batch,
-  with and without the look-ahead schedule (round 4: a group's update of the
-  columns past the next group on a second stream, MFGP_FACTOR_LOOKAHEAD=1, CU
-  masks by default; off by default).
+  bit-equal to MFGP_FACTOR_DEPTH=1 for every group depth, on a ragged batch.
 - F = L^-1 by recursive doubling (mfgp_nlml.hip k_trinv_diag / k_trinv_lvl)
   against the block-column k_trinv_f (MFGP_TRINV_COLUMNS=1): a different
   operation order, so the lattice step's posteriors agree to rounding, and both
@@ -44,16 +41,14 @@ def _mf(ctx, hyp, X, y, NL, Xs):
     return m
 
 
-@pytest.mark.parametrize("look", ["0", "1"])
 @pytest.mark.parametrize("depth", [2, 3, 4, 8])
-def test_two_level_factor_bit_equal(monkeypatch, depth, look):
+def test_two_level_factor_bit_equal(monkeypatch, depth):
     from mfgp_coverage_amd import _lib
     from mfgp_coverage_amd.synthetic import HYP
     hyp = HYP["australia8_mf"].copy()
     monkeypatch.setenv("MFGP_FACTOR_DEPTH", "1")
     c1 = _lib.Context(0)
     monkeypatch.setenv("MFGP_FACTOR_DEPTH", str(depth))
-    monkeypatch.setenv("MFGP_FACTOR_LOOKAHEAD", look)
     cd = _lib.Context(0)
     for c in (c1, cd):
         c.set_incremental(False)

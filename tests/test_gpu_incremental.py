@@ -457,6 +457,51 @@ def test_headline_batch_default_step_vs_full(full_ctx, B):
         assert st["lattice_g2"] == (1 if B == 8 else 0), st
 
 
+@pytest.mark.parametrize("B,rsplit", [(1, 1), (2, 2), (4, 4), (8, 0), (2, 1), (8, 4)])
+def test_headline_vstream_row_splits_vs_full(monkeypatch, full_ctx, B, rsplit):
+    """The one-pass predict (k_inc_stream / k_inc_stream_arg) at the headline size with
+    the lattice step off, so the V stream's row splits run on the grids it serves
+    (non-lattice grids, the LAT_MAXD refresh, one GP): the host's rule (rsplit 0: R = 4 /
+    2 / 1 for B = 1-2 / 4 / 8) and forced R = 1 / 2 / 4 (MFGP_RSPLIT). Each must equal
+    the full recompute to 1e-8 in the parity metric with the fused max / argmax of its
+    variance (the B = 2 / 4 / 8 stream test had moved to the lattice path)."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    G, NL, NH0, k = 128, 1024, 1016, 8
+    if rsplit:
+        monkeypatch.setenv("MFGP_RSPLIT", str(rsplit))
+    ctx = _lib.Context(0)
+    ctx.set_lattice(False)
+    cases = [_points(G, NL + NH0 + k, seed=330 + b, ongrid=True) for b in range(B)]
+    inc = [_model(ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0] for Xs, X, y in cases]
+    full = [_model(full_ctx, "mf", X[:NL + NH0], y[:NL + NH0], NL, Xs)[0] for Xs, X, y in cases]
+    for mdl in inc:
+        mdl.predict()
+    M = G * G
+    lo = NL + NH0
+    Xn = np.ascontiguousarray(np.vstack([X[lo:lo + k] for _, X, _ in cases]))
+    yn = np.ascontiguousarray(np.concatenate([y[lo:lo + k] for _, _, y in cases]))
+    Xd, yd = torch.from_numpy(Xn).cuda(), torch.from_numpy(yn).cuda()
+    outs = []
+    for models in (inc, full):
+        mu_d = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        var_d = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        vmax = torch.full((B,), -1.0, dtype=torch.float64, device="cuda")
+        varg = torch.full((B,), -1, dtype=torch.int64, device="cuda")
+        _lib.batch_append_predict(models, Xd.data_ptr(), yd.data_ptr(), [k] * B, mu_d.data_ptr(),
+                                  var_d.data_ptr(), vmax_ptr=vmax.data_ptr(), vargmax_ptr=varg.data_ptr())
+        outs.append((mu_d.cpu().numpy().reshape(B, M), var_d.cpu().numpy().reshape(B, M),
+                     vmax.cpu().numpy(), varg.cpu().numpy()))
+    (mu, var, vm, va), (mu_f, var_f, vm_f, va_f) = outs
+    for b in range(B):
+        assert _err(mu[b], var[b], mu_f[b], var_f[b], HYP_MF) < 1e-8, (B, rsplit, b)
+        assert vm[b] == np.amax(var[b]) and va[b] == int(np.argmax(var[b]))
+    for m in inc:
+        st = m.stats()
+        assert st["inc_factor"] == 1 and st["lattice"] == 0 and st["vstream"] >= 1, st
+    ctx.synchronize()
+
+
 @pytest.mark.parametrize("kind", ["sf", "mf"])
 def test_deferred_appends_vs_oracle(kind):
     """Deferred appends (mfgp_ctx_set_deferred_appends): appends stage their rows and the

@@ -440,80 +440,6 @@ def test_lattice_gemm2_equals_in_launch_split4(monkeypatch, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
-def test_lattice_gemm3_equals_gemm2(monkeypatch, dtype):
-    """The second launch building its own Z rows (k_lat_gemm3: launch 1's scan units
-    sort each part's rows by lattice row into member lists, the GEMM workgroup sums
-    w c ex(px) over a row's members into LDS in row order) against k_lat_gemm2 fed by
-    launch 1's Z units (MFGP_LAT_G3=0): the same FMA chain per Z element, the same K
-    stages and the same order of the four K splits' sums, so the same bits -- mean,
-    variance, fused max / argmax -- over ragged batches (1 and 3 GPs) at a 128-wide
-    grid with off-lattice training rows (virtual K rows); appends of 8 and 3 rows take gemm3, 12 (KA = 16) falls back to gemm2 in both
-    contexts; the g3 context against the oracle at every cell."""
-    import torch
-    from mfgp_coverage_amd import _lib
-    hyp = _hyp("australia8_mf")
-    G = 128
-    dt = _lib.F32 if dtype == "f32" else _lib.F64
-    ks = (8, 3, 12)
-
-    def run(ctx, B, g3):
-        models, data = [], []
-        for i in range(B):
-            nl, nh = 300 + 17 * i, 400 - 9 * i
-            Xs, X, y = _data(G, nl + nh + 40, seed=190 + i)
-            X[5:9] += 0.31 / (G - 1)   # off-lattice lofi rows: virtual K rows
-            models.append(_model(ctx, hyp, X[:nl + nh], y[:nl + nh], nl, Xs, dtype=dt))
-            data.append((X, y, nl, nl + nh))
-        M = Xs.shape[0]
-        mu = torch.empty(B * M, dtype=torch.float64, device="cuda")
-        var = torch.empty_like(mu)
-        vmax = torch.empty(B, dtype=torch.float64, device="cuda")
-        vam = torch.empty(B, dtype=torch.int64, device="cuda")
-        _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
-        out = []
-        for k in ks:
-            Xn = np.concatenate([X[n:n + k] for X, _, _, n in data])
-            yn = np.concatenate([y[n:n + k] for _, y, _, n in data])
-            Xt = torch.from_numpy(np.ascontiguousarray(Xn)).cuda()
-            yt = torch.from_numpy(np.ascontiguousarray(yn)).cuda()
-            _lib.batch_append_predict(models, Xt.data_ptr(), yt.data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
-                                      vmax_ptr=vmax.data_ptr(), vargmax_ptr=vam.data_ptr())
-            data = [(X, y, nl, n + k) for X, y, nl, n in data]
-            out.append((mu.cpu().numpy(), var.cpu().numpy(), vmax.cpu().numpy(), vam.cpu().numpy()))
-        st = [m.stats() for m in models]
-        assert all(s["lattice"] == 3 and s["lattice_g2"] == 3 for s in st), st
-        assert all(s["lattice_g3"] == (2 if g3 else 0) for s in st), st
-        if g3:
-            mu_h, var_h = out[-2][0].reshape(B, M), out[-2][1].reshape(B, M)
-            for i, (X, y, nl, n) in enumerate(data):
-                n -= ks[-1]
-                mu_r, var_r = _ref(hyp, X[:n], y[:n], nl, Xs)
-                if dtype == "f64":
-                    assert _err(hyp, mu_h[i], var_h[i], mu_r, var_r) < TOL, i
-                else:
-                    e = O.parity_errors_f32(mu_h[i], var_h[i], mu_r, var_r, O.prior_variance(hyp))
-                    assert max(e) < O.F32_TOL, (i, e)
-                assert np.isclose(out[-2][2][i], var_h[i].max()) and out[-2][3][i] == int(np.argmax(var_h[i]))
-        ctx.synchronize()
-        return out
-
-    for B in (1, 3):
-        monkeypatch.setenv("MFGP_LAT_GEMM2", "1")   # (these batches are below the chip's size)
-        monkeypatch.setenv("MFGP_LAT_G3", "0")
-        a = _lib.Context(0)
-        monkeypatch.setenv("MFGP_LAT_G3", "1")
-        b = _lib.Context(0)
-        monkeypatch.delenv("MFGP_LAT_G3")
-        monkeypatch.delenv("MFGP_LAT_GEMM2")
-        a.set_lattice("force")
-        b.set_lattice("force")
-        ra, rb = run(a, B, False), run(b, B, True)
-        for step, (sa, sb) in enumerate(zip(ra, rb)):
-            for xa, xb in zip(sa, sb):
-                assert np.array_equal(xa, xb), (B, step)
-
-
-@pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_lattice_zcsr_equals_zunits(monkeypatch, dtype):
     """Z units reading the scan units' member lists (MFGP_LAT_ZCSR=1, the default
     where each Z unit would bucket many rows: configs[4]) against Z units that bucket
@@ -571,3 +497,73 @@ def test_lattice_zcsr_equals_zunits(monkeypatch, dtype):
         for step, (sa, sb) in enumerate(zip(ra, rb)):
             for xa, xb in zip(sa, sb):
                 assert np.array_equal(xa, xb), (B, g2, step)
+
+
+def test_concurrent_contexts_equal_sequential():
+    """Two contexts in concurrent mode (mfgp_ctx_set_concurrent: several streams on one
+    GPU) step independent lattice batches at the same time -- default gates, member
+    lists (lat_zcsr), the GEMM as its own launch -- and must give the bits of the same
+    batches stepped one after the other (the dispatch-order argument of the
+    hand-offs, every waiter behind the roles it waits on, must hold when another
+    context's launch shares the chip; a wait on a later workgroup would hang here,
+    bounded, and report MFGP_ERR_DEVICE)."""
+    import torch
+    from mfgp_coverage_amd import _lib
+    hyp = _hyp("australia8_mf")
+    G, NL, NH, B, steps, k = 128, 700, 600, 4, 3, 8
+
+    def setup(ctx, seed0):
+        ctx.set_concurrent(True)
+        ctx.set_lattice("force")
+        models, data = [], []
+        for i in range(B):
+            Xs, X, y = _data(G, NL + NH + steps * k, seed=seed0 + i)
+            models.append(_model(ctx, hyp, X[:NL + NH], y[:NL + NH], NL, Xs))
+            data.append((X, y))
+        M = G * G
+        mu = torch.empty(B * M, dtype=torch.float64, device="cuda")
+        var = torch.empty_like(mu)
+        _lib.batch_predict(models, mu.data_ptr(), var.data_ptr())
+        ctx.synchronize()
+        pts = []
+        for s in range(steps):
+            lo = NL + NH + s * k
+            Xn = np.ascontiguousarray(np.vstack([X[lo:lo + k] for X, _ in data]))
+            yn = np.ascontiguousarray(np.concatenate([y[lo:lo + k] for _, y in data]))
+            pts.append((torch.from_numpy(Xn).cuda(), torch.from_numpy(yn).cuda()))
+        return models, mu, var, pts
+
+    def step(models, mu, var, pts, s):
+        Xd, yd = pts[s]
+        _lib.batch_append_predict(models, Xd.data_ptr(), yd.data_ptr(), [k] * B, mu.data_ptr(), var.data_ptr(),
+                                  asynchronous=True)
+
+    # sequential
+    seq = []
+    for seed0 in (510, 520):
+        ctx = _lib.Context(0)
+        models, mu, var, pts = setup(ctx, seed0)
+        outs = []
+        for s in range(steps):
+            step(models, mu, var, pts, s)
+            ctx.synchronize()
+            outs.append((mu.cpu().numpy(), var.cpu().numpy()))
+        seq.append(outs)
+        assert all(m.stats()["lattice"] == steps for m in models)
+    # concurrent: both contexts' steps enqueued before either is waited for
+    ca, cb = _lib.Context(0), _lib.Context(0)
+    A, Bm = setup(ca, 510), setup(cb, 520)
+    conc = [[], []]
+    for s in range(steps):
+        step(*A, s)
+        step(*Bm, s)
+        ca.synchronize()
+        cb.synchronize()
+        conc[0].append((A[1].cpu().numpy(), A[2].cpu().numpy()))
+        conc[1].append((Bm[1].cpu().numpy(), Bm[2].cpu().numpy()))
+    for which in (0, 1):
+        for s in range(steps):
+            for xa, xb in zip(seq[which][s], conc[which][s]):
+                assert np.array_equal(xa, xb), (which, s)
+    for m in A[0] + Bm[0]:
+        assert m.stats()["lattice"] == steps

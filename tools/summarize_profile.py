@@ -4,24 +4,27 @@ usage: python tools/summarize_profile.py gpurun_out/prof_r01 r01
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, names shortened) and
 profiles/<tag>_hbm_traffic.csv (per-kernel mean FETCH_SIZE / WRITE_SIZE per
 dispatch in KB as reported, plus bytes with the gfx950 FETCH_SIZE x2 correction
-of MI355X_MICROARCH.md section HBM), and profiles/<tag>_mfma_util.csv, per kernel:
-  mfma_util_grbm = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD x 1024
-      SIMDs), the rocprofv3 derived-counter formula (the CSV's GRBM_GUI_ACTIVE is
-      the sum over the 8 XCDs), and the clock it implies (clock_ghz). For
-      dispatches shorter than ~100 us that denominator does not match the dispatch
-      (implied clocks of 2.6-11.6 GHz in round 3, VERDICT r03 item 7);
+of MI355X_MICROARCH.md section HBM), profiles/<tag>_build.json (the source hash of
+the library the counters were collected on: bench.py reports roofline.traffic only
+from a summary of the same sources), and profiles/<tag>_mfma_util.csv, per kernel:
   mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (dur x SCLK x 1024 SIMDs): the busy
       cycles over the kernel's own duration -- the mean duration of the same kernel
       in the counter-free kernel-trace pass (the counter pass serialises and slows
       dispatches) -- at the shader clock measured on the long dispatches of the
       same pass (sclk_ghz: GRBM_GUI_ACTIVE per XCD over the duration of the
-      dispatches >= 1 ms, median).
+      dispatches >= 1 ms, median). (The GRBM-per-XCD form of the rocprofv3 derived
+      counter implied 2.4-12.8 GHz clocks for sub-100 us dispatches, VERDICT r03 item
+      7 / r04 item 7: not written.)
 """
+import json
 import os
 import re
 import sys
 
 import pandas as pd
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_sha  # noqa: E402
 
 
 def short(n):
@@ -62,12 +65,10 @@ def main(d, tag):
         tr["dur_ns"] = tr.End_Timestamp - tr.Start_Timestamp
         g = g.merge(tr[["Dispatch_Id", "dur_ns"]], on="Dispatch_Id")
         g["grbm_per_xcd"] = g.GRBM_GUI_ACTIVE / 8
-        g["mfma_util_grbm"] = g.SQ_VALU_MFMA_BUSY_CYCLES / (g.grbm_per_xcd * 1024)
         g["clock_ghz"] = g.grbm_per_xcd / g.dur_ns
         long_ = g[g.dur_ns >= 1e6]
         sclk = float(long_.clock_ghz.median()) if len(long_) else 2.0
-        m = g.groupby("Name")[["mfma_util_grbm", "clock_ghz", "SQ_VALU_MFMA_BUSY_CYCLES", "grbm_per_xcd",
-                               "dur_ns"]].median()
+        m = g.groupby("Name")[["SQ_VALU_MFMA_BUSY_CYCLES", "dur_ns"]].median()
         m = m.reset_index()
         # the kernel's own duration: the counter-free trace pass's mean (ns)
         trace_mean = dict(zip(s["Name"], s["AverageNs"]))
@@ -76,6 +77,8 @@ def main(d, tag):
         m["mfma_util"] = m.SQ_VALU_MFMA_BUSY_CYCLES / (m.trace_dur_ns.fillna(m.dur_ns) * sclk * 1024)
         m.to_csv(f"profiles/{tag}_mfma_util.csv", index=False)
         print(m.to_string())
+    with open(f"profiles/{tag}_build.json", "w") as f:
+        json.dump({"tag": tag, "src_sha": source_sha(), "profile_dir": d}, f)
     print(s.head(8).to_string())
 
 
