@@ -934,6 +934,12 @@ __device__ __forceinline__ void stx(double* p, double v) {
   else *p = v;
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// 16-byte write-through store (global_store_dwordx4 ... sc1): a whole line per wave
+// instruction where 8 lanes cover it, and no dirty line left in the XCD's L2 for the
+// launch's end to write back (MI355X_MICROARCH.md: 16-B sc1 stores cost as plain ones)
+__device__ __forceinline__ void st16_wt(double* p, dv2 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 // The consumer's side of a hand-off. Every byte handed between workgroups of one
 // launch is stored write-through (sc1, drained before the flag) and loaded with
 // device-scope (sc1) loads that L2 does not serve from a possibly stale line, or

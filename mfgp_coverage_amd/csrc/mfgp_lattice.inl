@@ -864,10 +864,11 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
     const int64_t nrow = ny - q0 < ZH ? ny - q0 : ZH;
     double* const zr = zb + (part * zrows + q0) * tabw * KA;
     if (d.lat_g2) {
-      // read by the next launch (k_lat_gemm2): plain stores, no drain, no flags
-      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) zr[e] = zst[e];
+      // read by the next launch (k_lat_gemm2): no drain, no flags; written through (16 B
+      // a lane), so the launch's end has no dirty Z lines to write back
+      for (int64_t e = tid; e < nrow * tabw * KA / 2; e += NT) st16_wt(zr + 2 * e, dv2{zst[2 * e], zst[2 * e + 1]});
     } else {
-      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) stx<true>(zr + e, zst[e]);
+      for (int64_t e = tid; e < nrow * tabw * KA / 2; e += NT) st16_wt(zr + 2 * e, dv2{zst[2 * e], zst[2 * e + 1]});
     }
   }
   if (d.lat_g2) {
@@ -1057,9 +1058,9 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
     const int64_t nrow = ny - q0 < ZH ? ny - q0 : ZH;
     double* const zr = zb + (part * zrows + q0) * tabw * KA;
     if (d.lat_g2) {
-      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) zr[e] = zst[e];
+      for (int64_t e = tid; e < nrow * tabw * KA / 2; e += NT) st16_wt(zr + 2 * e, dv2{zst[2 * e], zst[2 * e + 1]});
     } else {
-      for (int64_t e = tid; e < nrow * tabw * KA; e += NT) stx<true>(zr + e, zst[e]);
+      for (int64_t e = tid; e < nrow * tabw * KA / 2; e += NT) st16_wt(zr + 2 * e, dv2{zst[2 * e], zst[2 * e + 1]});
     }
   }
   if (d.lat_g2) {
@@ -1922,6 +1923,17 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
     slot0 += him;
   };
   prologue();
+  // the cells' resident posterior (the previous step's), loaded before the K loop so
+  // that the epilogue does not wait a round trip for it
+  double pcov = 0.0, pcom = 0.0;
+  if (tid < IXPT * 64) {
+    const int64_t ix = ix0 + (tid >> 6), iy = iy0 + (tid & 63);
+    if (ix < lat.nx && iy < lat.ny) {
+      const int64_t c = ix * lat.sx + iy * lat.sy;
+      pcov = d.rvar_in[c];
+      pcom = d.rmu_in[c];
+    }
+  }
   pass(NA, false, false);
   if (nvs[0] + nvs[1] > 0) {
     __syncthreads();   // the ring's last reads of the axis pass are done
@@ -1963,7 +1975,7 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
     const int64_t ix = ix0 + ixl, iy = iy0 + iyl;
     if (ix < lat.nx && iy < lat.ny) {
       const int64_t c = ix * lat.sx + iy * lat.sy;
-      const double cov = d.rvar_in[c], com = d.rmu_in[c];
+      const double cov = pcov, com = pcom;
       VT* const vt = const_cast<VT*>(vres_ptr<VT>(d)) + (c / PBM) * d.vld * PBM + (c % PBM);
       const double* const Tc = Tt + (ixl * KA) * 64 + iyl;
       const int iyc = IXPT + iyl;

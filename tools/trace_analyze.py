@@ -39,13 +39,16 @@ for rep, raw in enumerate(raw_all):
     print(f"  Z published    : {q(tr[isz, 2])}")
     g0 = tr[isg, 0]
     print(f"  gemm start     : {q(g0)}")
+    print(f"  gemm Z built   : {q(tr[isg, 1])}  (lat_zl2)")
+    print(f"  gemm Z waited  : {q(tr[isg, 5])}  (lat_zl2)")
     print(f"  gemm K done    : {q(tr[isg, 2])}  (K loop {q(tr[isg, 2] - tr[isg, 0])})")
     print(f"  gemm end       : {q(tr[isg, 4])}")
     print("  per GP: [w F-loop end max, w publ max, Z publ max] ; per XCC of its w units")
     for g in range(B):
         sw, sz = isw & (gp == g), isz & (gp == g)
         xs = np.unique(xcc[sw])
-        print(f"    GP {g}: {np.nanmax(tr[sw, 3]):6.1f} {np.nanmax(tr[sw, 2]):6.1f} {np.nanmax(tr[sz, 2]):6.1f}   xcc {xs}")
+        mx = lambda a: np.nanmax(a) if np.isfinite(a).any() else float("nan")
+        print(f"    GP {g}: {mx(tr[sw, 3]):6.1f} {mx(tr[sw, 2]):6.1f} {mx(tr[sz, 2]):6.1f}   xcc {xs}")
     print("  per XCC: w F-loop length p50/max, #w units, #CUs used by w")
     for x in range(8):
         sw = isw & (xcc == x)
