@@ -211,6 +211,15 @@ int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, 
  * synchronisation per 32 iterations). Needs the grid set and incremental
  * updates enabled. */
 int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, double* points, int64_t* count);
+/* mfgp_sample_points for `count` models stepped together (the Choi planner of many
+ * Monte-Carlo seeds, sim:326-374 once per seed): per iteration one decision launch
+ * for all models and one batched 1-row append + predict (the lattice step where
+ * the batch takes it); each model stops at its own thresholds[b] (host or device)
+ * or after max_points points, and is unchanged (each works on a copy). points:
+ * [count][max_points][2], host or device; counts[b] = points chosen for model b.
+ * The models share one context and dtype and need their grids set. */
+int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thresholds, int64_t max_points,
+                             double* points, int64_t* counts);
 /* Keep only the first n_keep_hifi hifi rows (no refactor; benchmark reset). */
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi);
 /* mfgp_truncate of count models with one call (the benchmark's per-step reset). */

@@ -50,6 +50,8 @@ SIGNATURES = {
                                               ctypes.c_void_p, ctypes.c_void_p]),
     "mfgp_sample_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p,
                                           _c_int64_p]),
+    "mfgp_batch_sample_points": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                                ctypes.c_void_p, ctypes.c_void_p]),
     "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int64_p, _c_double_p, _c_int64_p]),
     "mfgp_ctx_reset_timing": (ctypes.c_int, [ctypes.c_void_p]),
@@ -427,6 +429,19 @@ def batch_append_factor(models, X, y, k, asynchronous=False):
     ks = (ctypes.c_int64 * n)(*[int(v) for v in k])
     check(lib().mfgp_batch_append_factor(arr, n, ctypes.c_void_p(X), ctypes.c_void_p(y), ks,
                                          ASYNC if asynchronous else 0))
+
+
+def batch_sample_points(models, thresholds, max_points):
+    """mfgp_batch_sample_points: compute_sample_points (simulator.py:326-374) for every
+    model of the batch, stepped together -> one [n_b, 2] array of chosen cells per model."""
+    n = len(models)
+    arr = (ctypes.c_void_p * n)(*[m.handle.value for m in models])
+    thr = np.ascontiguousarray(np.broadcast_to(np.asarray(thresholds, dtype=np.float64), (n,)))
+    P = max(int(max_points), 1)
+    pts = np.empty((n, P, 2), dtype=np.float64)
+    cnt = np.zeros(n, dtype=np.int64)
+    check(lib().mfgp_batch_sample_points(arr, n, ptr(thr), int(max_points), ptr(pts), ptr(cnt)))
+    return [pts[b, :cnt[b]].copy() for b in range(n)]
 
 
 def batch_predict(models, mu_ptr, var_ptr, asynchronous=False):

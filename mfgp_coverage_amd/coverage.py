@@ -211,6 +211,53 @@ def _decide(algo, iteration, max_var_t, max_var_0, streams, agents):
     return prob_explore_t, explore_t
 
 
+class Replay:
+    """A logged run to replay (the reference's own, tests/golden/sim_reference.npz):
+    at every iteration the drivers take the agents' positions, the samples and the
+    Lloyd partition's seeds from the log instead of their own decisions, so each
+    iteration's GP step, cell reduction and logged values (VarMax, XMax, centroids,
+    loss) can be compared with the logged ones wherever rounding would otherwise
+    have decided a discrete choice (an explorer's near-tie argmax, a grid point on a
+    cell edge) and parted the runs. ``agent_log`` / ``sample_log``: the encoded logs
+    (runner.encode, runner.AGENT_COLUMNS / SAMPLE_COLUMNS) of one seed."""
+
+    def __init__(self, agent_log, sample_log):
+        from . import runner
+        A, S = runner.AGENT_COLUMNS, runner.SAMPLE_COLUMNS
+        self._a, self._s = np.asarray(agent_log, dtype=np.float64), np.asarray(sample_log, dtype=np.float64)
+        self._ai = {c: A.index(c) for c in ("Iteration", "Agent", "X", "Y", "XCentroid", "YCentroid",
+                                            "ProbExplore", "Explore")}
+        self._si = {c: S.index(c) for c in ("Iteration", "Agent", "X", "Y", "Sample")}
+
+    def _rows(self, t):
+        r = self._a[self._a[:, self._ai["Iteration"]] == t]
+        return r[np.argsort(r[:, self._ai["Agent"]], kind="stable")]
+
+    def positions(self, t):
+        """the agents' positions logged at iteration t [agents, 2]"""
+        r = self._rows(t)
+        return r[:, [self._ai["X"], self._ai["Y"]]].copy()
+
+    def lloyd_seeds(self, t):
+        """the Lloyd partition's seeds at t: the centroids logged at t - 1 (at t = 0
+        the start positions, as sim:862-863 initialises centroids_t)"""
+        if t == 0:
+            return self.positions(0)
+        r = self._rows(t - 1)
+        return r[:, [self._ai["XCentroid"], self._ai["YCentroid"]]].copy()
+
+    def decisions(self, t):
+        """(prob_explore_t, explore_t) logged at t (decided at t - 1) [agents, 1] each"""
+        r = self._rows(t)
+        return (r[:, [self._ai["ProbExplore"]]].copy(), r[:, [self._ai["Explore"]]].copy())
+
+    def samples(self, t):
+        """(x_new [k, 2], y_new [k, 1], id_new [k, 1]) logged at t, in log order"""
+        s = self._s[self._s[:, self._si["Iteration"]] == t]
+        return (s[:, [self._si["X"], self._si["Y"]]].copy(), s[:, [self._si["Sample"]]].copy(),
+                s[:, [self._si["Agent"]]].copy())
+
+
 def _algo(name):
     for a in ALGOS:
         if a in name:
@@ -222,11 +269,13 @@ def _algo(name):
 # one seed through the drop-in API (the reference's process model)
 # ---------------------------------------------------------------------------
 def simulate(algo, sim_num, iterations, agents, truth_arr, sigma_n, prior, hyp, positions=None, streams=None,
-             log=True):
+             log=True, forced=None):
     """todescato() / periodic() (sim:788-954 / 618-785) of one seed, with this
     package's SFGP / MFGP and device cell reductions. ``truth_arr`` [M, 3] (x, y,
     f) as in sim:833, ``prior`` [P, 3] or None, ``hyp`` the 4 / 9 log-scaled
-    hyperparameters. Returns (loss_log, agent_log, sample_log)."""
+    hyperparameters. ``forced``: a ``Replay`` whose positions, samples, Lloyd seeds
+    and decisions replace the run's own at every iteration. Returns (loss_log,
+    agent_log, sample_log)."""
     from . import geometry
     from .gaussian_process import MFGP, SFGP
     algo = _algo(algo)
@@ -269,15 +318,22 @@ def simulate(algo, sim_num, iterations, agents, truth_arr, sigma_n, prior, hyp, 
     centroids_t = np.copy(positions)
     period = 0
     for iteration in range(iterations):
+        if forced is not None:
+            positions = forced.positions(iteration)
+            centroids_t = forced.lloyd_seeds(iteration)
+            prev_positions = forced.positions(iteration - 1) if iteration > 0 else positions
+            prob_explore_t, explore_t = forced.decisions(iteration)
         # 7) samples of the exploring agents (sim:868-885)
         x_new, y_new, id_new = np.empty([0, 2]), np.empty([0, 1]), np.empty([0, 1])
         for i in range(agents):
-            if explore_t[i] == 1:
+            if forced is None and explore_t[i] == 1:
                 x_sample = positions[i, :]
                 y_sample = _sample(truth_arr, x_sample, streams, sigma_n, tindex)
                 x_new = np.vstack((x_new, x_sample))
                 y_new = np.vstack((y_new, y_sample))
                 id_new = np.vstack((id_new, i))
+        if forced is not None:
+            x_new, y_new, id_new = forced.samples(iteration)
         distance = np.sqrt(np.sum((positions - prev_positions) ** 2, axis=1)).reshape(-1, 1)
         # 8) update and predict (sim:887-892)
         if fidelity == "S":
@@ -334,10 +390,11 @@ class LockstepStats:
 
 
 def run_lockstep(algo, sim_nums, iterations, agents, truth_arr, sigma_n, prior, hyp, log=True, ctx=None,
-                 stats=None, key=0):
+                 stats=None, key=0, forced=None):
     """todescato() / periodic() (sim:788-954 / 618-785) for the seeds ``sim_nums``
     stepped together on the device. Same arguments as ``simulate`` (one truth,
-    prior and hyperparameter set for all seeds, as runner.py:131-132 passes them).
+    prior and hyperparameter set for all seeds, as runner.py:131-132 passes them;
+    ``forced``: one ``Replay`` per seed, as in ``simulate``).
     Returns one (loss_log, agent_log, sample_log) per seed, in ``sim_nums`` order;
     each equals ``simulate`` of that seed up to the rounding of the batched kernels.
     """
@@ -408,12 +465,20 @@ def run_lockstep(algo, sim_nums, iterations, agents, truth_arr, sigma_n, prior, 
     logs = [([], [], []) for _ in range(B)]
     for iteration in range(iterations):
         t0 = time.perf_counter()
+        if forced is not None:
+            for b in range(B):
+                positions[b] = forced[b].positions(iteration)
+                centroids_t[b] = forced[b].lloyd_seeds(iteration)
+                prev_positions[b] = forced[b].positions(iteration - 1) if iteration > 0 else positions[b]
+                prob_explore_t[b], explore_t[b] = forced[b].decisions(iteration)
         # 7) every seed's samples (sim:868-885)
         x_new, y_new, id_new, dist = [], [], [], []
         for b in range(B):
             xb, yb, ib = np.empty([0, 2]), np.empty([0, 1]), np.empty([0, 1])
+            if forced is not None:
+                xb, yb, ib = forced[b].samples(iteration)
             for i in range(agents):
-                if explore_t[b][i] == 1:
+                if forced is None and explore_t[b][i] == 1:
                     x_sample = positions[b][i, :]
                     y_sample = _sample(truth_arr, x_sample, streams[b], sigma_n, tindex)
                     xb = np.vstack((xb, x_sample))

@@ -149,6 +149,7 @@ struct mfgp_ctx {
 
 struct mfgp_model {
   mfgp_ctx* ctx = nullptr;
+  int* gate_dev = nullptr;  // device gate of every step of this model (mfgp_batch_sample_points' clones: 0 = skip)
   int kind = MFGP_SF;
   int dtype = MFGP_F64;     // precision of the resident V (MFGP_F32: fp32 storage and stream)
   int nhyp = 4;
@@ -544,7 +545,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.vmax = nullptr;
   d.vargmax = nullptr;
   d.tred = m->tred;
-  d.gate = nullptr;
+  d.gate = m->gate_dev;
   d.status = m->status;
   d.status_host = nullptr;
   d.srcX = nullptr;
@@ -1557,6 +1558,12 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
   std::memcpy(m->hyp, hyp, sizeof(double) * nhyp);
   m->jitter = jitter;
   HIP_TRY(hipMalloc(&m->status, sizeof(int)));
+  {
+    // "no failure" until a step writes it: a step whose kernels all skip (a gated
+    // model of mfgp_batch_sample_points) must not read an uninitialised word
+    const int ok = INT_MAX;
+    HIP_TRY(hipMemcpy(m->status, &ok, sizeof(int), hipMemcpyHostToDevice));
+  }
   int rc = ensure_cap(m, 63);
   if (rc) {
     mfgp_model_destroy(m);
@@ -2489,6 +2496,150 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
     return fail(set_err(MFGP_ERR_DEVICE, "sample_points: copy out failed"));
   *count = done;
   mfgp_model_destroy(t);
+  return MFGP_OK;
+}
+
+// compute_sample_points for a batch of models (the Choi planner's sample-set
+// selection of many seeds, sim:326-374) stepped together: per iteration ONE
+// k_choi_select_batch (every model's decision from its fused max / argmax) and ONE
+// batched append + predict of every model's chosen row through the general batch
+// step -- the lattice step where the batch takes it (its kernels and the V stream's
+// honour each model's device gate, so a model past its threshold skips the rest of
+// the chunk) -- with one host synchronisation per CH iterations. Each model works on
+// its own copy (sim:339); the chosen points are the single-model loop's, up to the
+// rounding of the batch step (ties decided by it).
+int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thresholds, int64_t max_points,
+                             double* points, int64_t* counts) {
+  const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
+  if (count <= 0 || !models || !thresholds || !counts || (max_points > 0 && !points))
+    return set_err(MFGP_ERR_ARG, "bad batch_sample_points arguments");
+  if (max_points < 0) return set_err(MFGP_ERR_ARG, "negative max_points");
+  mfgp_ctx* c = models[0]->ctx;
+  if (!c->incremental) return set_err(MFGP_ERR_ARG, "mfgp_batch_sample_points needs incremental updates enabled");
+  int rc = MFGP_OK;
+  for (int b = 0; b < count; ++b) {
+    if ((rc = check_model(models[b]))) return rc;
+    if (models[b]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
+    if (models[b]->dtype != models[0]->dtype) return set_err(MFGP_ERR_ARG, "batch models must share one dtype");
+    if (models[b]->M <= 0) return set_err(MFGP_ERR_ARG, "model %d: no grid (call mfgp_set_grid first)", b);
+    counts[b] = 0;
+  }
+  for (int b = 0; b < count; ++b)
+    if ((rc = update_factor(models[b]))) return rc;
+  std::vector<mfgp_model*> t(count, nullptr);
+  auto fail = [&](int code) {
+    for (auto m : t)
+      if (m) {
+        m->gate_dev = nullptr;
+        mfgp_model_destroy(m);
+      }
+    return code;
+  };
+  for (int b = 0; b < count; ++b)
+    if ((rc = mfgp_clone(models[b], &t[b]))) return fail(rc);
+  // device state: mu, var [sum M] | vmax [B] | vargmax [B] | state [B][2] | thr [B] | moff [B] |
+  // Ms [B] | grids [B] | xn [B][2] | yn [B] | pos [B] | points [B][max_points][2]
+  std::vector<int64_t> moff(count), Ms(count);
+  int64_t Mtot = 0;
+  for (int b = 0; b < count; ++b) {
+    moff[b] = Mtot;
+    Ms[b] = t[b]->M;
+    Mtot += t[b]->M;
+  }
+  const int64_t P = std::max<int64_t>(max_points, 1);
+  const size_t nd = 2 * (size_t)Mtot + 10 * (size_t)count + 2 * (size_t)count * (size_t)P + 8;
+  double* ws = nullptr;
+  if (hipMalloc(&ws, sizeof(double) * nd) != hipSuccess) return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: out of memory"));
+  auto fail2 = [&](int code) {
+    (void)hipFree(ws);
+    return fail(code);
+  };
+  double* mu = ws;
+  double* var = mu + Mtot;
+  double* vmax = var + Mtot;
+  int64_t* vargmax = reinterpret_cast<int64_t*>(vmax + count);
+  int64_t* state = vargmax + count;
+  double* thr = reinterpret_cast<double*>(state + 2 * count);
+  int64_t* moff_d = reinterpret_cast<int64_t*>(thr + count);
+  int64_t* Ms_d = moff_d + count;
+  const double** grids_d = reinterpret_cast<const double**>(Ms_d + count);
+  double* xn = reinterpret_cast<double*>(grids_d + count);
+  double* yn = xn + 2 * count;
+  int* pos_d = reinterpret_cast<int*>(yn + count);
+  double* pts = yn + 2 * count;
+  std::vector<int64_t> st(2 * count);
+  std::vector<const double*> grids(count);
+  for (int b = 0; b < count; ++b) {
+    st[2 * b] = 1;
+    st[2 * b + 1] = 0;
+    grids[b] = t[b]->grid;
+  }
+  hipStream_t s = c->stream;
+  if (hipMemcpyAsync(state, st.data(), sizeof(int64_t) * 2 * count, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(thr, thresholds, sizeof(double) * count, hipMemcpyDefault, s) != hipSuccess ||
+      hipMemcpyAsync(moff_d, moff.data(), sizeof(int64_t) * count, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(Ms_d, Ms.data(), sizeof(int64_t) * count, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(grids_d, grids.data(), sizeof(double*) * count, hipMemcpyHostToDevice, s) != hipSuccess)
+    return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: state upload failed"));
+  // the copies' initial posteriors and their max / argmax (sim:340-342)
+  if ((rc = batch_run(t.data(), count, nullptr, nullptr, nullptr, mu, var, vmax, vargmax, 0, false, true)))
+    return fail2(rc);
+  for (int b = 0; b < count; ++b) t[b]->gate_dev = reinterpret_cast<int*>(state + 2 * b);
+  // the models still running (the batch step's members; a stopped one leaves at the
+  // next chunk boundary), their offsets into mu / var and indices into vmax
+  std::vector<int> live(count);
+  for (int b = 0; b < count; ++b) live[b] = b;
+  constexpr int64_t CH = 32;
+  int64_t it_done = 0;
+  while (!live.empty() && it_done < max_points) {
+    const int64_t C = std::min<int64_t>(CH, max_points - it_done);
+    // the live models are the batch step's members, in batch order: their rows at
+    // their member places (pos), their outputs at their own offsets / indices
+    std::vector<mfgp_model*> lm;
+    std::vector<int64_t> lk, loff;
+    std::vector<int> lvi, pos(count, -1);
+    for (int b : live) {
+      pos[b] = (int)lm.size();
+      lm.push_back(t[b]);
+      lk.push_back(1);
+      loff.push_back(moff[b]);
+      lvi.push_back(b);
+    }
+    if (hipMemcpyAsync(pos_d, pos.data(), sizeof(int) * count, hipMemcpyHostToDevice, s) != hipSuccess)
+      return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: upload failed"));
+    for (int64_t it = 0; it < C; ++it) {
+      if (launch_choi_select_batch(count, pos_d, state, thr, vmax, vargmax, mu, moff_d, grids_d, Ms_d, xn, yn, pts,
+                                   max_points, s) != hipSuccess)
+        return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: launch failed"));
+      if ((int)lm.size() == count)
+        rc = batch_run(lm.data(), count, xn, yn, lk.data(), mu, var, vmax, vargmax, MFGP_ASYNC, true, true);
+      else
+        rc = batch_run(lm.data(), (int)lm.size(), xn, yn, lk.data(), mu, var, vmax, vargmax, MFGP_ASYNC, true, true,
+                       loff.data(), lvi.data());
+      if (rc) return fail2(rc);
+    }
+    it_done += C;
+    if (hipMemcpyAsync(st.data(), state, sizeof(int64_t) * 2 * count, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: state read failed"));
+    for (int b : live)
+      if ((rc = read_status(t[b]))) return fail2(rc);
+    std::vector<int> keep;
+    for (int b : live)
+      if ((int)st[2 * b] != 0) keep.push_back(b);
+    live.swap(keep);
+  }
+  for (int b = 0; b < count; ++b) {
+    counts[b] = st[2 * b + 1];
+    if (counts[b] > 0 && hipMemcpy(points + 2 * (size_t)b * (size_t)P, pts + 2 * (size_t)b * (size_t)P,
+                                   sizeof(double) * 2 * counts[b], hipMemcpyDefault) != hipSuccess)
+      return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: copy out failed"));
+  }
+  (void)hipFree(ws);
+  for (auto m : t) {
+    m->gate_dev = nullptr;
+    mfgp_model_destroy(m);
+  }
   return MFGP_OK;
 }
 

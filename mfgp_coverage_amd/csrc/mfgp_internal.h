@@ -259,5 +259,9 @@ hipError_t launch_nlml_grad(const GPDesc* d, int64_t N, double* Xi, double* Kv, 
 int64_t nlml_partials(int64_t N);
 hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,
                               hipStream_t s);
+hipError_t launch_choi_select_batch(int count, const int* pos, int64_t* state, const double* thr, const double* vmax,
+                                    const int64_t* vargmax, const double* mu, const int64_t* moff,
+                                    const double* const* grids, const int64_t* Ms, double* xn, double* yn,
+                                    double* pts, int64_t max_points, hipStream_t s);
 
 }  // namespace mfgp

@@ -934,6 +934,10 @@ __device__ __forceinline__ void stx(double* p, double v) {
   else *p = v;
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// A workgroup barrier that orders LDS only: this wave's LDS accesses complete, then
+// s_barrier. Loads in flight stay in flight (__syncthreads' workgroup fence waits for
+// them); for LDS data exchanged between the waves of one workgroup.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // 16-byte write-through store (global_store_dwordx4 ... sc1): a whole line per wave
 // instruction where 8 lanes cover it, and no dirty line left in the XCD's L2 for the
 // launch's end to write back (MI355X_MICROARCH.md: 16-B sc1 stores cost as plain ones)
@@ -2553,6 +2557,38 @@ __global__ void k_choi_select(const GPDesc* __restrict__ descs, double threshold
   *cnt += 1;
 }
 
+// The batched form (mfgp_batch_sample_points): thread b decides for model b of the
+// batch from its fused (max, argmax) -- stop at its threshold or its point budget
+// (state[b] = {gate, count}), else take the argmax cell and its posterior mean as the
+// next hifi row, staged in xn / yn at the model's place pos[b] among the batch
+// step's members (its device-source rows), and record it in pts[b][count].
+__global__ void k_choi_select_batch(int count, const int* __restrict__ pos, int64_t* __restrict__ state,
+                                    const double* __restrict__ thr,
+                                    const double* __restrict__ vmax, const int64_t* __restrict__ vargmax,
+                                    const double* __restrict__ mu, const int64_t* __restrict__ moff,
+                                    const double* const* __restrict__ grids, const int64_t* __restrict__ Ms,
+                                    double* __restrict__ xn, double* __restrict__ yn, double* __restrict__ pts,
+                                    int64_t max_points) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= count) return;
+  int64_t* st = state + 2 * b;
+  if (st[0] == 0) return;
+  const double v = vmax[b];
+  const int64_t j = vargmax[b], cnt = st[1];
+  if (!(v > thr[b]) || cnt >= max_points || j < 0 || j >= Ms[b]) {
+    st[0] = 0;
+    return;
+  }
+  const double gx = grids[b][2 * j], gy = grids[b][2 * j + 1];
+  const int p = pos[b];
+  xn[2 * p] = gx;
+  xn[2 * p + 1] = gy;
+  yn[p] = mu[moff[b] + j];
+  pts[2 * (b * max_points + cnt)] = gx;
+  pts[2 * (b * max_points + cnt) + 1] = gy;
+  st[1] = cnt + 1;
+}
+
 // Append the batch's new (device-resident) rows to every model's training set:
 // one launch for the whole batch instead of two copies per model (full-refactor
 // path; k_inc_l21 lands the rows of the bordered appends itself).
@@ -2611,6 +2647,14 @@ hipError_t launch_extract_z(const GPDesc* d, int count, int64_t max_n, hipStream
 hipError_t launch_inc_factor(const GPDesc* d, int count, int64_t max_nprod, int vf32, hipStream_t s) {
   if (vf32) hipLaunchKernelGGL(k_inc_stream<float>, dim3(count, (unsigned)max_nprod), dim3(NT), 0, s, d);
   else hipLaunchKernelGGL(k_inc_stream<double>, dim3(count, (unsigned)max_nprod), dim3(NT), 0, s, d);
+  return hipGetLastError();
+}
+hipError_t launch_choi_select_batch(int count, const int* pos, int64_t* state, const double* thr, const double* vmax,
+                                    const int64_t* vargmax, const double* mu, const int64_t* moff,
+                                    const double* const* grids, const int64_t* Ms, double* xn, double* yn,
+                                    double* pts, int64_t max_points, hipStream_t s) {
+  hipLaunchKernelGGL(k_choi_select_batch, dim3((count + 63) / 64), dim3(64), 0, s, count, pos, state, thr, vmax, vargmax,
+                     mu, moff, grids, Ms, xn, yn, pts, max_points);
   return hipGetLastError();
 }
 hipError_t launch_choi_select(const GPDesc* d, double threshold, double* points, int64_t max_points,

@@ -413,30 +413,16 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   };
   int nseg = 0;
   // the end of block jb's steps in this unit: the waves' sums in wave order (one
-  // 32-column half at a time), stored as the unit's partial of the block
-  auto seg_done = [&](int64_t jb) {
-    // thread tid: outputs e = tid + 256 m, (jl, a) = (e >> 4, e & 15), jl = 32 hh +
-    // jh; lane (rr, g) register v of acc[2 hh + c] is w row a = g + 4 v, column
-    // jh = 2 rr + c
-    double own[4];
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) red[w * 512 + (c * 4 + v) * 64 + lane] = acc[2 * hh + c][v];
-      __syncthreads();
-#pragma unroll
-      for (int m2 = 0; m2 < 2; ++m2) {
-        const int e = tid + NT * m2, jh = e >> 4, a = e & 15;
-        const int o = ((jh & 1) * 4 + (a >> 2)) * 64 + 16 * (a & 3) + (jh >> 1);
-        own[2 * hh + m2] = (red[o] + red[512 + o]) + (red[1024 + o] + red[1536 + o]);
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
-    // own[2 hh + m2] is output e = 512 hh + tid + 256 m2 of the block
+  // 32-column half at a time), stored as the unit's partial of the block. Its
+  // barriers wait for the LDS accesses only (lds_barrier: __syncthreads' fence would
+  // wait for every load in flight). A block that ends inside the unit's stream keeps
+  // its partial in registers (own_s) until the stream is done: its write-through
+  // stores sit in the same in-order vmcnt queue as the F loads, and the loop's waits
+  // for the loads behind them waited for their write acknowledgements too (the units
+  // whose share spans two blocks streamed ~2.2 us longer)
+  double own_s[4] = {0.0, 0.0, 0.0, 0.0};
+  int64_t jb_s = -1;
+  auto store_part = [&](const double (&own)[4], int64_t jb) {
     double* const part = d.wpart + (u + wst_pos(nwb, jb)) * 1024;
     if constexpr (sizeof(VT) == 4) {
       // (the fp32 F's lanes: own[2 hh + m2] is column 4 (jp >> 1) + 2 hh + (jp & 1), row a)
@@ -448,6 +434,37 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     } else {
 #pragma unroll
       for (int m = 0; m < 4; ++m) stx<true>(part + tid + NT * m, own[m]);
+    }
+  };
+  auto seg_done = [&](int64_t jb, bool defer) {
+    // thread tid: outputs e = tid + 256 m, (jl, a) = (e >> 4, e & 15), jl = 32 hh +
+    // jh; lane (rr, g) register v of acc[2 hh + c] is w row a = g + 4 v, column
+    // jh = 2 rr + c
+    double own[4];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) red[w * 512 + (c * 4 + v) * 64 + lane] = acc[2 * hh + c][v];
+      lds_barrier();
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2) {
+        const int e = tid + NT * m2, jh = e >> 4, a = e & 15;
+        const int o = ((jh & 1) * 4 + (a >> 2)) * 64 + 16 * (a & 3) + (jh >> 1);
+        own[2 * hh + m2] = (red[o] + red[512 + o]) + (red[1024 + o] + red[1536 + o]);
+      }
+      lds_barrier();
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+    // own[2 hh + m2] is output e = 512 hh + tid + 256 m2 of the block
+    if (defer && jb_s < 0) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) own_s[m] = own[m];
+      jb_s = jb;
+    } else {
+      store_part(own, jb);
     }
     if (tid == 0) segs[nseg] = (int)jb;
     ++nseg;
@@ -499,11 +516,12 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       next_load();
       compute(fb[b], ab[b], t < T && row_of(cc) < n0);
       if (t < T) {
-        if (cc.st + 1 == cc.nb || t + 1 == T) seg_done(cc.jb);
+        if (cc.st + 1 == cc.nb || t + 1 == T) seg_done(cc.jb, t + 1 < T);
         if (t + 1 < T) adv(cc);
       }
     }
   }
+  if (jb_s >= 0) store_part(own_s, jb_s);   // (the stream is done: no load behind it)
   WTRACE(3);
   // count the unit's partials in (one arrival per block, all at once)
   drain_stores();
@@ -556,7 +574,9 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   }
   drain_stores();
   __syncthreads();
-  if (tid < nlast) arrive_phase(d.ldone, epoch, (int64_t)nwb);
+  // each block's own flag (the Z units poll all nwb of them: no count of the blocks'
+  // arrivals on one word in between, one round trip fewer on the step's chain)
+  if (tid < nlast) publish(d.wflag + segs[tid], epoch);
   WTRACE(2);
   // F's new rows for the blocks (read from the next launch on): F[n0 + a][j] =
   // -sum_{b <= a} L22^-1[a][b] w[j][b], w reloaded (this workgroup stored it)
@@ -711,7 +731,7 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
   auto wait_w = [&]() {
     if (!waited) {
       WTRACE(1);
-      wait_phase(d, d.ldone, epoch);   // w of every block
+      wait_flags_all(d, d.wflag, d.nwb, epoch);   // w of every block
       WTRACE(3);
       waited = true;
     }
@@ -983,7 +1003,7 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
     };
     load_ex(0);
     if (!waited) {
-      wait_phase(d, d.ldone, epoch);   // w of every block (every wave: a barrier)
+      wait_flags_all(d, d.wflag, d.nwb, epoch);   // w of every block (every wave: a barrier)
       WTRACE(3);
       waited = true;
     }
@@ -1021,7 +1041,7 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
     }
   }
   if (!waited) {
-    wait_phase(d, d.ldone, epoch);   // (a unit without members still waits: its virtual rows need w)
+    wait_flags_all(d, d.wflag, d.nwb, epoch);   // (a unit without members still waits: its virtual rows need w)
     WTRACE(3);
   }
   WTRACE(4);

@@ -9,6 +9,12 @@ on the device (libmfgp_hip's mfgp_sample_points): every iteration is a 1-row
 bordered Cholesky append plus one pass over the resident V with a fused argmax,
 and the host synchronises once per 32 iterations. Same signature, same return
 value, same model-unchanged contract (the reference works on ``copy.deepcopy``).
+
+``compute_sample_points_batch`` runs the same loop for many models at once (the
+Choi planner of a rank's Monte-Carlo seeds: one seed's sample set each): every
+iteration is one decision launch for all of them and one batched 1-row append +
+predict (libmfgp_hip's mfgp_batch_sample_points, the lattice step where the batch
+takes it); each model stops at its own threshold.
 """
 from __future__ import annotations
 
@@ -33,4 +39,31 @@ def compute_sample_points(model, x_star, threshold, console):
         raise RuntimeError("compute_sample_points: no convergence within %d points" % cap)
     if console:
         print("Sample points to reduce max var below " + str(threshold) + ": " + str(pts.shape[0]))
+    return pts
+
+
+def compute_sample_points_batch(models, x_star, thresholds, console=False):
+    """compute_sample_points (simulator.py:326-374) for every model of ``models``
+    (one context, one dtype, the same grid ``x_star``), stepped together ->
+    list of [n_b, 2] arrays, each model's cells in order. ``thresholds``: one value
+    or one per model."""
+    from . import _lib
+    if not models:
+        return []
+    for m in models:
+        if not isinstance(m, (SFGP, MFGP)):
+            raise TypeError("Invalid model type: must be SFGP or MFGP")
+    xs = np.ascontiguousarray(np.asarray(x_star, dtype=np.float64).reshape(-1, 2))
+    for m in models:
+        m._sync_data()
+        m._push_hyp()
+        m._grid_to_device(xs)
+    cap = 4 * xs.shape[0] + 1
+    thr = np.broadcast_to(np.asarray(thresholds, dtype=np.float64), (len(models),))
+    pts = _lib.batch_sample_points([m._dev() for m in models], thr, cap)
+    for b, p in enumerate(pts):
+        if p.shape[0] >= cap:
+            raise RuntimeError("compute_sample_points: no convergence within %d points" % cap)
+        if console:
+            print("Sample points to reduce max var below " + str(thr[b]) + ": " + str(p.shape[0]))
     return pts

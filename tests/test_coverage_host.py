@@ -113,3 +113,37 @@ def test_truth_index_selects_the_mask_rows():
         a = C._sample(truth, p, C.SeedStreams(3), 0.1)
         b = C._sample(truth, p, C.SeedStreams(3), 0.1, ti)
         assert a.shape == b.shape and np.array_equal(a, b), p
+
+
+@pytest.mark.parametrize("case", [str(c) for c in SIM["cases"]])
+def test_replay_reads_the_reference_logs(case):
+    """coverage.Replay (the forced replay of tests/test_gpu_coverage.py) hands the
+    drivers the reference's own state: positions at t are the moves of t - 1 (an
+    explorer to its logged argmax XMax -- the reference logs the agent's own y as
+    "YMax", so the y is checked against the position -- an exploiter to its logged
+    centroid, sim:945-951); the Lloyd seeds at t are the centroids of t - 1 (the
+    start positions at t = 0); the samples at t sit at the explorers' positions."""
+    agents, iterations, _ = (int(v) for v in SIM[case + "_meta"])
+    A = runner.AGENT_COLUMNS
+    for s in SIM[case + "_seeds"]:
+        ag, sa = SIM[f"{case}_s{s}_agent"], SIM[f"{case}_s{s}_sample"]
+        rp = C.Replay(ag, sa)
+        np.testing.assert_array_equal(rp.lloyd_seeds(0), rp.positions(0))
+        for t in range(iterations):
+            pos = rp.positions(t)
+            assert pos.shape == (agents, 2)
+            _, explore = rp.decisions(t)
+            xn, yn, idn = rp.samples(t)
+            assert xn.shape[0] == yn.shape[0] == idn.shape[0] == int(explore.sum())
+            np.testing.assert_array_equal(xn, pos[idn[:, 0].astype(int)])
+            if t == 0:
+                continue
+            prev = ag[_col(ag, A, "Iteration") == t - 1]
+            prev = prev[np.argsort(_col(prev, A, "Agent"), kind="stable")]
+            cen = np.column_stack([_col(prev, A, "XCentroid"), _col(prev, A, "YCentroid")])
+            np.testing.assert_array_equal(rp.lloyd_seeds(t), cen)
+            for i in range(agents):
+                if explore[i, 0]:
+                    assert pos[i, 0] == _col(prev, A, "XMax")[i]
+                else:
+                    np.testing.assert_array_equal(pos[i], cen[i])

@@ -5,7 +5,11 @@ Prints one JSON line: points chosen, wall time, time per iteration, and the CPU
 oracle's time for ONE iteration of the same loop (refactor + diag predict at the
 final size) for scale.
 
-usage: python tools/bench_planner.py [--nh 512] [--frac 0.5] [--cpu]
+With --batch B: B such GPs (seeds 0..B-1), compute_sample_points_batch (one
+batched step per iteration, mfgp_batch_sample_points) against the same B loops
+run one model at a time; the line reports both and whether the point sets agree.
+
+usage: python tools/bench_planner.py [--nh 512] [--frac 0.5] [--cpu] [--batch 8]
 """
 import argparse
 import json
@@ -26,7 +30,10 @@ def main():
     p.add_argument("--nh", type=int, default=512)
     p.add_argument("--frac", type=float, default=0.5)
     p.add_argument("--cpu", action="store_true")
+    p.add_argument("--batch", type=int, default=0)
     a = p.parse_args()
+    if a.batch:
+        return batch(a)
     from mfgp_coverage_amd import gaussian_process as gp, synthetic
     from mfgp_coverage_amd.planners import compute_sample_points
     hyp = synthetic.HYP["australia8_mf"]
@@ -49,6 +56,37 @@ def main():
         t0 = time.perf_counter()
         O.mf_diag(wl.XL, wl.yL, XH, yH, hyp, wl.xs)
         out["cpu_oracle_s_per_iteration"] = time.perf_counter() - t0
+    print(json.dumps(out), flush=True)
+
+
+def batch(a):
+    from mfgp_coverage_amd import gaussian_process as gp, synthetic
+    from mfgp_coverage_amd.planners import compute_sample_points, compute_sample_points_batch
+    hyp = synthetic.HYP["australia8_mf"]
+    ms, thr = [], []
+    for s in range(a.batch):
+        wl = synthetic.Workload(a.grid, a.nl, a.nh, 1, 1, seed=s)
+        m = gp.MFGP(wl.XL, wl.yL[:, None], wl.XH, wl.yH[:, None], 1, 1)
+        m.hyp = hyp.copy()
+        m.updt_info(m.X_L, m.y_L, m.X_H, m.y_H)
+        _, cov = m.predict(wl.xs)
+        ms.append(m)
+        thr.append(a.frac * float(np.amax(cov)))
+    xs = wl.xs
+    compute_sample_points_batch(ms, xs, [0.99 * t / a.frac for t in thr])   # warm-up
+    compute_sample_points(ms[0], xs, 0.99 * thr[0] / a.frac, False)
+    t0 = time.perf_counter()
+    pb = compute_sample_points_batch(ms, xs, thr)
+    tb = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ps = [compute_sample_points(m, xs, t, False) for m, t in zip(ms, thr)]
+    t1 = time.perf_counter() - t0
+    same = [int(np.array_equal(x, y)) for x, y in zip(pb, ps)]
+    its = max(p.shape[0] for p in pb)
+    out = {"batch": a.batch, "points": [int(p.shape[0]) for p in pb], "batched_s": tb, "one_at_a_time_s": t1,
+           "speedup": t1 / tb, "batched_ms_per_iteration": 1e3 * tb / max(1, its),
+           "seed_iterations_per_s": sum(p.shape[0] for p in pb) / tb, "equal_to_single": same,
+           "grid": a.grid, "N_start": a.nl + a.nh, "threshold_frac": a.frac}
     print(json.dumps(out), flush=True)
 
 
