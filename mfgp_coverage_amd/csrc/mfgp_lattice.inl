@@ -274,9 +274,12 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   const int r = lane & 15, q = lane >> 4;
   const unsigned epoch = d.epoch;
   WTRACE(0);
-  // a share of the new rows' separable tables (read from the next launch on)
   const int k = (int)(d.N - n0);
-  {
+  // a share of the new rows' separable tables and lattice indices: read by the
+  // GEMM's cells (in this launch, G1; after it, lat_g2) and by later steps. With
+  // the GEMM as a second launch they are stored after the unit's F stream, off the
+  // stream's start (two dependent round trips: the rows' coordinates, then the grid)
+  auto tables_share = [&]() {
     const int64_t tabw = d.tabw, tstride = (d.ld) * tabw;
     const int64_t tot = 4 * (int64_t)k * tabw;
     const int64_t per = (tot + U - 1) / U, e0 = u * per;
@@ -287,15 +290,15 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       const int a = (int)(rem / tabw);
       const int64_t col = rem % tabw;
       const double* pt = row_pt(d, n0 + a);
-      // written through: the GEMM tiles' epilogues read them in this launch
+      // written through: the GEMM tiles' epilogues read them in this launch (G1)
       stx<true>(&d.tab[t * tstride + (n0 + a) * tabw + col], lat_tab_value(d, t, n0 + a, col, pt[0], pt[1]));
     }
-    // the new rows' lattice indices (read from the next launch on)
     if (u == 0 && tid < k) {
       const double* pt = row_pt(d, n0 + tid);
       d.lidx[n0 + tid] = lattice_xy(d, pt[0], pt[1]);
     }
-  }
+  };
+  if (!d.lat_g2) tables_share();
   const int64_t C = (n0 + 15) / 16;
   const int64_t K2 = 2 * C - 4 * (nwb - 1);
   const int64_t S = (nwb / 2) * K2 + (nwb & 1) * (C - 4 * (nwb / 2));
@@ -545,7 +548,10 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   }
   __syncthreads();
   const int nlast = lastm[0];
-  if (nlast == 0) return;
+  if (nlast == 0) {
+    if (d.lat_g2) tables_share();
+    return;
+  }
   // the blocks' w: every contributor's partial in slot order (the same bits whoever
   // is last), stored, then counted into ldone[0] together (one lane each; the Z
   // units wait for all nwb blocks)
@@ -608,6 +614,7 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       }
     __syncthreads();   // Wh is reused by the next block
   }
+  if (d.lat_g2) tables_share();
 }
 
 // Wait (wave 0 polls, the workgroup joins at the barrier) until flags f[0, n)
