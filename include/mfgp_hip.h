@@ -139,7 +139,12 @@ int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL,
 /* updt (gp:257-268) / updt_hifi (gp:531-542): append k >= 0 rows and refactor.
  * When the previous append was followed by a predict (the simulator's step), the
  * append also runs the one-pass predict in the same launch and keeps the result
- * for the next mfgp_predict; a non-PD step is still reported here. */
+ * for the next mfgp_predict; a non-PD step is still reported here. That launch
+ * publishes the step's positive-definiteness verdict as soon as it has it, and
+ * mfgp_append returns then, while the launch computes the posterior: the next
+ * entry point called on the context waits for the launch first (and reports a
+ * failure of its later phases, e.g. a hand-off wait's timeout), so the caller's
+ * host work in between overlaps it (MFGP_EARLY_PD=0: return at the launch's end). */
 int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k);
 
 /* predict (gp:121-148 / gp:401-438): posterior mean and the diagonal of the
@@ -155,6 +160,12 @@ int mfgp_predict(mfgp_model* m, double* mu, double* var);
  * pool for its next host-bound predict, so a predict of an unchanged model after
  * a view recomputes. M = 0: *mu = *var = *view = NULL. */
 int mfgp_predict_view(mfgp_model* m, double** mu, double** var, void** view);
+/* mfgp_predict_view that may hand over the buffer of an eager append's launch
+ * still computing into it (mfgp_append above): then *running = 1 and the caller
+ * must call mfgp_ctx_synchronize before it reads the buffer or gives it to anyone
+ * (the drop-in predict wraps the arrays meanwhile); else *running = 0 and it is
+ * mfgp_predict_view. */
+int mfgp_predict_view_running(mfgp_model* m, double** mu, double** var, void** view, int* running);
 /* Return a buffer handed over by mfgp_predict_view (any thread, any time, also
  * after its model or context is destroyed). */
 int mfgp_release_view(void* view);

@@ -67,6 +67,9 @@ SIGNATURES = {
     "mfgp_predict": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mfgp_predict_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                          ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)]),
+    "mfgp_predict_view_running": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_int)]),
     "mfgp_release_view": (ctypes.c_int, [ctypes.c_void_p]),
     "mfgp_model_n": (ctypes.c_int64, [ctypes.c_void_p]),
     "mfgp_model_nl": (ctypes.c_int64, [ctypes.c_void_p]),
@@ -320,13 +323,20 @@ class Model:
         """predict() without the host copy: (mu, var) are writable arrays over the
         model's pinned result buffer, handed over to them (mfgp_predict_view); the
         buffer goes back to the library's pool when both arrays are gone."""
-        mu_p, var_p, view = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
-        check(lib().mfgp_predict_view(self.handle, ctypes.byref(mu_p), ctypes.byref(var_p), ctypes.byref(view)))
-        M = lib().mfgp_model_m(self.handle)
+        mu_p, var_p, view, running = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int(0)
+        L = lib()
+        check(L.mfgp_predict_view_running(self.handle, ctypes.byref(mu_p), ctypes.byref(var_p), ctypes.byref(view),
+                                          ctypes.byref(running)))
+        M = L.mfgp_model_m(self.handle)
         if not view.value:
             return np.empty(M, dtype=np.float64), np.empty(M, dtype=np.float64)
         lease = _ViewLease(view.value)
-        return np.asarray(_HostView(mu_p.value, M, lease)), np.asarray(_HostView(var_p.value, M, lease))
+        mu, var = np.asarray(_HostView(mu_p.value, M, lease)), np.asarray(_HostView(var_p.value, M, lease))
+        if running.value:
+            # the eager append's launch was still computing into the buffer: the arrays
+            # were wrapped meanwhile and are given out once it has ended
+            check(L.mfgp_ctx_synchronize(self.ctx.handle))
+        return mu, var
 
     def factor(self):
         n = lib().mfgp_model_n(self.handle)

@@ -137,6 +137,13 @@ struct mfgp_ctx {
   int lat_zcsr = 1;           // the Z units read member lists built by one scan unit per part
                               // instead of bucketing every row themselves (MFGP_LAT_ZCSR=0: off)
   int64_t spin_us = 2000;     // host polling of mapped status words before a synchronise (MFGP_SPIN_US; 0: off)
+  // the eager append of one GP (spec_append_predict) returns at the step's L22
+  // verdict, published by the launch as soon as it is known, instead of at the
+  // launch's end: the caller's host work until its next call (the simulator's
+  // grid check, the predict's argument handling) overlaps the posterior
+  // (MFGP_EARLY_PD=0: wait for the launch's end)
+  bool early_pd = true;
+  bool early_running = false;  // such a launch may still run: the next entry point settles it first
   bool desc_arg = true;       // a batch step that is one k_inc_lat / k_inc_stream launch passes its
                               // descriptors by value
                               // (MFGP_DESC_ARG=0: upload them, diagnostics)
@@ -166,7 +173,8 @@ struct mfgp_model {
   double* zv = nullptr;     // [cap] z = L^-1 (y - m)
   double* iscr = nullptr;   // incremental-append scratch (inc_scratch_doubles(cap))
   int* status = nullptr;
-  int* status_host = nullptr;       // mapped pinned word the single-GP fused launch publishes status into
+  int* status_host = nullptr;       // mapped pinned words the single-GP fused launch publishes into:
+                                    // [0] its status (last act), [1] the L22 verdict (pd_host)
   int* status_host_dev = nullptr;   // its device address
   bool factored = false;
   int64_t factor_N = -1;    // rows [0, factor_N) of A / Linv / zv hold the current factor
@@ -525,6 +533,11 @@ void release_slot_unread(mfgp_ctx* c, int slot) { c->ring_used[slot] = false; }
 
 constexpr int STATUS_UNSET = INT_MIN + 1;   // status_host before the launch writes it
 
+// An eager append that returned at its L22 verdict (mfgp_ctx::early_pd) may still
+// run: every entry point waits for it, and takes its status, before it reads or
+// reuses anything the launch touches.
+int settle(mfgp_ctx* c) { return (c && c->early_running) ? mfgp_ctx_synchronize(c) : MFGP_OK; }
+
 void fill_desc(GPDesc& d, mfgp_model* m) {
   d.X = m->X;
   d.y = m->y;
@@ -548,6 +561,7 @@ void fill_desc(GPDesc& d, mfgp_model* m) {
   d.gate = m->gate_dev;
   d.status = m->status;
   d.status_host = nullptr;
+  d.pd_host = nullptr;
   d.srcX = nullptr;
   d.srcY = nullptr;
   d.k_new = 0;
@@ -1352,6 +1366,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
   c->stream = c->own;
   if (const char* e = std::getenv("MFGP_DESC_ARG")) c->desc_arg = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_SPIN_US")) c->spin_us = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("MFGP_EARLY_PD")) c->early_pd = std::atoi(e) != 0;
   if (const char* e = std::getenv("MFGP_LAT_ZCSR")) c->lat_zcsr = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("MFGP_RSPLIT")) {
     const int r = std::atoi(e);
@@ -1381,6 +1396,7 @@ int mfgp_ctx_create(int device, mfgp_ctx** out) {
 
 void mfgp_ctx_destroy(mfgp_ctx* c) {
   const DeviceGuard dg_(c ? c->device : -1);
+  (void)settle(c);
   if (!c) return;
   (void)hipStreamSynchronize(c->stream);
   (void)drain_timing(c);
@@ -1397,6 +1413,7 @@ void mfgp_ctx_destroy(mfgp_ctx* c) {
 
 int mfgp_ctx_trim(mfgp_ctx* c) {
   const DeviceGuard dg_(c ? c->device : -1);
+  if (const int rc_ = settle(c)) return rc_;
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->vscr) HIP_TRY(hipFree(c->vscr));
@@ -1410,6 +1427,7 @@ int mfgp_ctx_trim(mfgp_ctx* c) {
 
 int mfgp_ctx_set_stream(mfgp_ctx* c, void* s) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->stream = s ? (hipStream_t)s : c->own;
   return MFGP_OK;
@@ -1420,6 +1438,7 @@ void* mfgp_ctx_get_stream(mfgp_ctx* c) { return c ? (void*)c->stream : nullptr; 
 int mfgp_ctx_synchronize(mfgp_ctx* c) {
   const DeviceGuard dg_(c ? c->device : -1);
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  c->early_running = false;
   int rc = ensure_h_status(c, c->async_status.size());
   if (rc) return rc;
   // the status words come back through pinned memory with the stream's last copies
@@ -1543,6 +1562,7 @@ int mfgp_ctx_reset_timing(mfgp_ctx* c) {
 int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int nhyp, double jitter,
                       mfgp_model** out) {
   const DeviceGuard dg_(c ? c->device : -1);
+  if (const int rc_ = settle(c)) return rc_;
   if (!c || !out) return set_err(MFGP_ERR_ARG, "null ctx/out");
   *out = nullptr;
   if (kind != MFGP_SF && kind != MFGP_MF) return set_err(MFGP_ERR_ARG, "kind must be MFGP_SF or MFGP_MF");
@@ -1575,6 +1595,7 @@ int mfgp_model_create(mfgp_ctx* c, int kind, int dtype, const double* hyp, int n
 
 void mfgp_model_destroy(mfgp_model* m) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  (void)settle(m ? m->ctx : nullptr);
   if (!m) return;
   if (m->ctx) {
     (void)hipStreamSynchronize(m->ctx->stream);
@@ -1602,6 +1623,7 @@ void mfgp_model_destroy(mfgp_model* m) {
 
 int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
   const DeviceGuard dg_(src ? src->ctx->device : -1);
+  if (const int rc_ = settle(src ? src->ctx : nullptr)) return rc_;
   int rc = check_model(src);
   if (rc) return rc;
   if (!out) return set_err(MFGP_ERR_ARG, "null out");
@@ -1651,6 +1673,7 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
 
 int mfgp_model_set_hyp(mfgp_model* m, const double* hyp, int nhyp, double jitter) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   if (!hyp || nhyp != m->nhyp)
@@ -1708,6 +1731,7 @@ GridLattice detect_lattice(const double* g, int64_t M) {
 
 int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   if (M < 0 || (M > 0 && !xs)) return set_err(MFGP_ERR_ARG, "bad grid");
@@ -1737,6 +1761,7 @@ int mfgp_set_grid(mfgp_model* m, const double* xs, int64_t M) {
 int mfgp_set_data(mfgp_model* m, const double* XL, const double* yL, int64_t NL, const double* XH,
                   const double* yH, int64_t NH) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   if (NL < 0 || NH < 0) return set_err(MFGP_ERR_ARG, "negative sizes");
@@ -1755,6 +1780,7 @@ int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t
 
 int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   if (k < 0) return set_err(MFGP_ERR_ARG, "negative k");
@@ -1780,6 +1806,7 @@ int mfgp_append(mfgp_model* m, const double* X, const double* y, int64_t k) {
 
 int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   if (n_keep_hifi != m->NH) m->spec_valid = false;
@@ -1800,6 +1827,7 @@ int mfgp_truncate(mfgp_model* m, int64_t n_keep_hifi) {
 
 int mfgp_batch_truncate(mfgp_model** models, int count, int64_t n_keep_hifi) {
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
+  if (const int rc_ = settle((models && count > 0 && models[0]) ? models[0]->ctx : nullptr)) return rc_;
   if (count < 0 || (count > 0 && !models)) return set_err(MFGP_ERR_ARG, "bad batch");
   for (int i = 0; i < count; ++i) {
     const int rc = mfgp_truncate(models[i], n_keep_hifi);
@@ -1817,9 +1845,29 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
 // here, as by update_factor), with mu | var kept for the next predict.
 int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t k) {
   mfgp_ctx* c = m->ctx;
-  int rc = ensure_spec_out(m);
+  int rc = settle(c);
+  if (rc == MFGP_OK) rc = ensure_spec_out(m);
   if (rc) return rc;
+  if (m->status_host) reinterpret_cast<volatile int*>(m->status_host)[1] = STATUS_UNSET;
   rc = batch_run(&m, 1, X, y, &k, m->spec_out_dev, m->spec_out_dev + m->spec_cap, nullptr, nullptr, MFGP_ASYNC, true, true);
+  if (rc == MFGP_OK && c->early_pd && c->spin_us > 0 && m->status_host && c->async_status.size() == 1 &&
+      c->async_status[0].host == m->status_host) {
+    // the launch publishes the L22 verdict of the step (the only status its
+    // factor can fail with) into the model's second mapped word: a positive
+    // definite step returns now, and the next entry point settles the launch
+    // (its outputs, hang guards) before anything reads or reuses its buffers
+    const volatile int* w = reinterpret_cast<const volatile int*>(m->status_host) + 1;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*w == STATUS_UNSET) {
+      __builtin_ia32_pause();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->spin_us)) break;
+    }
+    if (*w == INT_MAX) {
+      c->early_running = true;
+      m->spec_valid = true;
+      return MFGP_OK;
+    }
+  }
   if (rc == MFGP_OK) rc = mfgp_ctx_synchronize(c);
   if (rc != MFGP_OK) {
     m->factored = false;   // a failed step leaves no usable factor
@@ -1829,17 +1877,27 @@ int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t
   return MFGP_OK;
 }
 
-int mfgp_predict_view(mfgp_model* m, double** mu, double** var, void** view) {
+static int predict_view(mfgp_model* m, double** mu, double** var, void** view, int* running) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
   int rc = check_model(m);
   if (rc) return rc;
   if (!mu || !var || !view) return set_err(MFGP_ERR_ARG, "null output");
   *mu = *var = nullptr;
   *view = nullptr;
-  if (m->M == 0) return mfgp_predict(m, nullptr, nullptr);
-  if ((rc = ensure_spec_out(m))) return rc;
-  // the predict's host outputs are the result buffer itself: no copy
-  if ((rc = mfgp_predict(m, m->spec_out, m->spec_out + m->spec_cap))) return rc;
+  if (running) *running = 0;
+  if (running && m->ctx->early_running && m->spec_valid && m->spec_out && m->M > 0 && factor_current(m)) {
+    // the result of the eager append still being computed into the buffer handed
+    // over here: the caller wraps it, then settles (mfgp_ctx_synchronize) before it
+    // reads it or lets anyone else
+    *running = 1;
+    m->pred_since_append = true;
+  } else {
+    if ((rc = settle(m->ctx))) return rc;
+    if (m->M == 0) return mfgp_predict(m, nullptr, nullptr);
+    if ((rc = ensure_spec_out(m))) return rc;
+    // the predict's host outputs are the result buffer itself: no copy
+    if ((rc = mfgp_predict(m, m->spec_out, m->spec_out + m->spec_cap))) return rc;
+  }
   ViewBuf* v = new ViewBuf{m->spec_out, m->spec_cap};
   *mu = m->spec_out;
   *var = m->spec_out + m->spec_cap;
@@ -1850,6 +1908,15 @@ int mfgp_predict_view(mfgp_model* m, double** mu, double** var, void** view) {
   m->spec_cap = 0;
   m->spec_valid = false;
   return MFGP_OK;
+}
+
+int mfgp_predict_view(mfgp_model* m, double** mu, double** var, void** view) {
+  return predict_view(m, mu, var, view, nullptr);
+}
+
+int mfgp_predict_view_running(mfgp_model* m, double** mu, double** var, void** view, int* running) {
+  if (!running) return set_err(MFGP_ERR_ARG, "null output");
+  return predict_view(m, mu, var, view, running);
 }
 
 int mfgp_release_view(void* view) {
@@ -1870,6 +1937,7 @@ int mfgp_release_view(void* view) {
 
 int mfgp_predict(mfgp_model* m, double* mu, double* var) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   mfgp_ctx* c = m->ctx;
@@ -1954,6 +2022,7 @@ int64_t mfgp_model_m(const mfgp_model* m) { return m ? m->M : -1; }
 
 int mfgp_get_factor(mfgp_model* m, double* L_out) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   if ((rc = update_factor(m))) return rc;
@@ -2196,7 +2265,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       // ~40 us of host work between launches: rocprofv3, tools/prof_dropin.sh), so
       // the fixed cost is priced at 64 and one GP at this size keeps the V stream;
       // configs[4] (32 GPs, 256x256, N = 8192, fp32 V) 11.2 / 2.4 ms
-      double vs_us = 10.0, lat_us = 64.0;
+      double vs_us = 10.0, lat_us = 50.0;
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];
         const double n0 = (double)hd[i].n0, es = m->dtype == MFGP_F32 ? 4.0 : 8.0;
@@ -2311,13 +2380,15 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
     if (single) {
       mfgp_model* m = order[0];
       if (!m->status_host) {
-        HIP_TRY(hipHostMalloc(&m->status_host, sizeof(int), hipHostMallocMapped));
+        HIP_TRY(hipHostMalloc(&m->status_host, 2 * sizeof(int), hipHostMallocMapped));
         void* dev = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&dev, m->status_host, 0));
         m->status_host_dev = static_cast<int*>(dev);
       }
       *reinterpret_cast<volatile int*>(m->status_host) = STATUS_UNSET;
+      reinterpret_cast<volatile int*>(m->status_host)[1] = STATUS_UNSET;
       hd[0].status_host = m->status_host_dev;
+      hd[0].pd_host = m->status_host_dev + 1;
       for (auto it = c->async_status.rbegin(); it != c->async_status.rend(); ++it)
         if (it->m == m) {
           it->host = m->status_host;
@@ -2394,6 +2465,7 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
 // loop did not append (the leading rows' factor and V stay valid).
 int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, double* points, int64_t* count) {
   const DeviceGuard dg_(model ? model->ctx->device : -1);
+  if (const int rc_ = settle(model ? model->ctx : nullptr)) return rc_;
   int rc = check_model(model);
   if (rc) return rc;
   if (!count || (max_points > 0 && !points)) return set_err(MFGP_ERR_ARG, "null output");
@@ -2511,6 +2583,7 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
 int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thresholds, int64_t max_points,
                              double* points, int64_t* counts) {
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
+  if (const int rc_ = settle((models && count > 0 && models[0]) ? models[0]->ctx : nullptr)) return rc_;
   if (count <= 0 || !models || !thresholds || !counts || (max_points > 0 && !points))
     return set_err(MFGP_ERR_ARG, "bad batch_sample_points arguments");
   if (max_points < 0) return set_err(MFGP_ERR_ARG, "negative max_points");
@@ -2724,6 +2797,7 @@ int mfgp_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncells, con
                      const double* seeds, const double* w, const double* f, const double* var, double* out,
                      int64_t* argmax) {
   const DeviceGuard dg_(c ? c->device : -1);
+  if (const int rc_ = settle(c)) return rc_;
   return cell_reduce_impl(c, grid, M, ncells, vstart, verts, seeds, nullptr, 1, w, f, var, out, argmax);
 }
 
@@ -2731,6 +2805,7 @@ int mfgp_batch_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncell
                            const double* verts, const double* seeds, const int* field, int nfield, const double* w,
                            const double* f, const double* var, double* out, int64_t* argmax) {
   const DeviceGuard dg_(c ? c->device : -1);
+  if (const int rc_ = settle(c)) return rc_;
   if (!field) return set_err(MFGP_ERR_ARG, "null field");
   return cell_reduce_impl(c, grid, M, ncells, vstart, verts, seeds, field, nfield, w, f, var, out, argmax);
 }
@@ -2739,6 +2814,7 @@ int mfgp_batch_cell_reduce(mfgp_ctx* c, const double* grid, int64_t M, int ncell
 // for the model's data under the given hyperparameters (the model is unchanged).
 int mfgp_nlml(mfgp_model* m, const double* hyp, int nhyp, double* nlml, double* grad) {
   const DeviceGuard dg_(m ? m->ctx->device : -1);
+  if (const int rc_ = settle(m ? m->ctx : nullptr)) return rc_;
   int rc = check_model(m);
   if (rc) return rc;
   if (!hyp || nhyp != m->nhyp)
@@ -2827,6 +2903,7 @@ int mfgp_nlml(mfgp_model* m, const double* hyp, int nhyp, double* nlml, double* 
 int mfgp_batch_append_predict(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                               double* mu, double* var, int flags) {
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
+  if (const int rc_ = settle((models && count > 0 && models[0]) ? models[0]->ctx : nullptr)) return rc_;
   return batch_run(models, count, X, y, k, mu, var, nullptr, nullptr, flags, true, true);
 }
 
@@ -2834,6 +2911,7 @@ int mfgp_batch_append_predict_ex(mfgp_model** models, int count, const double* X
                                  const int64_t* k, double* mu, double* var, double* var_max, int64_t* var_argmax,
                                  int flags) {
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
+  if (const int rc_ = settle((models && count > 0 && models[0]) ? models[0]->ctx : nullptr)) return rc_;
   if ((var_max && !is_device_ptr(var_max)) || (var_argmax && !is_device_ptr(var_argmax)))
     return set_err(MFGP_ERR_ARG, "var_max / var_argmax must be device memory");
   return batch_run(models, count, X, y, k, mu, var, var_max, var_argmax, flags, true, true);
@@ -2842,11 +2920,13 @@ int mfgp_batch_append_predict_ex(mfgp_model** models, int count, const double* X
 int mfgp_batch_append_factor(mfgp_model** models, int count, const double* X, const double* y, const int64_t* k,
                              int flags) {
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
+  if (const int rc_ = settle((models && count > 0 && models[0]) ? models[0]->ctx : nullptr)) return rc_;
   return batch_run(models, count, X, y, k, nullptr, nullptr, nullptr, nullptr, flags, true, false);
 }
 
 int mfgp_batch_predict(mfgp_model** models, int count, double* mu, double* var, int flags) {
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
+  if (const int rc_ = settle((models && count > 0 && models[0]) ? models[0]->ctx : nullptr)) return rc_;
   return batch_run(models, count, nullptr, nullptr, nullptr, mu, var, nullptr, nullptr, flags, false, true);
 }
 

@@ -77,6 +77,8 @@ struct GPDesc {
   int* status;         // INT_MAX = ok, else 1 + first non-positive pivot row
   int* status_host;    // k_inc_stream with cell tiles: the launch's last cell group copies *status here
                        // (mapped pinned host word: the host reads it without a copy), or null
+  int* pd_host;        // the fused step's L22 verdict (INT_MAX = positive definite, else the
+                       // status value), published as soon as the finish knows it, or null
   const double* srcX;  // device rows to append at row N - k_new (k_append), or null
   const double* srcY;
   int64_t k_new;

@@ -1497,6 +1497,9 @@ __device__ __forceinline__ void inc_finish(const GPDesc& d, double* sm, int64_t 
       stx<FUSED>(&d.l22r[KINC * KINC + lane], x);
     }
     if (fail != INT_MAX && lane == 0) atomicMin(d.status, fail);
+    // the step's positive-definiteness verdict as soon as it is known (a mapped host
+    // word: the eager append returns here while the posterior is still computed)
+    if (FUSED && d.pd_host && lane == 0) __hip_atomic_store(d.pd_host, fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (FUSED) {
       drain_stores();
       if (lane == 0) publish(d.sync + 2, d.epoch);   // L22 and z2 are in A / zv

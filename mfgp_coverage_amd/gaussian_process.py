@@ -328,15 +328,25 @@ class MFGP(_DeviceGP):
     def updt_hifi(self, X_H_addition, y_H_addition):
         """gaussian_process.py:531-542: append hifi rows (k >= 0) and refactor."""
         prev = (self.X_L, self.y_L, self.X_H, self.y_H)
-        self.X_H = np.vstack((self.X_H, X_H_addition))
-        self.y_H = np.vstack((self.y_H, y_H_addition))
         syn = self.__dict__.get("_synced")
-        if syn is not None and all(a is b for a, b in zip(syn, prev)):
+        xa, ya = np.atleast_2d(X_H_addition), np.atleast_2d(y_H_addition)
+        if (syn is not None and all(a is b for a, b in zip(syn, prev)) and xa.ndim == 2 and ya.ndim == 2
+                and xa.shape[1:] == np.shape(self.X_H)[1:] and ya.shape[1:] == np.shape(self.y_H)[1:]):
+            # the rows go to the device first: the append returns at the step's
+            # positive-definiteness verdict, and the host copies below overlap the
+            # posterior the launch is still computing (the reference stacks before it
+            # factors; a non-PD append still leaves the stacked rows, as there)
             self._push_hyp()
             self.__dict__["_synced"] = None
-            self._dev().append(_as2(X_H_addition), _as1(y_H_addition))
+            try:
+                self._dev().append(_as2(X_H_addition), _as1(y_H_addition))
+            finally:
+                self.X_H = np.vstack((self.X_H, X_H_addition))
+                self.y_H = np.vstack((self.y_H, y_H_addition))
             self.__dict__["_synced"] = (self.X_L, self.y_L, self.X_H, self.y_H)
         else:
+            self.X_H = np.vstack((self.X_H, X_H_addition))
+            self.y_H = np.vstack((self.y_H, y_H_addition))
             self.__dict__["_synced"] = None
             self._sync_data()
 

@@ -601,6 +601,64 @@ def test_speculative_append_not_pd_raises_at_append():
         m.append(X[20:21], y[20:21])       # speculative form (after a predict): raises here
 
 
+def test_early_verdict_append_then_other_calls():
+    """The eager append of one GP returns at the step's L22 verdict (the launch
+    publishes it before it computes the posterior): every later call -- factor
+    download, clone, truncate, a second append, destroy, a predict -- first waits
+    for that launch, so each sees the appended state."""
+    import gc
+
+    from mfgp_coverage_amd import _lib
+    Xs, X, y = _points(36, 420, seed=17, ongrid=True)
+    NL, n = 150, 270
+    m, hyp = _model(_lib.context(), "mf", X[:n], y[:n], NL, Xs)
+    m.predict()
+    m.append(X[n:n + 8], y[n:n + 8])
+    n += 8
+    L = m.factor()                                         # right after the early return
+    assert L.shape == (n, n) and np.all(np.isfinite(L))
+    m.predict()
+    m.append(X[n:n + 8], y[n:n + 8])
+    n += 8
+    c = m.clone()                                          # clone of a launch still running
+    mu_c, var_c = c.predict()
+    mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs, hyp)
+    assert _err(mu_c, var_c, mu_r, var_r, hyp) < TOL
+    mu, var = m.predict()
+    assert _err(mu, var, mu_r, var_r, hyp) < TOL
+    m.append(X[n:n + 4], y[n:n + 4])
+    m.truncate(n - NL - 2)                                 # truncate while it runs
+    n -= 2
+    mu, var = m.predict()
+    mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs, hyp)
+    assert _err(mu, var, mu_r, var_r, hyp) < TOL
+    c.append(X[n:n + 8], y[n:n + 8])
+    del c                                                  # destroyed while its launch runs
+    gc.collect()
+    m.append(X[n:n + 8], y[n:n + 8])
+    n += 8
+    mu, var = m.predict()
+    mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs, hyp)
+    assert _err(mu, var, mu_r, var_r, hyp) < TOL
+
+
+def test_dropin_updt_hifi_not_pd_raises_and_stacks(gp_mod):
+    """The drop-in updt_hifi sends the rows to the device before it stacks them on
+    the host (the append returns at the verdict; the stacking overlaps the launch):
+    a non-PD append still raises LinAlgError at updt_hifi and leaves the stacked
+    rows, as the reference does (it stacks, then factors: gp:531-542)."""
+    Xs, X, y = _points(24, 30, seed=2, ongrid=True)
+    m = gp_mod.MFGP(X[:20], y[:20, None], np.empty((0, 2)), np.empty((0, 1)), 1, 1)
+    m.hyp = np.array([0.0, 0.0, -1.0, 0.0, -3.0, -1.0, -1.0, 2.0, -20.0])
+    m.jitter = -1.0
+    m.predict(Xs)
+    m.updt_hifi(X[20:20], y[20:20, None])
+    m.predict(Xs)
+    with pytest.raises(np.linalg.LinAlgError):
+        m.updt_hifi(X[20:21], y[20:21, None])
+    assert m.X_H.shape == (1, 2) and m.y_H.shape == (1, 1)
+
+
 def _bad_and_good(ctx, Xs, X, y):
     """A model whose next append is not positive definite (negative jitter, as in
     test_speculative_append_not_pd_raises_at_append) and a well-posed one."""
