@@ -871,7 +871,7 @@ int enqueue_factor(mfgp_ctx* c, const GPDesc* dd, const GPDesc* hd, int count) {
   for (int64_t K0 = 0; K0 < max_nb; K0 += FD) {
     const int64_t K1 = std::min<int64_t>(K0 + FD, max_nb);
     for (int64_t kb = K0; kb < K1; ++kb) {
-      HIP_TRY(launch_potrf_diag(dd, count, (int)kb, 0, cs));
+      HIP_TRY(launch_potrf_diag(dd, count, (int)kb, cs));
       const int64_t below = max_nb - kb - 1;
       if (below <= 0) continue;
       HIP_TRY(launch_panel(dd, count, (int)kb, below, cs));
@@ -2261,10 +2261,10 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       // stream and the GEMM (~0.8 us per million n0^2); the V stream reads 8 n0 M
       // bytes per GP (~5.5 TB/s) -- measured at 128x128, N = 2048 (us per step, V
       // stream / lattice with the second-launch GEMM, round 3): B = 8 345 / 80; B = 1
-      // 60 / 57 back to back, but ~66 / ~67+ in the drop-in simulator's step (one GP,
-      // ~40 us of host work between launches: rocprofv3, tools/prof_dropin.sh), so
-      // the fixed cost is priced at 64 and one GP at this size keeps the V stream;
-      // configs[4] (32 GPs, 256x256, N = 8192, fp32 V) 11.2 / 2.4 ms
+      // 60 / 57 back to back; in the drop-in step (one GP, the eager append returning
+      // at the L22 verdict, round 5: tools/bench_dropin.py) 93.2 / 88.3-90.3 us, so
+      // the fixed cost is priced at 50 and one GP from n0 ~ 1700 (at M = 16384) takes
+      // the lattice; configs[4] (32 GPs, 256x256, N = 8192, fp32 V) 11.2 / 2.4 ms
       double vs_us = 10.0, lat_us = 50.0;
       for (int i = 0; i < ninc; ++i) {
         const mfgp_model* m = order[i];

@@ -178,7 +178,7 @@ inline __host__ __device__ int64_t prow_blocks(int64_t N) { return (N + PRB - 1)
 // Launchers (mfgp_kernels.hip). `d` points to `count` descriptors in device memory.
 hipError_t launch_append(const GPDesc* d, int count, hipStream_t s);
 hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStream_t s);
-hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStream_t s);
+hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, hipStream_t s);
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s);
 hipError_t launch_syrk(const GPDesc* d, int count, int kb, int64_t max_tri, int t0, hipStream_t s);
 hipError_t launch_syrk_blk(const GPDesc* d, int count, int kb0, int nk, int jmin, int jmax, int64_t max_tiles,

@@ -143,35 +143,48 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-// Broadcast lane k of each 16-lane DPP row to the whole row (row_newbcast:k, gfx90a+).
-// The DPP control must be an immediate: the switch folds away once the callers'
-// fully unrolled loops make k a constant.
-// (Every lane reads a valid lane of its row, so no `old` operand is needed: with
-// bound_ctrl the compiler drops the zero-initialising moves of update_dpp.)
+// Broadcast lane k of each 16-lane DPP row to the whole row (row_newbcast:k, gfx90a+):
+// one v_mov_b64 with a 64-bit DPP source. The DPP control must be an immediate: the
+// switch folds away once the callers' fully unrolled loops make k a constant.
+// (s_nop 1: a DPP source written by the previous VALU instruction needs two wait
+// states, which the compiler does not count for inline assembly.)
 template <int K>
 __device__ __forceinline__ double bcast16_(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + K, 0xF, 0xF, true);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + K, 0xF, 0xF, true);
-  return __hiloint2double(hi, lo);
+  double r;
+  asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "i"(K));
+  return r;
 }
+// acc + (lane k's src) * mul (NEG: - ...), one v_fmac_f64 whose first source is the
+// row_newbcast:k DPP operand: a pivot chain's rank-1 update step, or a substitution
+// step, without a separate broadcast (fused multiply-add: the same rounding as
+// acc - b * mul written out)
+template <int K, bool NEG>
+__device__ __forceinline__ double fmac_bcast16_(double acc, double src, double mul) {
+  if (NEG)
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "i"(K));
+  else
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "i"(K));
+  return acc;
+}
+#define MFGP_BCAST16_CASES(F) \
+  F(0) F(1) F(2) F(3) F(4) F(5) F(6) F(7) F(8) F(9) F(10) F(11) F(12) F(13) F(14)
 __device__ __forceinline__ double bcast16(double v, int k) {
   switch (k) {
-    case 0: return bcast16_<0>(v);
-    case 1: return bcast16_<1>(v);
-    case 2: return bcast16_<2>(v);
-    case 3: return bcast16_<3>(v);
-    case 4: return bcast16_<4>(v);
-    case 5: return bcast16_<5>(v);
-    case 6: return bcast16_<6>(v);
-    case 7: return bcast16_<7>(v);
-    case 8: return bcast16_<8>(v);
-    case 9: return bcast16_<9>(v);
-    case 10: return bcast16_<10>(v);
-    case 11: return bcast16_<11>(v);
-    case 12: return bcast16_<12>(v);
-    case 13: return bcast16_<13>(v);
-    case 14: return bcast16_<14>(v);
+#define C_(K) case K: return bcast16_<K>(v);
+    MFGP_BCAST16_CASES(C_)
+#undef C_
     default: return bcast16_<15>(v);
+  }
+}
+template <bool NEG>
+__device__ __forceinline__ double fmac_bcast16(double acc, double src, double mul, int k) {
+  switch (k) {
+#define C_(K) case K: return fmac_bcast16_<K, NEG>(acc, src, mul);
+    MFGP_BCAST16_CASES(C_)
+#undef C_
+    default: return fmac_bcast16_<15, NEG>(acc, src, mul);
   }
 }
 
@@ -191,7 +204,7 @@ __device__ __forceinline__ d4 mfma16(const double* __restrict__ A, int ars, int 
 
 // S: 64x64 row-major (stride SP), lower triangle = the matrix. On exit S = L
 // (zeros above the diagonal) and R = L^-1 (row-major, zeros above).
-__device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R, double* __restrict__ T,
+__device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
                                  double* __restrict__ U, int64_t g0, int64_t N, int* status) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r16 = lane & 15, q16 = lane >> 4;
@@ -217,12 +230,14 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
         fail = bad ? min(fail, (int)(g + 1)) : fail;
         p = (pad || bad) ? 1.0 : p;
         const double rs = rsqrt(p);
-        const double l = (r16 > j) ? d[j] * rs : (r16 == j ? p * rs : 0.0);
+        const double l = (r16 >= j) ? (r16 == j ? p : d[j]) * rs : 0.0;
         rdiag = (r16 == j) ? rs : rdiag;
         d[j] = l;
-        const double lu = (r16 > j) ? l : 0.0;
+        // d[k] -= l_r l_k for every row r: rows r > j are the update; rows r < j have
+        // l_r = 0; row j's columns k > j are above the diagonal (never read: the
+        // store below and the substitution read columns <= the row)
 #pragma unroll
-        for (int k = j + 1; k < DB; ++k) d[k] -= lu * bcast16(l, k);
+        for (int k = j + 1; k < DB; ++k) d[k] = fmac_bcast16<true>(d[k], l, l, k);
       }
       if (fail != INT_MAX && lane == 0) atomicMin(status, fail);
       if (lane < DB) {
@@ -236,15 +251,23 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
       for (int i = 0; i < DB; ++i) {
         double s0 = (i == r16) ? 1.0 : 0.0, s1 = 0.0;
 #pragma unroll
-        for (int m = 0; m < i; ++m) {
-          const double lim = bcast16(d[m], i);
-          if (m & 1) s1 -= lim * x[m]; else s0 -= lim * x[m];
+        for (int m = 0; m < i; ++m) {   // s -= L[i][m] x[m]
+          if (m & 1) s1 = fmac_bcast16<true>(s1, d[m], x[m], i);
+          else s0 = fmac_bcast16<true>(s0, d[m], x[m], i);
         }
         x[i] = (s0 + s1) * bcast16(rdiag, i);
       }
+      // column c of Dinv (zero above the diagonal) into R's diagonal block
       if (lane < DB) {
 #pragma unroll
-        for (int i = 0; i < DB; ++i) T[kk * DB * DP + i * DP + lane] = x[i];
+        for (int i = 0; i < DB; ++i) R[(o + i) * SP + o + lane] = x[i];
+      }
+    } else if (kk == 0) {
+      // the other waves meanwhile: R's blocks above the diagonal are zero
+      for (int e = tid - 64; e < 6 * DB * DB; e += NT - 64) {
+        const int b = e >> 8, i = (e >> 4) & 15, j = e & 15;   // blocks (0,1..3), (1,2..3), (2,3)
+        const int I = b < 3 ? 0 : (b < 5 ? 1 : 2), J = b < 3 ? b + 1 : (b < 5 ? b - 1 : 3);
+        R[(I * DB + i) * SP + J * DB + j] = 0.0;
       }
     }
     __syncthreads();
@@ -254,7 +277,7 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
     if (w < nrest) {
       const int R0 = o + DB + DB * w;
       d4 acc = {0.0, 0.0, 0.0, 0.0};
-      acc = mfma16<false>(S + R0 * SP + o, SP, 1, T + kk * DB * DP, 1, DP, DB, acc, lane);
+      acc = mfma16<false>(S + R0 * SP + o, SP, 1, R + o * SP + o, 1, SP, DB, acc, lane);   // B[k][j] = Dinv[j][k]
 #pragma unroll
       for (int v = 0; v < 4; ++v) S[(R0 + q16 + 4 * v) * SP + o + r16] = acc[v];
     }
@@ -276,13 +299,9 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
     __syncthreads();
     STAMP(4 + 3 * kk);
   }
-  // Linv: diagonal blocks from T, then block rows I = 1..3 by substitution:
+  // Linv: the diagonal blocks are in R (and the blocks above them zero); block rows
+  // I = 1..3 by substitution:
   //   Linv_IJ = -Dinv_I * sum_{m=J}^{I-1} L_Im Linv_mJ      (MFMA, wave w -> J = w)
-  for (int e = tid; e < NB * NB; e += NT) {
-    const int i = e >> 6, j = e & 63;
-    R[i * SP + j] = ((i >> 4) == (j >> 4) && j <= i) ? T[(i >> 4) * DB * DP + (i & 15) * DP + (j & 15)] : 0.0;
-  }
-  __syncthreads();
   STAMP(14);
   for (int I = 1; I < NB / DB; ++I) {
     if (w < I) {
@@ -296,7 +315,7 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-      acc2 = mfma16<true>(T + I * DB * DP, DP, 1, Uj, DP, 1, DB, acc2, lane);
+      acc2 = mfma16<true>(R + (I * DB) * SP + I * DB, SP, 1, Uj, DP, 1, DB, acc2, lane);   // Dinv_I
 #pragma unroll
       for (int v = 0; v < 4; ++v) R[(I * DB + q16 + 4 * v) * SP + J * DB + r16] = acc2[v];
     }
@@ -305,48 +324,19 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
   }
 }
 
-// With `upd`, the tile first receives the last trailing update of the previous
-// step, A_kk -= L_k,k-1 L_k,k-1^T (f64 MFMA), so that the rest of that trailing
-// update can run concurrently on the side stream (look-ahead, see capi).
-__global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb, int upd) {
+__global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ descs, int kb) {
   const GPDesc& d = descs[blockIdx.x];
   const int64_t N = d.N, ld = d.ld;
   if (kb >= nblocks_factor(N)) return;
-  // one LDS array: As/Bs of the update (2 x 32 KB) alias S/R/T/U of the factor
-  __shared__ double sh[2 * NB * SP + (NB / DB) * DB * DP + (NB / DB - 1) * DB * DP];
+  __shared__ double sh[2 * NB * SP + (NB / DB - 1) * DB * DP];
   double* const S = sh;
   double* const R = sh + NB * SP;
-  double* const T = R + NB * SP;
-  double* const U = T + (NB / DB) * DB * DP;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  double* const U = R + NB * SP;
+  const int tid = threadIdx.x;
   const int64_t o = (int64_t)kb * NB;
   double* __restrict__ A = d.A;
   STAMP(0);
-  if (upd && kb > 0) {
-    double* As = sh;
-    load_tile_cm(As, A, ld, o, o - NB, tid);   // L_k,k-1 (A operand and, transposed, B operand)
-    const int r = lane & 15, q = lane >> 4;
-    Acc acc;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          acc.c[mt][nt][v] = A[(o + acc_col(wn, nt, r)) * ld + o + acc_row(wm, mt, q, v)];
-    __syncthreads();
-    tile_mma<true>(As, As, acc, wm, wn, lane);
-    __syncthreads();   // As is overwritten by S below
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int i = acc_row(wm, mt, q, v), j = acc_col(wn, nt, r);
-          S[i * SP + j] = (j <= i) ? acc.c[mt][nt][v] : 0.0;
-        }
-  } else {
+  {
     // unconditional loads (the upper part of the tile is masked afterwards) keep
     // all 16 loads per thread in flight
     double v[NB * NB / NT];
@@ -363,7 +353,7 @@ __global__ __launch_bounds__(NT) void k_potrf_diag(const GPDesc* __restrict__ de
   }
   __syncthreads();
   STAMP(1);
-  factor_invert_64(S, R, T, U, o, N, d.status);
+  factor_invert_64(S, R, U, o, N, d.status);
   double* __restrict__ Li = d.Linv + (int64_t)kb * TILE;
 #pragma unroll 4
   for (int e = tid; e < NB * NB; e += NT) {
@@ -1474,7 +1464,7 @@ __device__ __forceinline__ void inc_finish(const GPDesc& d, double* sm, int64_t 
       dd[j] = l;
       const double lu = (r > j) ? l : 0.0;
 #pragma unroll
-      for (int kk = j + 1; kk < KINC; ++kk) dd[kk] -= lu * bcast16(l, kk);
+      for (int kk = j + 1; kk < KINC; ++kk) dd[kk] = fmac_bcast16<true>(dd[kk], l, lu, kk);   // -= lu * l_kk
     }
     // z2 = L22^-1 (r2 - L21 z1), r2 = y - m_H (new rows are hifi; gp:133 / gp:421)
     double x = 0.0;
@@ -2620,8 +2610,8 @@ hipError_t launch_assemble(const GPDesc* d, int count, int64_t max_tiles, hipStr
   hipLaunchKernelGGL(k_assemble, dim3((unsigned)max_tiles, count), dim3(NT), 0, s, d);
   return hipGetLastError();
 }
-hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, int upd, hipStream_t s) {
-  hipLaunchKernelGGL(k_potrf_diag, dim3(count), dim3(NT), 0, s, d, kb, upd);
+hipError_t launch_potrf_diag(const GPDesc* d, int count, int kb, hipStream_t s) {
+  hipLaunchKernelGGL(k_potrf_diag, dim3(count), dim3(NT), 0, s, d, kb);
   return hipGetLastError();
 }
 hipError_t launch_panel(const GPDesc* d, int count, int kb, int64_t max_below, hipStream_t s) {

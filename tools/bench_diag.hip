@@ -26,21 +26,17 @@ int main() {
   }
   CK(hipMemcpy(dd, hd.data(), sizeof(GPDesc) * B, hipMemcpyHostToDevice));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int it = 0; it < 5; it++) (void)launch_potrf_diag(dd, B, 0, 0, 0);
+  for (int it = 0; it < 5; it++) (void)launch_potrf_diag(dd, B, 0, 0);
   CK(hipDeviceSynchronize());
   const int R = 200; float ms;
   CK(hipEventRecord(e0));
-  for (int it = 0; it < R; it++) (void)launch_potrf_diag(dd, B, 0, 0, 0);
+  for (int it = 0; it < R; it++) (void)launch_potrf_diag(dd, B, 0, 0);
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
   long long s[64]; CK(hipMemcpy(s, dS, 8 * 64, hipMemcpyDeviceToHost));
   printf("k_potrf_diag: %.2f us per launch (B=%d, back-to-back)\n", 1e3 * ms / R, B);
-  CK(hipEventRecord(e0));
-  for (int it = 0; it < R; it++) (void)launch_potrf_diag(dd, B, 1, 1, 0);
-  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms1; CK(hipEventElapsedTime(&ms1, e0, e1));
-  printf("k_potrf_diag with the look-ahead update (kb = 1): %.2f us per launch\n", 1e3 * ms1 / R);
-  const char* nm[] = {"start","load","a0","b0","c0","a1","b1","c1","a2","b2","c2","a3","b3","c3","inv-init","inv1","inv2","inv3","store"};
-  int ids[] = {0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18};
-  for (int q = 1; q < 19; q++) printf("  %-9s %7lld cycles\n", nm[q], s[ids[q]] - s[ids[q-1]]);
+  const char* nm[] = {"start","load","a0","b0","c0","a1","b1","c1","a2","b2","c2","a3","b3","c3","inv1","inv2","inv3","store"};
+  int ids[] = {0,1,2,3,4,5,6,7,8,9,10,11,12,13,15,16,17,18};
+  for (int q = 1; q < 18; q++) printf("  %-9s %7lld cycles\n", nm[q], s[ids[q]] - s[ids[q-1]]);
   printf("  total     %7lld cycles\n", s[18] - s[0]);
   // empty-ish kernel for launch overhead reference
   return 0;
