@@ -1464,7 +1464,7 @@ __device__ __forceinline__ void inc_finish(const GPDesc& d, double* sm, int64_t 
       dd[j] = l;
       const double lu = (r > j) ? l : 0.0;
 #pragma unroll
-      for (int kk = j + 1; kk < KINC; ++kk) dd[kk] = fmac_bcast16<true>(dd[kk], l, lu, kk);   // -= lu * l_kk
+      for (int kk = j + 1; kk < KINC; ++kk) dd[kk] -= lu * bcast16(l, kk);
     }
     // z2 = L22^-1 (r2 - L21 z1), r2 = y - m_H (new rows are hifi; gp:133 / gp:421)
     double x = 0.0;
