@@ -939,24 +939,11 @@ __device__ __forceinline__ void st16_wt(double* p, dv2 v) {
 // device-scope (sc1) loads that L2 does not serve from a possibly stale line, or
 // read plain only when no workgroup of that XCD can have cached the line earlier
 // in the launch (L2 is invalidated at kernel start); the consumer issues its
-// loads after it saw the flag (no speculation). An agent-scope acquire after the
-// wait (MFGP_ACQUIRE builds) states that order in the HIP memory model, but its
-// L2 invalidate costs the lattice step 105 -> 172 us per launch at B = 8 and the
-// drop-in step 87 -> 105 us (tools/ab_acquire.sh): off by default.
-__device__ __forceinline__ void acquire_agent() {
-#ifdef MFGP_ACQUIRE
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-}
-// The narrow form (MFGP_ACQUIRE_NARROW builds): the acquire
-// is made once per wait by the polling wave, right after it saw the flag, and the
-// workgroup barrier that follows carries it to the other waves (no acquire after
-// the barrier in every wave).
-__device__ __forceinline__ void acquire_poller() {
-#ifdef MFGP_ACQUIRE_NARROW
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-}
+// loads after it saw the flag (no speculation). No acquire: an agent-scope
+// acquire after each wait (its L2 invalidate) cost the lattice step 105 -> 172 us
+// per launch at B = 8, and even one per wait on the polling lane 8 % (97.0k vs
+// 89.2k GP-updates/s, round 5): DESIGN 2.2. tests/test_codeobj.py checks the
+// emitted polls (sc1 loads, completed before the branch that leaves the spin).
 __device__ __forceinline__ void publish(unsigned* f, unsigned v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -974,10 +961,8 @@ __device__ void wait_flag(const GPDesc& d, const unsigned* f, unsigned v) {
         break;
       }
     }
-    acquire_poller();
   }
   __syncthreads();
-  acquire_agent();
 }
 
 // Wait (wave 0; the workgroup joins at the barrier) until the compact rows of
@@ -1000,9 +985,8 @@ __device__ void wait_l21(const GPDesc& d) {
         break;
       }
     }
-    acquire_poller();
   }
-  __syncthreads();  acquire_agent();
+  __syncthreads();
 }
 
 // Coordinates / observation of training row `row`: rows landing in this launch
@@ -1991,10 +1975,8 @@ __device__ __forceinline__ void vstream_wg(const GPDesc& d, int64_t wgt, double*
           break;
         }
       }
-      acquire_poller();
     }
     __syncthreads();
-    acquire_agent();
     // plain loads: no line of the record is read in this launch before sync[2]
     // (an L2 miss for the first workgroup of an XCD, hits for the others)
     for (int e = tid; e < KINC * KINC + KINC; e += NT) {
@@ -2301,10 +2283,8 @@ __device__ __forceinline__ void vstream_wg_f32(const GPDesc& d, int64_t wgt, dou
           break;
         }
       }
-      acquire_poller();
     }
     __syncthreads();
-    acquire_agent();
     for (int e = tid; e < KINC * KINC + KINC; e += NT) {
       const double v = d.l22r[e];
       const bool use = e < KINC * KINC ? (e / KINC < k && e % KINC <= e / KINC) : (e - KINC * KINC < k);

@@ -154,9 +154,8 @@ __device__ void wait_l21_from(const GPDesc& d, int64_t lo) {
         break;
       }
     }
-    acquire_poller();
   }
-  __syncthreads();  acquire_agent();
+  __syncthreads();
 }
 
 // Spin (this wave) until *f == v; bounded like wait_flag.
@@ -169,8 +168,6 @@ __device__ __forceinline__ void spin_wave(const GPDesc& d, const unsigned* f, un
       break;
     }
   }
-  acquire_poller();   // (this wave is its own poller)
-  acquire_agent();
 }
 
 template <class VT>
@@ -634,9 +631,8 @@ __device__ void wait_flags_all(const GPDesc& d, const unsigned* f, int64_t n, un
         break;
       }
     }
-    acquire_poller();
   }
-  __syncthreads();  acquire_agent();
+  __syncthreads();
 }
 
 // Exclusive prefix over the workgroup of NV per-thread counts (in thread order),

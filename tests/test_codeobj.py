@@ -114,3 +114,29 @@ def test_lattice_gemm2_kernels_fit_one_workgroup_per_cu(report):
     for n, r in ks.items():
         assert r["calls"] == 0 and r["vgpr"] + r["agpr"] <= 128 and r["lds"] <= 160 * 1024, (n, r)
         assert r["scratch"] == 0 and r["vgpr_spill"] == 0, (n, r)
+
+
+@pytest.fixture(scope="module")
+def hand_offs(report):
+    import check_codeobj
+    return check_codeobj.hand_off_report(os.path.join(ROOT, "mfgp_coverage_amd", "libmfgp_hip.so"),
+                                         ("k_inc_stream", "k_inc_lat"))
+
+
+def test_hand_off_polls_read_device_scope_and_wait(hand_offs):
+    """the hand-offs inside one launch carry no acquire (its L2
+    invalidate costs 8 % at the headline); their order rests on the code
+    the compiler emits, which this checks in every consumer kernel: each poll of a
+    hand-off word (every spin iteration, found by its s_sleep) reads the word with a
+    device-scope (sc1) load, and an s_waitcnt vmcnt(0) completes that load before
+    the branch that leaves the spin -- so the flag's value is seen before anything
+    after the wait is issued (no speculation), and a stale L2 line never serves it.
+    The loads of the handed-off data are sc1 loads, or plain loads of lines no
+    workgroup of that XCD read earlier in the launch."""
+    assert len(hand_offs) == 22, sorted(hand_offs)   # 6 k_inc_stream*, 16 k_inc_lat*
+    for name, its in hand_offs.items():
+        # every consumer kernel waits (k_inc_stream*: L21 and L22; k_inc_lat*: more)
+        assert len(its) >= 10 if "k_inc_stream" in name else len(its) >= 14, (name, len(its))
+        for it in its:
+            assert it["loads"] and it["sc1"], (name, it)
+            assert it["waited"], (name, it)

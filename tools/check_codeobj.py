@@ -55,6 +55,70 @@ def calls(co):
     return out
 
 
+def disassembly(co):
+    """{kernel symbol: [(address, mnemonic, operands, branch target address or None)]}."""
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True, capture_output=True,
+                         text=True).stdout
+    out, cur, base = {}, None, 0
+    for line in dis.splitlines():
+        m = re.match(r"^([0-9a-f]+) <([^>]+)>:", line)
+        if m:
+            cur, base = out.setdefault(m.group(2), []), int(m.group(1), 16)
+            continue
+        m = re.match(r"^\s+([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-Fa-f]+):", line)
+        if cur is not None and m:
+            t = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", line)
+            cur.append((int(m.group(3), 16), m.group(1), m.group(2), base + int(t.group(1), 16) if t else None))
+    return out
+
+
+VMEM_LOAD = ("global_load", "buffer_load", "flat_load")
+
+
+def poll_iterations(ins):
+    """The hand-off waits' poll iterations of one kernel. Every bounded spin sleeps
+    (s_sleep) between polls, so each s_sleep starts one iteration: its flag loads,
+    up to the first conditional branch after them, the one that decides whether to
+    poll again (a branch before them is the spin bound's), following unconditional
+    branches. Returns one record per iteration: the iteration's vector loads;
+    whether all carry sc1 (device scope, L2-coherent across the XCDs: a flag is
+    never served from a stale line); and whether an s_waitcnt vmcnt(0) lies
+    between the last of them and the branch (the branch reads the flag's value, so
+    nothing after the exit is issued before the flag was seen)."""
+    at = {a: i for i, (a, _, _, _) in enumerate(ins)}
+    out = []
+    for i, (_, op, _, _) in enumerate(ins):
+        if op != "s_sleep":
+            continue
+        loads, pending, waited, j = [], False, False, i + 1
+        for _ in range(300):
+            if j >= len(ins):
+                break
+            _, op2, args, tgt = ins[j]
+            if op2.startswith(VMEM_LOAD):
+                loads.append((op2, args))
+                pending = True
+            elif op2 == "s_waitcnt" and "vmcnt(0)" in args:
+                pending = False
+            elif op2.startswith("s_cbranch") and loads:
+                waited = not pending
+                break
+            elif op2 == "s_branch" and tgt in at:
+                j = at[tgt]
+                continue
+            j += 1
+        out.append({"loads": loads, "sc1": bool(loads) and all(re.search(r"\bsc1\b", a) for _, a in loads),
+                    "waited": waited})
+    return out
+
+
+def hand_off_report(path, names):
+    """{kernel: poll iterations} for the kernels whose symbol contains one of `names`."""
+    with tempfile.TemporaryDirectory() as td:
+        dis = disassembly(code_object(path, td))
+    return {k: poll_iterations(v) for k, v in dis.items() if any(n in k for n in names)}
+
+
 def kernel_report(path):
     with tempfile.TemporaryDirectory() as td:
         co = code_object(path, td)
