@@ -8,7 +8,8 @@
 #   bench20           bench.py --steps 20 --warmup 5 (the driver's) -> gpurun_out/TAG_bench20.json
 #   quick             bench.py 200 steps, GP leg only             -> gpurun_out/TAG_quick.json
 #   configs4          bench.py --workload configs4                -> gpurun_out/TAG_configs4.json
-#   dropin            tools/bench_dropin.py                       -> gpurun_out/TAG_dropin.jsonl
+#   dropin            tools/bench_dropin.py, 4 env settings        -> gpurun_out/TAG_dropin.jsonl
+#   choi              tools/bench_planner.py --batch 8            -> gpurun_out/TAG_choi.json
 #   profile           tools/profile_round.sh TAG                  -> gpurun_out/prof_TAG
 #   trace=LIB         tools/trace_dump.py LIB                     -> gpurun_out/TAG_trace.npz
 #   py=SCRIPT         python -u SCRIPT                            -> gpurun_out/TAG_py.log
@@ -46,8 +47,14 @@ for step in "$@"; do
            grep '^{' ${O}_quick.log > ${O}_quick.json ;;
     configs4) run 600 ${O}_configs4.log python -u bench.py --workload configs4
            grep '^{' ${O}_configs4.log > ${O}_configs4.json ;;
-    dropin) run 200 ${O}_dropin.log python -u tools/bench_dropin.py
-           grep '^{' ${O}_dropin.log > ${O}_dropin.jsonl ;;
+    dropin) : > ${O}_dropin.jsonl   # default, then without the early return, then the V stream
+           for v in "MFGP_EARLY_PD=1" "MFGP_EARLY_PD=0" "MFGP_LATTICE=0" "MFGP_EARLY_PD=1"; do
+             run 200 ${O}_dropin.log env $v python -u tools/bench_dropin.py
+             grep '^{' ${O}_dropin.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); d['env']='$v'; print(json.dumps(d))" >> ${O}_dropin.jsonl
+           done
+           cat ${O}_dropin.jsonl ;;
+    choi) run 300 ${O}_choi.log python -u tools/bench_planner.py --batch 8
+           grep '^{' ${O}_choi.log > ${O}_choi.json; cat ${O}_choi.json ;;
     profile) run 1100 ${O}_prof.log bash tools/profile_round.sh "$TAG" ;;
     trace=*) run 200 ${O}_trace.log python -u tools/trace_dump.py "${step#trace=}" ${O}_trace.npz ;;
     py=*) run 300 ${O}_py.log python -u "${step#py=}" ;;
