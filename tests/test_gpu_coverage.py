@@ -128,11 +128,13 @@ def _ref(case, s):
     return tuple(SIM[f"{case}_s{s}_{k}"] for k in ("loss", "agent", "sample"))
 
 
-# per case: the least mean number of iterations a natural (unforced) run of the seeds
-# must be compared over before a rounding-decided choice may part it from the
-# reference's (the forced replays below compare all 14); RECORD keeps each seed's
-# count and the reason its comparison stopped
-FLOOR = {"a6_todescato_hmf": 5.6, "a6_todescato_hsf": 3.0, "a6_periodic_nmf": 5.6, "a6_todescato_nsf": 5.6}
+# per case: the mean number of iterations a natural (unforced) run of the seeds must
+# be compared over. compare_runs stops at a rounding-decided choice that parts a run
+# from the reference's; none did in round 5 (`pytest -s` prints RECORD: every seed of
+# every case, both drivers, compared over all of its logged iterations -- 14, and 12
+# for a6_todescato_nsf seed 3), so the floor is the whole run. RECORD keeps each
+# seed's count and the reason its comparison stopped.
+FLOOR = {"a6_todescato_hmf": 14, "a6_todescato_hsf": 14, "a6_periodic_nmf": 14, "a6_todescato_nsf": 12}
 RECORD = {}
 
 
