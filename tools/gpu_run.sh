@@ -36,7 +36,8 @@ for step in "$@"; do
   case "$step" in
     tests) run 1500 ${O}_tests.log python -u -m pytest -v --timeout 600 --timeout-method thread -m gpu tests/
            tail -3 ${O}_tests.log ;;
-    tests=*) run 1200 ${O}_tests.log python -u -m pytest -v --timeout 600 --timeout-method thread -m gpu tests/ -k "${step#tests=}"
+    tests=*) K="${step#tests=}"; K="${K//_or_/ or }"   # tests=a_or_b -> -k "a or b"
+           run 1200 ${O}_tests.log python -u -m pytest -v --timeout 600 --timeout-method thread -m gpu tests/ -k "$K"
            tail -3 ${O}_tests.log ;;
     smoke) run 300 ${O}_smoke.log python -c "import __graft_entry__ as g; g.smoke()"; tail -1 ${O}_smoke.log ;;
     bench) run 400 ${O}_bench.log python -u bench.py
