@@ -121,7 +121,7 @@ struct mfgp_ctx {
   bool lattice = true;        // lattice-separable appends (k_inc_lat) where they apply
   int lat_ksplit = 0;         // split-K of its GEMM tiles (0: chosen per launch; MFGP_LAT_KSPLIT, diagnostics)
   int lat_wu = 0;             // w units of a launch, all GPs (0: two per CU; MFGP_LAT_WU, diagnostics)
-  int lat_selfg = -1;         // w units read L21 from V themselves (-1: for batches of <= 8 GPs; MFGP_LAT_SELFG, diagnostics)
+  int lat_selfg = -1;         // w units read L21 from V themselves (-1: for one GP; MFGP_LAT_SELFG, diagnostics)
   int lat_gemm2 = -1;         // the step's GEMM and cells as a second launch (k_lat_gemm2): -1 where its
                               // tiles fill the chip once or twice, 1 always, 0 never (in-launch split-K
                               // tiles); MFGP_LAT_GEMM2, diagnostics and tests
@@ -2309,10 +2309,9 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
       if (c->lat_wu > 0) wu_total = c->lat_wu;
       // w units that gather L21 from V themselves start the F stream at once; each
       // row's gather is repeated in every block column it meets (~2x F's bytes in
-      // cache lines): a bandwidth-bound batch pays for that (configs[4], 32 GPs:
-      // 12.5k vs 19.8k GP-updates/s), a latency-bound one gains (one GP: 57.1 vs
-      // 60.3 us; the headline's 8 GPs since round 5: 100.4-100.8k vs 99.3-99.4k)
-      const int selfg = c->lat_selfg >= 0 ? c->lat_selfg : (ninc <= DESC_ARG_MAX ? 1 : 0);
+      // cache lines), which a batch's concurrent streams pay for (B = 8: 101.7 vs
+      // 99.5 us) and one GP does not (57.1 vs 60.3 us)
+      const int selfg = c->lat_selfg >= 0 ? c->lat_selfg : (ninc == 1 ? 1 : 0);
       for (int i = 0; i < ninc; ++i) {
         mfgp_model* m = order[i];
         GPDesc& fd = hd[i];
