@@ -32,15 +32,15 @@ def short(n):
     return n if len(n) < 60 else n[:57] + "..."
 
 
-def main(d, tag):
+def main(d, tag, pre="bench"):
     os.makedirs("profiles", exist_ok=True)
-    s = pd.read_csv(os.path.join(d, "trace", "bench_kernel_stats.csv"))
+    s = pd.read_csv(os.path.join(d, "trace", f"{pre}_kernel_stats.csv"))
     s["Name"] = s["Name"].map(short)
     s = s[["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"]]
     s.to_csv(f"profiles/{tag}_kernel_stats.csv", index=False)
     rows = []
     for kind, cname in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        p = os.path.join(d, kind, "bench_counter_collection.csv")
+        p = os.path.join(d, kind, f"{pre}_counter_collection.csv")
         if not os.path.exists(p):
             continue
         c = pd.read_csv(p)
@@ -56,12 +56,12 @@ def main(d, tag):
             t["write_bytes"] = t["WRITE_SIZE"] * 1024
         t.to_csv(f"profiles/{tag}_hbm_traffic.csv", index=False)
         print(t.to_string())
-    p = os.path.join(d, "mfma", "bench_counter_collection.csv")
+    p = os.path.join(d, "mfma", f"{pre}_counter_collection.csv")
     if os.path.exists(p):
         c = pd.read_csv(p)
         c["Name"] = c["Kernel_Name"].map(short)
         g = c.groupby(["Name", "Dispatch_Id", "Counter_Name"]).Counter_Value.sum().unstack().reset_index()
-        tr = pd.read_csv(os.path.join(d, "mfma", "bench_kernel_trace.csv"))
+        tr = pd.read_csv(os.path.join(d, "mfma", f"{pre}_kernel_trace.csv"))
         tr["dur_ns"] = tr.End_Timestamp - tr.Start_Timestamp
         g = g.merge(tr[["Dispatch_Id", "dur_ns"]], on="Dispatch_Id")
         g["grbm_per_xcd"] = g.GRBM_GUI_ACTIVE / 8
@@ -75,6 +75,10 @@ def main(d, tag):
         m["trace_dur_ns"] = m["Name"].map(trace_mean)
         m["sclk_ghz"] = sclk
         m["mfma_util"] = m.SQ_VALU_MFMA_BUSY_CYCLES / (m.trace_dur_ns.fillna(m.dur_ns) * sclk * 1024)
+        # over every dispatch of the kernel (sizes vary within a factor): summed busy
+        # cycles over summed durations of the same counter pass
+        tot = g.groupby("Name")[["SQ_VALU_MFMA_BUSY_CYCLES", "dur_ns"]].sum()
+        m["mfma_util_all_dispatches"] = m["Name"].map(tot.SQ_VALU_MFMA_BUSY_CYCLES / (tot.dur_ns * sclk * 1024))
         m.to_csv(f"profiles/{tag}_mfma_util.csv", index=False)
         print(m.to_string())
     with open(f"profiles/{tag}_build.json", "w") as f:
@@ -83,4 +87,4 @@ def main(d, tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))
