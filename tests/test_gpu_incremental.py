@@ -601,17 +601,22 @@ def test_speculative_append_not_pd_raises_at_append():
         m.append(X[20:21], y[20:21])       # speculative form (after a predict): raises here
 
 
-def test_early_verdict_append_then_other_calls():
+@pytest.mark.parametrize("lattice", [False, True])
+def test_early_verdict_append_then_other_calls(lattice):
     """The eager append of one GP returns at the step's L22 verdict (the launch
     publishes it before it computes the posterior): every later call -- factor
     download, clone, truncate, a second append, destroy, a predict -- first waits
-    for that launch, so each sees the appended state."""
+    for that launch, so each sees the appended state. Both one-GP launches: the V
+    stream (k_inc_stream1) and the lattice step (forced: k_inc_lat_arg)."""
     import gc
 
     from mfgp_coverage_amd import _lib
     Xs, X, y = _points(36, 420, seed=17, ongrid=True)
     NL, n = 150, 270
-    m, hyp = _model(_lib.context(), "mf", X[:n], y[:n], NL, Xs)
+    ctx = _lib.Context(0)
+    if lattice:
+        ctx.set_lattice("force")
+    m, hyp = _model(ctx, "mf", X[:n], y[:n], NL, Xs)
     m.predict()
     m.append(X[n:n + 8], y[n:n + 8])
     n += 8
@@ -640,6 +645,7 @@ def test_early_verdict_append_then_other_calls():
     mu, var = m.predict()
     mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs, hyp)
     assert _err(mu, var, mu_r, var_r, hyp) < TOL
+    assert (m.stats()["lattice"] > 0) == lattice, m.stats()
 
 
 def test_dropin_updt_hifi_not_pd_raises_and_stacks(gp_mod):
