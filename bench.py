@@ -151,25 +151,21 @@ def source_sha():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(kernel="k_predict", tag=None):
-    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
-    (profiles/<round>_hbm_traffic.csv, written by tools/summarize_profile.py from
-    separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x2 per the gfx950 correction of
-    MI355X_MICROARCH.md section HBM) collected on THIS build: its profiles/<round>_build.json
-    must hold the current source_sha(). Returns (bytes, source) or (None, reason)."""
+def _pmc_summaries(suffix, tag=None):
+    """The committed rocprofv3 summaries profiles/<round>[_<tag>]_<suffix>.csv collected
+    on THIS build (their profiles/<round>[_<tag>]_build.json holds the current
+    source_sha()), oldest first -> (files, None), or ([], reason)."""
     import glob
-    import csv
-    import re
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.csv")))
-    # profiles/<round>_hbm_traffic.csv: the headline; <round>_<tag>_hbm_traffic.csv: another workload
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{suffix}.csv")))
+    # profiles/<round>_<suffix>.csv: the headline; <round>_<tag>_<suffix>.csv: another workload
     files = [f for f in files if (f"_{tag}_" in os.path.basename(f)) == (tag is not None)
              and (tag is not None or "configs4" not in os.path.basename(f))]
     if not files:
-        return None, "no committed PMC summary"
+        return [], f"no committed {suffix} summary"
     sha = source_sha()
     same = []
     for f in files:
-        bj = f[: -len("_hbm_traffic.csv")] + "_build.json"
+        bj = f[: -len(f"_{suffix}.csv")] + "_build.json"
         try:
             with open(bj) as fh:
                 if json.load(fh).get("src_sha") == sha:
@@ -177,7 +173,22 @@ def pmc_traffic(kernel="k_predict", tag=None):
         except (OSError, ValueError):
             pass
     if not same:
-        return None, f"no PMC summary of this build (sources {sha}); newest: {os.path.relpath(files[-1], ROOT)}"
+        return [], f"no {suffix} summary of this build (sources {sha}); newest: {os.path.relpath(files[-1], ROOT)}"
+    return same, None
+
+
+def pmc_traffic(kernel="k_predict", tag=None):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
+    (profiles/<round>_hbm_traffic.csv, written by tools/summarize_profile.py from
+    separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x2 per the gfx950 correction of
+    MI355X_MICROARCH.md section HBM) collected on THIS build: its profiles/<round>_build.json
+    must hold the current source_sha(). Returns (bytes, source) or (None, reason)."""
+    import csv
+    import re
+    same, why = _pmc_summaries("hbm_traffic", tag)
+    if not same:
+        return None, why
+    sha = source_sha()
     # kernel: one name, or several (the launches of one step: their bytes add up)
     names = [kernel] if isinstance(kernel, str) else list(kernel)
     tot, found = 0.0, set()
@@ -192,23 +203,26 @@ def pmc_traffic(kernel="k_predict", tag=None):
     return tot, f"{os.path.relpath(same[-1], ROOT)} (sources {sha})"
 
 
-def pmc_mfma(kernel):
-    """MFMA utilisation of `kernel` from the newest committed rocprofv3 summary
-    (profiles/<round>_mfma_util.csv, tools/summarize_profile.py): the busy cycles over
-    the kernel's own duration at the measured shader clock."""
-    import glob
+def pmc_mfma(kernel, tag=None):
+    """MFMA utilisation of `kernel` from the newest committed rocprofv3 summary of THIS
+    build (profiles/<round>_mfma_util.csv, tools/summarize_profile.py, whose
+    <round>_build.json holds the current source_sha(), as for pmc_traffic): the busy
+    cycles over the kernel's own duration at the measured shader clock. Returns the
+    figure with its source, or {"mfma_util": None, "reason": ...}."""
     import csv
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_mfma_util.csv")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
+    import re
+    same, why = _pmc_summaries("mfma_util", tag)
+    if not same:
+        return {"mfma_util": None, "reason": why}
+    with open(same[-1]) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Name"]:
-                out = {"mfma_util": float(row["mfma_util"]), "source": os.path.relpath(files[-1], ROOT)}
+            if re.search(rf"::{kernel}(?![A-Za-z0-9_])", row["Name"]) or kernel == row["Name"]:
+                out = {"mfma_util": float(row["mfma_util"]),
+                       "source": f"{os.path.relpath(same[-1], ROOT)} (sources {source_sha()})"}
                 if row.get("sclk_ghz"):
                     out["sclk_ghz"] = float(row["sclk_ghz"])
                 return out
-    return None
+    return {"mfma_util": None, "reason": f"{os.path.relpath(same[-1], ROOT)} lacks {kernel}"}
 
 
 def cpu_baseline(wl, hyp, s, NL, NH0, k, reps=5):

@@ -114,6 +114,14 @@ int mfgp_ctx_set_timing_stride(mfgp_ctx* ctx, int64_t stride);
 int mfgp_ctx_get_timing(mfgp_ctx* ctx, double* predict_ms, int64_t* predict_launches,
                         double* factor_ms, int64_t* factor_calls);
 int mfgp_ctx_reset_timing(mfgp_ctx* ctx);
+/* Path counters of the planners' working copies (mfgp_sample_points,
+ * mfgp_batch_sample_points) since the last reset, added up as each copy is
+ * dropped: out[0..n) = {copies, bordered appends, one-pass predicts (V stream or
+ * lattice step), lattice steps, of them launched with their descriptors by
+ * value, of them with the GEMM and cells as a second launch, full refactors, full
+ * predicts}; n <= 8. reset != 0 zeroes them after the read. Which step form the
+ * Choi iterations took (tools/bench_planner.py). */
+int mfgp_ctx_planner_stats(mfgp_ctx* ctx, int64_t* out, int n, int reset);
 
 /* SFGP.__init__ (gp:28-64) / MFGP.__init__ (gp:276-327) with the caller's
  * hyperparameters (the simulator overwrites .hyp right after construction,
@@ -169,6 +177,12 @@ int mfgp_predict_view_running(mfgp_model* m, double** mu, double** var, void** v
 /* Return a buffer handed over by mfgp_predict_view (any thread, any time, also
  * after its model or context is destroyed). */
 int mfgp_release_view(void* view);
+/* The fused np.amax / np.argmax of a handed-over buffer's variance (the eager
+ * append's launch reduces them beside its status word): *valid = 1 and the max
+ * and its first cell when the launch that wrote the buffer computed them, else
+ * *valid = 0 (a predict without an append before it). Read after the buffer is
+ * ready (mfgp_predict_view_running: after mfgp_ctx_synchronize). */
+int mfgp_view_max(const void* view, double* vmax, int64_t* argmax, int* valid);
 
 /* Sizes and state readers (the Python mirror's .X/.L attributes). */
 int64_t mfgp_model_n(const mfgp_model* m);      /* N = NL + NH */
@@ -182,8 +196,9 @@ int64_t mfgp_model_m(const mfgp_model* m);
  * the context's stream; only when n > 9), lattice steps launched with their
  * descriptors as the kernel argument, lattice steps whose GEMM and cells ran as a
  * second launch (k_lat_gemm2 or k_lat_gemm3), batch predicts served from the
- * resident posterior because the model appended nothing (k_post_copy), lattice
- * steps whose second launch built its own Z rows (k_lat_gemm3)}; n <= 14. */
+ * resident posterior because the model appended nothing (k_post_copy), eager
+ * appends of one GP that returned at the launch's published L22 verdict
+ * (mfgp_append above)}; n <= 14. */
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n);
 /* Copy the lower Cholesky factor L [N,N] (row-major, zeros above the diagonal). */
 int mfgp_get_factor(mfgp_model* m, double* L_out);

@@ -55,6 +55,7 @@ SIGNATURES = {
     "mfgp_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mfgp_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int64_p, _c_double_p, _c_int64_p]),
     "mfgp_ctx_reset_timing": (ctypes.c_int, [ctypes.c_void_p]),
+    "mfgp_ctx_planner_stats": (ctypes.c_int, [ctypes.c_void_p, _c_int64_p, ctypes.c_int, ctypes.c_int]),
     "mfgp_model_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                          ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
     "mfgp_model_destroy": (None, [ctypes.c_void_p]),
@@ -71,6 +72,7 @@ SIGNATURES = {
                                                  ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                                  ctypes.POINTER(ctypes.c_int)]),
     "mfgp_release_view": (ctypes.c_int, [ctypes.c_void_p]),
+    "mfgp_view_max": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int64_p, ctypes.POINTER(ctypes.c_int)]),
     "mfgp_model_n": (ctypes.c_int64, [ctypes.c_void_p]),
     "mfgp_model_nl": (ctypes.c_int64, [ctypes.c_void_p]),
     "mfgp_model_m": (ctypes.c_int64, [ctypes.c_void_p]),
@@ -211,6 +213,18 @@ class Context:
         return {"predict_ms": pm.value, "predict_launches": pn.value,
                 "factor_ms": fm.value, "factor_calls": fn.value}
 
+    PLANNER_KEYS = ("copies", "inc_factor", "vstream", "lattice", "lattice_arg", "lattice_g2", "full_factor",
+                    "full_predict")
+
+    def planner_stats(self, reset=False):
+        """Path counters of the planners' working copies (mfgp_sample_points /
+        mfgp_batch_sample_points) since the last reset: how many copies, and which step
+        form their iterations took (vstream counts every one-pass predict, lattice steps
+        included)."""
+        out = (ctypes.c_int64 * len(self.PLANNER_KEYS))()
+        check(lib().mfgp_ctx_planner_stats(self.handle, out, len(self.PLANNER_KEYS), 1 if reset else 0))
+        return dict(zip(self.PLANNER_KEYS, (int(v) for v in out)))
+
 
 _tls = threading.local()
 _default_device = int(os.environ.get("MFGP_DEVICE", "0"))
@@ -319,24 +333,31 @@ class Model:
         check(lib().mfgp_predict(self.handle, ptr(mu) if M else None, ptr(var) if M else None))
         return mu, var
 
-    def predict_view(self):
+    def predict_view(self, with_max=False):
         """predict() without the host copy: (mu, var) are writable arrays over the
         model's pinned result buffer, handed over to them (mfgp_predict_view); the
-        buffer goes back to the library's pool when both arrays are gone."""
+        buffer goes back to the library's pool when both arrays are gone. with_max:
+        (mu, var, fused) where fused is (max var, its first cell) as the launch that
+        wrote the buffer reduced them (mfgp_view_max), or None."""
         mu_p, var_p, view, running = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int(0)
         L = lib()
         check(L.mfgp_predict_view_running(self.handle, ctypes.byref(mu_p), ctypes.byref(var_p), ctypes.byref(view),
                                           ctypes.byref(running)))
         M = L.mfgp_model_m(self.handle)
         if not view.value:
-            return np.empty(M, dtype=np.float64), np.empty(M, dtype=np.float64)
+            e = np.empty(M, dtype=np.float64), np.empty(M, dtype=np.float64)
+            return (*e, None) if with_max else e
         lease = _ViewLease(view.value)
         mu, var = np.asarray(_HostView(mu_p.value, M, lease)), np.asarray(_HostView(var_p.value, M, lease))
         if running.value:
             # the eager append's launch was still computing into the buffer: the arrays
             # were wrapped meanwhile and are given out once it has ended
             check(L.mfgp_ctx_synchronize(self.ctx.handle))
-        return mu, var
+        if not with_max:
+            return mu, var
+        vm, am, ok = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int(0)
+        check(L.mfgp_view_max(ctypes.c_void_p(view.value), ctypes.byref(vm), ctypes.byref(am), ctypes.byref(ok)))
+        return mu, var, ((np.float64(vm.value), int(am.value)) if ok.value else None)
 
     def factor(self):
         n = lib().mfgp_model_n(self.handle)
@@ -359,12 +380,13 @@ class Model:
         the lattice steps launched with their descriptors by value (k_inc_lat_arg);
         {lattice_g2}: the lattice steps whose GEMM and cells ran as a second launch
         (k_lat_gemm2); {post_copy}: batch predicts served from the resident posterior
-        because the model appended nothing (k_post_copy)."""
-        out = (ctypes.c_int64 * 13)()
-        check(lib().mfgp_model_stats(self.handle, out, 13))
+        because the model appended nothing (k_post_copy); {early_pd}: eager appends that
+        returned at the launch's published L22 verdict (mfgp_append, one GP)."""
+        out = (ctypes.c_int64 * 14)()
+        check(lib().mfgp_model_stats(self.handle, out, 14))
         keys = ("factor_rows", "v_rows", "full_factor", "inc_factor", "full_predict", "vstream",
                 "lattice_nx", "lattice_ny", "lattice", "lattice_virtual", "lattice_arg", "lattice_g2",
-                "post_copy")
+                "post_copy", "early_pd")
         return dict(zip(keys, (int(v) for v in out)))
 
     def sample_points(self, threshold, max_points):

@@ -72,6 +72,10 @@ constexpr size_t F32_SCRATCH = size_t(16) << 30;   // bytes of fp64 V scratch fo
 // and for at most LAT_MAXD consecutive steps before var / mu are recomputed from V
 constexpr double LAT_RMAX = 1e4;
 constexpr int LAT_MAXD = 256;
+// planner working-copy counters (mfgp_ctx_planner_stats): copies, bordered appends,
+// V-stream predicts, lattice steps (of them by value / with k_lat_gemm2), full
+// factors, full predicts
+constexpr int PLAN_NSTATS = 8;
 
 struct EvPair {
   hipEvent_t a, b;
@@ -152,6 +156,10 @@ struct mfgp_ctx {
   size_t h_status_n = 0;
 
   int ncu = 256;              // compute units (hipDeviceProp multiProcessorCount)
+  // the path counters of the planners' working copies (mfgp_sample_points,
+  // mfgp_batch_sample_points), added up when each copy is dropped: which step
+  // form the Choi iterations took (mfgp_ctx_planner_stats)
+  int64_t plan_stats[PLAN_NSTATS] = {0};
 };
 
 struct mfgp_model {
@@ -204,12 +212,17 @@ struct mfgp_model {
   double* spec_out_dev = nullptr;
   int64_t spec_cap = 0;
   bool spec_valid = false;
+  // spec_out's trailer [2 cap] = (max var, its first argmax) holds the fused var
+  // max / argmax of the launch that wrote spec_out (the eager append's): the
+  // drop-in's np.amax / np.argmax of the covariance read it instead of rescanning
+  bool spec_max = false;
   bool pred_since_append = false;   // a predict came after the last append
   // path counters (mfgp_model_stats)
   int64_t n_full_factor = 0, n_inc_factor = 0, n_full_predict = 0, n_vstream = 0, n_lattice = 0;
   int64_t n_lattice_arg = 0;   // lattice steps launched with their descriptors by value (k_inc_lat_arg)
   int64_t n_lattice_g2 = 0;    // lattice steps whose GEMM and cells ran as a second launch (k_lat_gemm2)
   int64_t n_post_copy = 0;     // batch predicts served from the resident posterior (k_post_copy: nothing appended)
+  int64_t n_early_pd = 0;      // eager appends that returned at the launch's published L22 verdict
   unsigned* csr = nullptr;     // the scan units' member lists (csr_bytes; mfgp_internal.h)
   int64_t csr_n = 0;           // (bytes)
   // state generation: a new factor from scratch, a new grid or new hyperparameters
@@ -1005,7 +1018,8 @@ bool is_device_ptr(const void* p);
 // returned buffer is freed.
 struct ViewBuf {
   double* host;
-  int64_t cap;   // doubles per half ([2][cap])
+  int64_t cap;   // doubles per half ([2][cap]), then the trailer (max var, argmax) at [2 cap]
+  int has_max;   // the trailer holds the fused max / argmax of the var half
 };
 std::mutex g_view_mu;
 std::vector<ViewBuf> g_view_pool;
@@ -1022,6 +1036,7 @@ int ensure_spec_out(mfgp_model* m) {
   m->spec_out_dev = nullptr;
   m->spec_cap = 0;
   m->spec_valid = false;
+  m->spec_max = false;
   {
     // best fit: the smallest pooled buffer that holds M (a small model does not take
     // the large buffer another model just returned)
@@ -1044,7 +1059,8 @@ int ensure_spec_out(mfgp_model* m) {
     return MFGP_OK;
   }
   // portable: a pooled buffer may serve a model of a context on another device
-  HIP_TRY(hipHostMalloc(&m->spec_out, sizeof(double) * 2 * (size_t)m->M, hipHostMallocMapped | hipHostMallocPortable));
+  HIP_TRY(hipHostMalloc(&m->spec_out, sizeof(double) * (2 * (size_t)m->M + 2),
+                        hipHostMallocMapped | hipHostMallocPortable));
   void* dev = nullptr;
   HIP_TRY(hipHostGetDevicePointer(&dev, m->spec_out, 0));
   m->spec_out_dev = static_cast<double*>(dev);
@@ -1063,6 +1079,7 @@ int model_out(mfgp_model* m, double* mu, double* var, double*& kmu, double*& kva
   }
   int rc = ensure_spec_out(m);
   if (rc) return rc;
+  m->spec_max = false;   // (this predict computes no fused max into the trailer)
   kmu = m->spec_out_dev;
   kvar = m->spec_out_dev + m->spec_cap;
   return MFGP_OK;
@@ -1492,6 +1509,7 @@ int mfgp_ctx_synchronize(mfgp_ctx* c) {
 
 int mfgp_ctx_set_incremental(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->incremental = enable != 0;
   return MFGP_OK;
@@ -1499,6 +1517,7 @@ int mfgp_ctx_set_incremental(mfgp_ctx* c, int enable) {
 
 int mfgp_ctx_set_fused(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->fused = enable != 0;
   return MFGP_OK;
@@ -1506,6 +1525,7 @@ int mfgp_ctx_set_fused(mfgp_ctx* c, int enable) {
 
 int mfgp_ctx_set_deferred_appends(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->deferred = enable != 0;
   return MFGP_OK;
@@ -1513,6 +1533,7 @@ int mfgp_ctx_set_deferred_appends(mfgp_ctx* c, int enable) {
 
 int mfgp_ctx_set_lattice(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->lattice = enable != 0;
   c->lat_force = enable == 2;
@@ -1521,6 +1542,7 @@ int mfgp_ctx_set_lattice(mfgp_ctx* c, int enable) {
 
 int mfgp_ctx_set_concurrent(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->concurrent = enable != 0;
   return MFGP_OK;
@@ -1528,12 +1550,14 @@ int mfgp_ctx_set_concurrent(mfgp_ctx* c, int enable) {
 
 int mfgp_ctx_enable_timing(mfgp_ctx* c, int enable) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   c->timing = (enable == 2) ? 2 : (enable != 0 ? 1 : 0);
   return MFGP_OK;
 }
 
 int mfgp_ctx_set_timing_stride(mfgp_ctx* c, int64_t stride) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   if (stride < 1) return set_err(MFGP_ERR_ARG, "timing stride must be >= 1");
   c->timing_stride = stride;
   c->timing_seq = 0;
@@ -1542,6 +1566,7 @@ int mfgp_ctx_set_timing_stride(mfgp_ctx* c, int64_t stride) {
 
 int mfgp_ctx_get_timing(mfgp_ctx* c, double* pm, int64_t* pn, double* fm, int64_t* fn) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   int rc = drain_timing(c);
   if (rc) return rc;
   if (pm) *pm = c->t_predict;
@@ -1553,6 +1578,7 @@ int mfgp_ctx_get_timing(mfgp_ctx* c, double* pm, int64_t* pn, double* fm, int64_
 
 int mfgp_ctx_reset_timing(mfgp_ctx* c) {
   if (!c) return set_err(MFGP_ERR_ARG, "null ctx");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
   int rc = drain_timing(c);
   c->t_predict = c->t_factor = 0.0;
   c->n_predict = c->n_factor = 0;
@@ -1619,6 +1645,28 @@ void mfgp_model_destroy(mfgp_model* m) {
   if (m->sync) (void)hipFree(m->sync);
   free_lat(m);
   delete m;
+}
+
+// add a planner working copy's path counters to its context's (mfgp_ctx_planner_stats)
+static void plan_account(const mfgp_model* t) {
+  int64_t* p = t->ctx->plan_stats;
+  p[0] += 1;
+  p[1] += t->n_inc_factor;
+  p[2] += t->n_vstream;
+  p[3] += t->n_lattice;
+  p[4] += t->n_lattice_arg;
+  p[5] += t->n_lattice_g2;
+  p[6] += t->n_full_factor;
+  p[7] += t->n_full_predict;
+}
+
+int mfgp_ctx_planner_stats(mfgp_ctx* c, int64_t* out, int n, int reset) {
+  if (!c || (n > 0 && !out)) return set_err(MFGP_ERR_ARG, "null ctx/out");
+  if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
+  for (int i = 0; i < n && i < PLAN_NSTATS; ++i) out[i] = c->plan_stats[i];
+  if (reset)
+    for (int64_t& v : c->plan_stats) v = 0;
+  return MFGP_OK;
 }
 
 int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
@@ -1849,7 +1897,13 @@ int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t
   if (rc == MFGP_OK) rc = ensure_spec_out(m);
   if (rc) return rc;
   if (m->status_host) reinterpret_cast<volatile int*>(m->status_host)[1] = STATUS_UNSET;
-  rc = batch_run(&m, 1, X, y, &k, m->spec_out_dev, m->spec_out_dev + m->spec_cap, nullptr, nullptr, MFGP_ASYNC, true, true);
+  // (the fused var max / argmax into the buffer's trailer: the launch's last cell
+  // group reduces the groups' partials for the status word anyway)
+  double* tr = m->spec_out_dev + 2 * m->spec_cap;
+  m->spec_max = false;
+  rc = batch_run(&m, 1, X, y, &k, m->spec_out_dev, m->spec_out_dev + m->spec_cap, tr,
+                 reinterpret_cast<int64_t*>(tr + 1), MFGP_ASYNC, true, true);
+  if (rc == MFGP_OK) m->spec_max = true;
   if (rc == MFGP_OK && c->early_pd && c->spin_us > 0 && m->status_host && c->async_status.size() == 1 &&
       c->async_status[0].host == m->status_host) {
     // the launch publishes the L22 verdict of the step (the only status its
@@ -1865,6 +1919,7 @@ int spec_append_predict(mfgp_model* m, const double* X, const double* y, int64_t
     if (*w == INT_MAX) {
       c->early_running = true;
       m->spec_valid = true;
+      m->n_early_pd += 1;
       return MFGP_OK;
     }
   }
@@ -1898,7 +1953,7 @@ static int predict_view(mfgp_model* m, double** mu, double** var, void** view, i
     // the predict's host outputs are the result buffer itself: no copy
     if ((rc = mfgp_predict(m, m->spec_out, m->spec_out + m->spec_cap))) return rc;
   }
-  ViewBuf* v = new ViewBuf{m->spec_out, m->spec_cap};
+  ViewBuf* v = new ViewBuf{m->spec_out, m->spec_cap, m->spec_max ? 1 : 0};
   *mu = m->spec_out;
   *var = m->spec_out + m->spec_cap;
   *view = v;
@@ -1907,6 +1962,18 @@ static int predict_view(mfgp_model* m, double** mu, double** var, void** view, i
   m->spec_out_dev = nullptr;
   m->spec_cap = 0;
   m->spec_valid = false;
+  m->spec_max = false;
+  return MFGP_OK;
+}
+
+int mfgp_view_max(const void* view, double* vmax, int64_t* argmax, int* valid) {
+  if (!view || !vmax || !argmax || !valid) return set_err(MFGP_ERR_ARG, "null view/output");
+  const ViewBuf* v = static_cast<const ViewBuf*>(view);
+  *valid = v->has_max;
+  if (v->has_max) {
+    *vmax = v->host[2 * v->cap];
+    std::memcpy(argmax, v->host + 2 * v->cap + 1, sizeof(int64_t));
+  }
   return MFGP_OK;
 }
 
@@ -2000,6 +2067,7 @@ int64_t mfgp_model_n(const mfgp_model* m) { return m ? m->NL + m->NH : -1; }
 
 int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
   if (!m || !out) return set_err(MFGP_ERR_ARG, "null model/out");
+  if (const int rc_ = settle(m->ctx)) return rc_;
   // off-lattice training rows the last lattice step's Z units found (lidx = -1,
   // the step's "virtual" K rows): the counts they published, read back from the
   // device (both parts; an MF hifi row off the lattice counts in each)
@@ -2011,10 +2079,10 @@ int mfgp_model_stats(const mfgp_model* m, int64_t* out, int n) {
     if (m->kind == MFGP_MF) HIP_TRY(hipMemcpy(&nv[1], m->zvl + m->zb_rows + 1, sizeof(int), hipMemcpyDeviceToHost));
     virt = (int64_t)nv[0] + nv[1];
   }
-  const int64_t v[13] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
+  const int64_t v[14] = {m->factored ? m->factor_N : -1, m->v_n, m->n_full_factor, m->n_inc_factor,
                          m->n_full_predict, m->n_vstream, m->lat.nx, m->lat.ny, m->n_lattice, virt,
-                         m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy};
-  for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
+                         m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy, m->n_early_pd};
+  for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
   return MFGP_OK;
 }
 int64_t mfgp_model_nl(const mfgp_model* m) { return m ? m->NL : -1; }
@@ -2567,6 +2635,7 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
   if (done > 0 && hipMemcpy(points, pts, sizeof(double) * 2 * done, hipMemcpyDefault) != hipSuccess)
     return fail(set_err(MFGP_ERR_DEVICE, "sample_points: copy out failed"));
   *count = done;
+  plan_account(t);
   mfgp_model_destroy(t);
   return MFGP_OK;
 }
@@ -2620,26 +2689,32 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
     Mtot += t[b]->M;
   }
   const int64_t P = std::max<int64_t>(max_points, 1);
-  const size_t nd = 2 * (size_t)Mtot + 10 * (size_t)count + 2 * (size_t)count * (size_t)P + 8;
+  // one 8-byte slot per entry (pos's ints take a slot each); the offsets below are
+  // the only description of the layout, and the allocation is their end
+  const size_t B_ = (size_t)count;
+  const size_t o_mu = 0, o_var = o_mu + (size_t)Mtot, o_vmax = o_var + (size_t)Mtot, o_varg = o_vmax + B_;
+  const size_t o_state = o_varg + B_, o_thr = o_state + 2 * B_, o_moff = o_thr + B_, o_Ms = o_moff + B_;
+  const size_t o_grids = o_Ms + B_, o_xn = o_grids + B_, o_yn = o_xn + 2 * B_, o_pos = o_yn + B_;
+  const size_t o_pts = o_pos + B_, nd = o_pts + 2 * B_ * (size_t)P;
   double* ws = nullptr;
   if (hipMalloc(&ws, sizeof(double) * nd) != hipSuccess) return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: out of memory"));
   auto fail2 = [&](int code) {
     (void)hipFree(ws);
     return fail(code);
   };
-  double* mu = ws;
-  double* var = mu + Mtot;
-  double* vmax = var + Mtot;
-  int64_t* vargmax = reinterpret_cast<int64_t*>(vmax + count);
-  int64_t* state = vargmax + count;
-  double* thr = reinterpret_cast<double*>(state + 2 * count);
-  int64_t* moff_d = reinterpret_cast<int64_t*>(thr + count);
-  int64_t* Ms_d = moff_d + count;
-  const double** grids_d = reinterpret_cast<const double**>(Ms_d + count);
-  double* xn = reinterpret_cast<double*>(grids_d + count);
-  double* yn = xn + 2 * count;
-  int* pos_d = reinterpret_cast<int*>(yn + count);
-  double* pts = yn + 2 * count;
+  double* mu = ws + o_mu;
+  double* var = ws + o_var;
+  double* vmax = ws + o_vmax;
+  int64_t* vargmax = reinterpret_cast<int64_t*>(ws + o_varg);
+  int64_t* state = reinterpret_cast<int64_t*>(ws + o_state);
+  double* thr = ws + o_thr;
+  int64_t* moff_d = reinterpret_cast<int64_t*>(ws + o_moff);
+  int64_t* Ms_d = reinterpret_cast<int64_t*>(ws + o_Ms);
+  const double** grids_d = reinterpret_cast<const double**>(ws + o_grids);
+  double* xn = ws + o_xn;
+  double* yn = ws + o_yn;
+  int* pos_d = reinterpret_cast<int*>(ws + o_pos);
+  double* pts = ws + o_pts;
   std::vector<int64_t> st(2 * count);
   std::vector<const double*> grids(count);
   for (int b = 0; b < count; ++b) {
@@ -2711,6 +2786,7 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
   (void)hipFree(ws);
   for (auto m : t) {
     m->gate_dev = nullptr;
+    plan_account(m);
     mfgp_model_destroy(m);
   }
   return MFGP_OK;

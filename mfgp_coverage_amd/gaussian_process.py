@@ -34,12 +34,19 @@ from . import _lib
 
 
 class DiagCov:
-    """Diagonal-only stand-in for the dense [M,M] posterior covariance of gp:146 / gp:435-436."""
+    """Diagonal-only stand-in for the dense [M,M] posterior covariance of gp:146 / gp:435-436.
 
-    __slots__ = ("var",)
+    fused: (max, first argmax) of ``var`` as the launch that computed it reduced them
+    (the eager append's epilogue, mfgp_view_max), or None: then ``np.amax`` /
+    ``np.argmax`` return it instead of rescanning the M-vector on the host. The
+    maximum of a vector is exact, so the value is the host scan's bit for bit
+    (tests/test_boundary.py)."""
 
-    def __init__(self, var):
+    __slots__ = ("var", "fused")
+
+    def __init__(self, var, fused=None):
         self.var = np.asarray(var, dtype=np.float64).reshape(-1)
+        self.fused = fused
 
     @property
     def shape(self):
@@ -75,12 +82,18 @@ class DiagCov:
         if func in (np.diag, np.diagonal):
             k = kwargs.get("k", kwargs.get("offset", args[1] if len(args) > 1 else 0))
             if k == 0:
-                return self.var.copy()
+                # what np.diag / np.diagonal of a 2-D array give: a read-only view of
+                # the diagonal (no copy; the view keeps the result buffer alive)
+                d = self.var.view()
+                d.flags.writeable = False
+                return d
+        if (func in (np.amax, np.max) and len(args) == 1 and not kwargs):
+            return self.fused[0] if self.fused is not None else self.var.max()
         if func in (np.amax, np.max) and kwargs.get("axis", args[1] if len(args) > 1 else None) is None:
             return self.var.max()
         if func is np.argmax and kwargs.get("axis", args[1] if len(args) > 1 else None) is None:
             # flat index of the maximum of the dense matrix (first diagonal maximum)
-            i = int(np.argmax(self.var))
+            i = self.fused[1] if (self.fused is not None and len(args) == 1 and not kwargs) else int(np.argmax(self.var))
             return i * self.var.shape[0] + i
         if func is np.trace:
             return self.var.sum()
@@ -161,9 +174,10 @@ class _DeviceGP:
         self._sync_data()
         self._push_hyp()
         self._grid_to_device(X_star)
-        # (the arrays are the model's pinned result buffer, handed over: no copy)
-        mu, var = self._dev().predict_view()
-        return mu.reshape(-1, 1), DiagCov(var)
+        # (the arrays are the model's pinned result buffer, handed over: no copy;
+        # with the max / argmax of var its launch reduced, when it did)
+        mu, var, fused = self._dev().predict_view(with_max=True)
+        return mu.reshape(-1, 1), DiagCov(var, fused)
 
     @property
     def L(self):

@@ -119,6 +119,10 @@ def test_diagcov_semantics():
     assert c.shape == (3, 3) and c[1, 1] == 0.5
     with pytest.raises(TypeError):
         np.asarray(c)
+    d = np.diag(c)                                              # as np.diag of a 2-D array: a
+    assert not d.flags.writeable and np.shares_memory(d, c.var)  # read-only view, no copy
+    f = DiagCov(v, fused=(np.float64(0.5), 1))                  # the launch's fused max / argmax
+    assert np.amax(f) == 0.5 and np.argmax(f) == 4 and np.max(f, axis=None) == 0.5
     one = DiagCov(np.array([0.25]))                             # get_neg_var's 1x1 (gp:556-557)
     assert float(2.0 * one[0, 0]) == 0.5
     np.testing.assert_array_equal(np.asarray(one), [[0.25]])
@@ -158,3 +162,14 @@ def test_predict_arrays_are_the_callers(lib):
         gc.collect()
     np.testing.assert_array_equal(mu0, keep_mu.reshape(-1, 1))   # untouched by later steps
     np.testing.assert_array_equal(np.diag(cov0), keep_var)
+    # the drop-in step's consumers (sim:301, 672 / 842 / 1014): after an append the
+    # covariance carries its launch's fused max / argmax, equal to the host scan's
+    for s in range(3):
+        m.updt_hifi(X[190 + 2 * s:192 + 2 * s], y[190 + 2 * s:192 + 2 * s])
+        mu, cov = m.predict(xs)
+        v = np.diag(cov)
+        assert cov.fused is not None
+        assert np.amax(cov) == v.max() and np.argmax(cov) == int(np.argmax(v)) * (xs.shape[0] + 1)
+        assert not v.flags.writeable and np.shares_memory(v, cov.var)
+    mu, cov = m.predict(xs)            # the same model again (no append: a host max)
+    assert np.amax(cov) == np.diag(cov).max()

@@ -646,6 +646,9 @@ def test_early_verdict_append_then_other_calls(lattice):
     mu_r, var_r = _ref("mf", X[:n], y[:n], NL, Xs, hyp)
     assert _err(mu, var, mu_r, var_r, hyp) < TOL
     assert (m.stats()["lattice"] > 0) == lattice, m.stats()
+    # the appends above did return at the published verdict (without it
+    # every call here would still pass, each after a full synchronise)
+    assert m.stats()["early_pd"] >= 3, m.stats()
 
 
 def test_dropin_updt_hifi_not_pd_raises_and_stacks(gp_mod):

@@ -75,18 +75,24 @@ def batch(a):
     xs = wl.xs
     compute_sample_points_batch(ms, xs, [0.99 * t / a.frac for t in thr])   # warm-up
     compute_sample_points(ms[0], xs, 0.99 * thr[0] / a.frac, False)
+    from mfgp_coverage_amd import _lib
+    ctx = _lib.context()
+    ctx.planner_stats(reset=True)
     t0 = time.perf_counter()
     pb = compute_sample_points_batch(ms, xs, thr)
     tb = time.perf_counter() - t0
+    st_b = ctx.planner_stats(reset=True)   # which step form the batched iterations took
     t0 = time.perf_counter()
     ps = [compute_sample_points(m, xs, t, False) for m, t in zip(ms, thr)]
     t1 = time.perf_counter() - t0
+    st_s = ctx.planner_stats(reset=True)
     same = [int(np.array_equal(x, y)) for x, y in zip(pb, ps)]
     its = max(p.shape[0] for p in pb)
     out = {"batch": a.batch, "points": [int(p.shape[0]) for p in pb], "batched_s": tb, "one_at_a_time_s": t1,
            "speedup": t1 / tb, "batched_ms_per_iteration": 1e3 * tb / max(1, its),
            "seed_iterations_per_s": sum(p.shape[0] for p in pb) / tb, "equal_to_single": same,
-           "grid": a.grid, "N_start": a.nl + a.nh, "threshold_frac": a.frac}
+           "grid": a.grid, "N_start": a.nl + a.nh, "threshold_frac": a.frac,
+           "batched_paths": st_b, "single_paths": st_s}
     print(json.dumps(out), flush=True)
 
 
