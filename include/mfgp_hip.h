@@ -114,9 +114,9 @@ int mfgp_ctx_set_timing_stride(mfgp_ctx* ctx, int64_t stride);
 int mfgp_ctx_get_timing(mfgp_ctx* ctx, double* predict_ms, int64_t* predict_launches,
                         double* factor_ms, int64_t* factor_calls);
 int mfgp_ctx_reset_timing(mfgp_ctx* ctx);
-/* Path counters of the planners' working copies (mfgp_sample_points,
- * mfgp_batch_sample_points) since the last reset, added up as each copy is
- * dropped: out[0..n) = {copies, bordered appends, one-pass predicts (V stream or
+/* Path counters of the planners' loops (mfgp_sample_points,
+ * mfgp_batch_sample_points: each model's appended rows, dropped at the end) since
+ * the last reset: out[0..n) = {model runs, bordered appends, one-pass predicts (V stream or
  * lattice step), lattice steps, of them launched with their descriptors by
  * value, of them with the GEMM and cells as a second launch, full refactors, full
  * predicts}; n <= 8. reset != 0 zeroes them after the read. Which step form the

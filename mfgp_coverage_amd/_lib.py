@@ -213,12 +213,12 @@ class Context:
         return {"predict_ms": pm.value, "predict_launches": pn.value,
                 "factor_ms": fm.value, "factor_calls": fn.value}
 
-    PLANNER_KEYS = ("copies", "inc_factor", "vstream", "lattice", "lattice_arg", "lattice_g2", "full_factor",
+    PLANNER_KEYS = ("runs", "inc_factor", "vstream", "lattice", "lattice_arg", "lattice_g2", "full_factor",
                     "full_predict")
 
     def planner_stats(self, reset=False):
-        """Path counters of the planners' working copies (mfgp_sample_points /
-        mfgp_batch_sample_points) since the last reset: how many copies, and which step
+        """Path counters of the planners' loops (mfgp_sample_points /
+        mfgp_batch_sample_points) since the last reset: how many model runs, and which step
         form their iterations took (vstream counts every one-pass predict, lattice steps
         included)."""
         out = (ctypes.c_int64 * len(self.PLANNER_KEYS))()

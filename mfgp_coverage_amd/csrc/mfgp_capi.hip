@@ -156,15 +156,15 @@ struct mfgp_ctx {
   size_t h_status_n = 0;
 
   int ncu = 256;              // compute units (hipDeviceProp multiProcessorCount)
-  // the path counters of the planners' working copies (mfgp_sample_points,
-  // mfgp_batch_sample_points), added up when each copy is dropped: which step
-  // form the Choi iterations took (mfgp_ctx_planner_stats)
+  // the path counters of the planners' loops (mfgp_sample_points,
+  // mfgp_batch_sample_points), moved here from the models when each loop ends:
+  // which step form the Choi iterations took (mfgp_ctx_planner_stats)
   int64_t plan_stats[PLAN_NSTATS] = {0};
 };
 
 struct mfgp_model {
   mfgp_ctx* ctx = nullptr;
-  int* gate_dev = nullptr;  // device gate of every step of this model (mfgp_batch_sample_points' clones: 0 = skip)
+  int* gate_dev = nullptr;  // device gate of every step of this model (the planners' loops: 0 = skip)
   int kind = MFGP_SF;
   int dtype = MFGP_F64;     // precision of the resident V (MFGP_F32: fp32 storage and stream)
   int nhyp = 4;
@@ -1647,19 +1647,6 @@ void mfgp_model_destroy(mfgp_model* m) {
   delete m;
 }
 
-// add a planner working copy's path counters to its context's (mfgp_ctx_planner_stats)
-static void plan_account(const mfgp_model* t) {
-  int64_t* p = t->ctx->plan_stats;
-  p[0] += 1;
-  p[1] += t->n_inc_factor;
-  p[2] += t->n_vstream;
-  p[3] += t->n_lattice;
-  p[4] += t->n_lattice_arg;
-  p[5] += t->n_lattice_g2;
-  p[6] += t->n_full_factor;
-  p[7] += t->n_full_predict;
-}
-
 int mfgp_ctx_planner_stats(mfgp_ctx* c, int64_t* out, int n, int reset) {
   if (!c || (n > 0 && !out)) return set_err(MFGP_ERR_ARG, "null ctx/out");
   if (const int rc_ = settle(c)) return rc_;   // (a running early-return launch first)
@@ -1706,7 +1693,7 @@ int mfgp_clone(const mfgp_model* src, mfgp_model** out) {
     HIP_TRY(hipMemcpyAsync(m->grid, src->grid, sizeof(double) * 2 * src->M, hipMemcpyDeviceToDevice, c->stream));
     m->M = m->Mcap = src->M;
     m->lat = src->lat;
-    // resident V (the Choi planner clones a model and keeps appending to the copy, sim:339)
+    // resident V (a deepcopy'd model keeps appending to the copy, sim:339)
     if (m->factored && src->V && src->v_n > 0 && src->vld == round_up(m->cap, PRB)) {
       if ((rc = ensure_v(m))) return rc;
       HIP_TRY(hipMemcpyAsync(m->V, src->V, v_elem(src) * (size_t)src->vtiles * src->vld * PBM,
@@ -2525,6 +2512,100 @@ static int batch_run(mfgp_model** models, int count, const double* X, const doub
   return mfgp_ctx_synchronize(c);
 }
 
+// The planners work on the caller's model itself instead of a deep copy (sim:339):
+// the rows they append lie past the model's own, and the factor, z, V, F and the
+// tables of the leading rows do not depend on later rows, so truncating back to the
+// model's rows restores it. What the loop overwrites that a truncate does not bring
+// back is saved and restored: the resident posterior (both ping-pong buffers and
+// their tags: the lattice steps write them), the kept result's validity, the path
+// counters (the loop's steps go to the context's planner counters instead). A copy
+// of A, V and F (~320 MB per model at 128 x 128, N = 2048) and the allocations it
+// took cost more than the whole loop (profiles/r06a_choi: ~36 of 44 ms for 8 seeds).
+struct PlanSave {
+  int64_t NH0 = 0;
+  double* res = nullptr;   // device copy of m->res ([2][2][res_M]), or null
+  int64_t res_n[2];
+  uint64_t res_gen[2], res_tick[2], tick;
+  int res_depth[2];
+  bool spec_valid, spec_max, pred_since_append;
+  int64_t cnt[9];
+};
+static void plan_counters(const mfgp_model* m, int64_t (&v)[9]) {
+  const int64_t x[9] = {m->n_full_factor, m->n_inc_factor, m->n_full_predict, m->n_vstream, m->n_lattice,
+                        m->n_lattice_arg, m->n_lattice_g2, m->n_post_copy, m->n_early_pd};
+  for (int i = 0; i < 9; ++i) v[i] = x[i];
+}
+// doubles of device room plan_enter needs for m's resident posterior
+static size_t plan_res_doubles(const mfgp_model* m) { return m->res ? 4 * (size_t)m->res_M : 0; }
+// save what the loop may overwrite; `room` (plan_res_doubles) receives the posterior
+static int plan_enter(mfgp_model* m, PlanSave& s, double* room) {
+  s.NH0 = m->NH;
+  s.res = (m->res && room) ? room : nullptr;
+  if (s.res) HIP_TRY(hipMemcpyAsync(s.res, m->res, sizeof(double) * 4 * m->res_M, hipMemcpyDeviceToDevice, m->ctx->stream));
+  for (int b = 0; b < 2; ++b) {
+    s.res_n[b] = m->res_n[b];
+    s.res_gen[b] = m->res_gen[b];
+    s.res_tick[b] = m->res_tick[b];
+    s.res_depth[b] = m->res_depth[b];
+  }
+  s.tick = m->tick;
+  s.spec_valid = m->spec_valid;
+  s.spec_max = m->spec_max;
+  s.pred_since_append = m->pred_since_append;
+  plan_counters(m, s.cnt);
+  return MFGP_OK;
+}
+// back to the model's own rows and state (also after a failed loop: the error is
+// the caller's to return); the loop's path counters go to the context's
+static int plan_leave(mfgp_model* m, const PlanSave& s) {
+  m->gate_dev = nullptr;
+  int64_t now[9];
+  plan_counters(m, now);
+  int64_t* p = m->ctx->plan_stats;
+  p[0] += 1;
+  p[1] += now[1] - s.cnt[1];
+  p[2] += now[3] - s.cnt[3];
+  p[3] += now[4] - s.cnt[4];
+  p[4] += now[5] - s.cnt[5];
+  p[5] += now[6] - s.cnt[6];
+  p[6] += now[0] - s.cnt[0];
+  p[7] += now[2] - s.cnt[2];
+  m->n_full_factor = s.cnt[0];
+  m->n_inc_factor = s.cnt[1];
+  m->n_full_predict = s.cnt[2];
+  m->n_vstream = s.cnt[3];
+  m->n_lattice = s.cnt[4];
+  m->n_lattice_arg = s.cnt[5];
+  m->n_lattice_g2 = s.cnt[6];
+  m->n_post_copy = s.cnt[7];
+  m->n_early_pd = s.cnt[8];
+  m->NH = s.NH0;
+  const int64_t N = m->NL + m->NH;
+  if (m->factored && m->factor_N > N) m->factor_N = N;
+  m->v_n = std::min(m->v_n, N);
+  m->F_n = std::min(m->F_n, N);
+  m->tab_n = std::min(m->tab_n, N);
+  m->l21c_N = -1;   // (the compact rows in iscr are the loop's now)
+  if (s.res && m->res) {
+    HIP_TRY(hipMemcpyAsync(m->res, s.res, sizeof(double) * 4 * m->res_M, hipMemcpyDeviceToDevice, m->ctx->stream));
+    for (int b = 0; b < 2; ++b) {
+      m->res_n[b] = s.res_n[b];
+      m->res_gen[b] = s.res_gen[b];
+      m->res_tick[b] = s.res_tick[b];
+      m->res_depth[b] = s.res_depth[b];
+    }
+    m->tick = std::max(m->tick, s.tick);
+  } else {
+    for (int b = 0; b < 2; ++b)
+      if (m->res_n[b] > N) m->res_n[b] = -1;
+  }
+  // the kept result of the model's last predict: spec_out is not written by the loop
+  m->spec_valid = s.spec_valid && factor_current(m);
+  m->spec_max = s.spec_max && m->spec_valid;
+  m->pred_since_append = s.pred_since_append;
+  return MFGP_OK;
+}
+
 // compute_sample_points (simulator.py:326-374) as a device loop. Each iteration
 // is k_choi_select (argmax cell + its mean -> new hifi row, or stop), a 1-row
 // bordered append and a one-pass predict with the fused argmax, all gated by a
@@ -2543,15 +2624,15 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
   mfgp_ctx* c = model->ctx;
   if (!c->incremental) return set_err(MFGP_ERR_ARG, "mfgp_sample_points needs incremental updates enabled");
   if ((rc = update_factor(model))) return rc;
-  mfgp_model* t = nullptr;   // the reference works on a deep copy (sim:339)
-  if ((rc = mfgp_clone(model, &t))) return rc;
+  // the reference works on a deep copy (sim:339); here on the model itself, brought
+  // back to its own rows and state at the end (plan_enter / plan_leave)
+  mfgp_model* t = model;
   const int64_t M = t->M;
-  // workspace: mu, var [M] | vmax | vargmax | state {gate, count} | points [max_points][2]
-  const size_t nd = 2 * (size_t)M + 4 + 2 * (size_t)std::max<int64_t>(max_points, 1);
-  if ((rc = ensure_ws(c, sizeof(double) * nd))) {
-    mfgp_model_destroy(t);
-    return rc;
-  }
+  // workspace: mu, var [M] | vmax | vargmax | state {gate, count} | points [max_points][2] |
+  // the saved resident posterior
+  const size_t npt = 2 * (size_t)std::max<int64_t>(max_points, 1);
+  const size_t nd = 2 * (size_t)M + 4 + npt + plan_res_doubles(t);
+  if ((rc = ensure_ws(c, sizeof(double) * nd))) return rc;
   double* mu_s = c->ws;
   double* var_s = mu_s + M;
   double* vmax = var_s + M;
@@ -2559,11 +2640,13 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
   int64_t* state = vargmax + 1;
   double* pts = reinterpret_cast<double*>(state + 2);
   int* gate = reinterpret_cast<int*>(state);
+  PlanSave sv;
+  if ((rc = plan_enter(t, sv, pts + npt))) return rc;
   auto fail = [&](int code) {
-    mfgp_model_destroy(t);
+    (void)plan_leave(t, sv);
     return code;
   };
-  // initial posterior of the copy (sim:340-342)
+  // initial posterior (sim:340-342)
   if ((rc = batch_run(&t, 1, nullptr, nullptr, nullptr, mu_s, var_s, vmax, vargmax, 0, false, true))) return fail(rc);
   const int64_t st0[2] = {1, 0};
   if (hipMemcpyAsync(state, st0, sizeof(st0), hipMemcpyHostToDevice, c->stream) != hipSuccess)
@@ -2635,9 +2718,8 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
   if (done > 0 && hipMemcpy(points, pts, sizeof(double) * 2 * done, hipMemcpyDefault) != hipSuccess)
     return fail(set_err(MFGP_ERR_DEVICE, "sample_points: copy out failed"));
   *count = done;
-  plan_account(t);
-  mfgp_model_destroy(t);
-  return MFGP_OK;
+  if ((rc = plan_leave(t, sv))) return rc;
+  return mfgp_ctx_synchronize(c);   // (the posterior's restore copy: ws is reused by the next call)
 }
 
 // compute_sample_points for a batch of models (the Choi planner's sample-set
@@ -2647,8 +2729,9 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
 // step -- the lattice step where the batch takes it (its kernels and the V stream's
 // honour each model's device gate, so a model past its threshold skips the rest of
 // the chunk) -- with one host synchronisation per CH iterations. Each model works on
-// its own copy (sim:339); the chosen points are the single-model loop's, up to the
-// rounding of the batch step (ties decided by it).
+// its own rows past its own (sim:339's deep copy: plan_enter / plan_leave bring it
+// back); the chosen points are the single-model loop's, up to the rounding of the
+// batch step (ties decided by it).
 int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thresholds, int64_t max_points,
                              double* points, int64_t* counts) {
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
@@ -2664,29 +2747,24 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
     if (models[b]->ctx != c) return set_err(MFGP_ERR_ARG, "batch models must share one context");
     if (models[b]->dtype != models[0]->dtype) return set_err(MFGP_ERR_ARG, "batch models must share one dtype");
     if (models[b]->M <= 0) return set_err(MFGP_ERR_ARG, "model %d: no grid (call mfgp_set_grid first)", b);
+    for (int b2 = 0; b2 < b; ++b2)
+      if (models[b2] == models[b]) return set_err(MFGP_ERR_ARG, "model %d appears twice in the batch", b);
     counts[b] = 0;
   }
   for (int b = 0; b < count; ++b)
     if ((rc = update_factor(models[b]))) return rc;
-  std::vector<mfgp_model*> t(count, nullptr);
-  auto fail = [&](int code) {
-    for (auto m : t)
-      if (m) {
-        m->gate_dev = nullptr;
-        mfgp_model_destroy(m);
-      }
-    return code;
-  };
-  for (int b = 0; b < count; ++b)
-    if ((rc = mfgp_clone(models[b], &t[b]))) return fail(rc);
+  mfgp_model* const* t = models;
   // device state: mu, var [sum M] | vmax [B] | vargmax [B] | state [B][2] | thr [B] | moff [B] |
-  // Ms [B] | grids [B] | xn [B][2] | yn [B] | pos [B] | points [B][max_points][2]
+  // Ms [B] | grids [B] | xn [B][2] | yn [B] | pos [B] | points [B][max_points][2] | the models'
+  // saved resident posteriors
   std::vector<int64_t> moff(count), Ms(count);
   int64_t Mtot = 0;
+  size_t nres = 0;
   for (int b = 0; b < count; ++b) {
     moff[b] = Mtot;
     Ms[b] = t[b]->M;
     Mtot += t[b]->M;
+    nres += plan_res_doubles(t[b]);
   }
   const int64_t P = std::max<int64_t>(max_points, 1);
   // one 8-byte slot per entry (pos's ints take a slot each); the offsets below are
@@ -2695,13 +2773,22 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
   const size_t o_mu = 0, o_var = o_mu + (size_t)Mtot, o_vmax = o_var + (size_t)Mtot, o_varg = o_vmax + B_;
   const size_t o_state = o_varg + B_, o_thr = o_state + 2 * B_, o_moff = o_thr + B_, o_Ms = o_moff + B_;
   const size_t o_grids = o_Ms + B_, o_xn = o_grids + B_, o_yn = o_xn + 2 * B_, o_pos = o_yn + B_;
-  const size_t o_pts = o_pos + B_, nd = o_pts + 2 * B_ * (size_t)P;
+  const size_t o_pts = o_pos + B_, o_res = o_pts + 2 * B_ * (size_t)P, nd = o_res + nres;
   double* ws = nullptr;
-  if (hipMalloc(&ws, sizeof(double) * nd) != hipSuccess) return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: out of memory"));
-  auto fail2 = [&](int code) {
+  if (hipMalloc(&ws, sizeof(double) * nd) != hipSuccess)
+    return set_err(MFGP_ERR_DEVICE, "batch_sample_points: out of memory");
+  std::vector<PlanSave> sv(count);
+  int entered = 0;
+  auto fail = [&](int code) {
+    for (int b = 0; b < entered; ++b) (void)plan_leave(t[b], sv[b]);
+    (void)hipStreamSynchronize(c->stream);   // (the restore copies read ws)
     (void)hipFree(ws);
-    return fail(code);
+    return code;
   };
+  for (size_t b = 0, off = o_res; b < B_; off += plan_res_doubles(t[b]), ++b) {
+    if ((rc = plan_enter(t[b], sv[b], ws + off))) return fail(rc);
+    ++entered;
+  }
   double* mu = ws + o_mu;
   double* var = ws + o_var;
   double* vmax = ws + o_vmax;
@@ -2728,10 +2815,11 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
       hipMemcpyAsync(moff_d, moff.data(), sizeof(int64_t) * count, hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(Ms_d, Ms.data(), sizeof(int64_t) * count, hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(grids_d, grids.data(), sizeof(double*) * count, hipMemcpyHostToDevice, s) != hipSuccess)
-    return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: state upload failed"));
-  // the copies' initial posteriors and their max / argmax (sim:340-342)
-  if ((rc = batch_run(t.data(), count, nullptr, nullptr, nullptr, mu, var, vmax, vargmax, 0, false, true)))
-    return fail2(rc);
+    return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: state upload failed"));
+  // the initial posteriors and their max / argmax (sim:340-342)
+  if ((rc = batch_run(const_cast<mfgp_model**>(t), count, nullptr, nullptr, nullptr, mu, var, vmax, vargmax, 0,
+                      false, true)))
+    return fail(rc);
   for (int b = 0; b < count; ++b) t[b]->gate_dev = reinterpret_cast<int*>(state + 2 * b);
   // the models still running (the batch step's members; a stopped one leaves at the
   // next chunk boundary), their offsets into mu / var and indices into vmax
@@ -2754,24 +2842,24 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
       lvi.push_back(b);
     }
     if (hipMemcpyAsync(pos_d, pos.data(), sizeof(int) * count, hipMemcpyHostToDevice, s) != hipSuccess)
-      return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: upload failed"));
+      return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: upload failed"));
     for (int64_t it = 0; it < C; ++it) {
       if (launch_choi_select_batch(count, pos_d, state, thr, vmax, vargmax, mu, moff_d, grids_d, Ms_d, xn, yn, pts,
                                    max_points, s) != hipSuccess)
-        return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: launch failed"));
+        return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: launch failed"));
       if ((int)lm.size() == count)
         rc = batch_run(lm.data(), count, xn, yn, lk.data(), mu, var, vmax, vargmax, MFGP_ASYNC, true, true);
       else
         rc = batch_run(lm.data(), (int)lm.size(), xn, yn, lk.data(), mu, var, vmax, vargmax, MFGP_ASYNC, true, true,
                        loff.data(), lvi.data());
-      if (rc) return fail2(rc);
+      if (rc) return fail(rc);
     }
     it_done += C;
     if (hipMemcpyAsync(st.data(), state, sizeof(int64_t) * 2 * count, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
-      return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: state read failed"));
+      return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: state read failed"));
     for (int b : live)
-      if ((rc = read_status(t[b]))) return fail2(rc);
+      if ((rc = read_status(t[b]))) return fail(rc);
     std::vector<int> keep;
     for (int b : live)
       if ((int)st[2 * b] != 0) keep.push_back(b);
@@ -2781,15 +2869,13 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
     counts[b] = st[2 * b + 1];
     if (counts[b] > 0 && hipMemcpy(points + 2 * (size_t)b * (size_t)P, pts + 2 * (size_t)b * (size_t)P,
                                    sizeof(double) * 2 * counts[b], hipMemcpyDefault) != hipSuccess)
-      return fail2(set_err(MFGP_ERR_DEVICE, "batch_sample_points: copy out failed"));
+      return fail(set_err(MFGP_ERR_DEVICE, "batch_sample_points: copy out failed"));
   }
+  for (int b = 0; b < count; ++b) (void)plan_leave(t[b], sv[b]);
+  entered = 0;
+  const bool sync_ok = hipStreamSynchronize(s) == hipSuccess;   // (the restore copies read ws)
   (void)hipFree(ws);
-  for (auto m : t) {
-    m->gate_dev = nullptr;
-    plan_account(m);
-    mfgp_model_destroy(m);
-  }
-  return MFGP_OK;
+  return sync_ok ? MFGP_OK : set_err(MFGP_ERR_DEVICE, "batch_sample_points: restore failed");
 }
 
 // Voronoi-cell reductions (simulator.py:194-323) on the device. Inputs may be

@@ -8,7 +8,11 @@ the threshold, and return the chosen cells in order. Here the whole loop runs
 on the device (libmfgp_hip's mfgp_sample_points): every iteration is a 1-row
 bordered Cholesky append plus one pass over the resident V with a fused argmax,
 and the host synchronises once per 32 iterations. Same signature, same return
-value, same model-unchanged contract (the reference works on ``copy.deepcopy``).
+value, same model-unchanged contract: the reference works on ``copy.deepcopy``;
+here the rows go past the model's own and are dropped at the end (the leading
+rows' factor, V and F do not depend on them), and what the loop overwrites
+besides -- the resident posterior, the kept result, the path counters -- is saved
+and restored, so no copy of the model's device state is made.
 
 ``compute_sample_points_batch`` runs the same loop for many models at once (the
 Choi planner of a rank's Monte-Carlo seeds: one seed's sample set each): every

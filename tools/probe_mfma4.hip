@@ -1,0 +1,87 @@
+// Probe: the 4x4x4 f64 MFMA (v_mfma_f64_4x4x4_4b_f64) on gfx950 -- its operand /
+// accumulator lane maps (one-hot products, every (a-lane, b-lane) pair in one launch)
+// and its issue rate against v_mfma_f64_16x16x4_f64. For the w units of the lattice
+// step, whose 16-row A operand holds only k <= 8 live rows.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/probe_mfma4.hip -o /tmp/probe_mfma4
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP %s at %d\n",hipGetErrorString(e),__LINE__); return 1;}}while(0)
+
+// wave p*64+q: a = one-hot at lane p (value 1), b = one-hot at lane q (value 1);
+// out[(p*64+q)*64 + l] = c of lane l
+__global__ void onehot_k(double* out) {
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  const int p = wv >> 6, q = wv & 63;
+  const double a = l == p ? 1.0 : 0.0, b = l == q ? 1.0 : 0.0;
+  const double c = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, 0.0, 0, 0, 0);
+  out[(size_t)wv * 64 + l] = c;
+}
+
+template <bool SMALL>
+__global__ __launch_bounds__(256) void rate_k(double* out, long long* st, int iters) {
+  const int l = threadIdx.x;
+  const double a = 1.0 + 1e-9 * l, b = 1.0 - 1e-9 * l;
+  long long t0 = __builtin_amdgcn_s_memtime();
+  double s = 0.0;
+  if constexpr (SMALL) {
+    double c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
+    for (int i = 0; i < iters; i++) {
+      c0 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c3, 0, 0, 0);
+      c4 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c4, 0, 0, 0);
+      c5 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c5, 0, 0, 0);
+      c6 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c6, 0, 0, 0);
+      c7 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c7, 0, 0, 0);
+    }
+    s = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
+  } else {
+    d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+    for (int i = 0; i < iters; i++) {
+      c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
+    }
+    d4 t = c0 + c1;
+    s = t[0] + t[1] + t[2] + t[3];
+  }
+  long long t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * 256 + l] = s;
+  if (l == 0 && blockIdx.x == 0) st[0] = t1 - t0;
+}
+
+int main() {
+  int dev; CK(hipGetDevice(&dev)); hipDeviceProp_t pr; CK(hipGetDeviceProperties(&pr, dev));
+  double* d; CK(hipMalloc(&d, sizeof(double) * 4096 * 64));
+  long long* st; CK(hipMalloc(&st, 16));
+  onehot_k<<<1024, 256>>>(d); CK(hipDeviceSynchronize());
+  std::vector<double> h(4096 * 64);
+  CK(hipMemcpy(h.data(), d, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+  // every (a-lane p, b-lane q) whose product lands somewhere: "p q -> l"
+  int n = 0;
+  for (int p = 0; p < 64; ++p)
+    for (int q = 0; q < 64; ++q)
+      for (int l = 0; l < 64; ++l)
+        if (h[(size_t)(p * 64 + q) * 64 + l] != 0.0) {
+          printf("map a%d b%d -> c%d (%g)\n", p, q, l, h[(size_t)(p * 64 + q) * 64 + l]);
+          ++n;
+        }
+  printf("products landing: %d\n", n);
+  const int nb = pr.multiProcessorCount * 4, iters = 4096;
+  for (int small = 0; small < 2; ++small) {
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); float ms;
+    if (small) rate_k<true><<<nb, 256>>>(d, st, 64); else rate_k<false><<<nb, 256>>>(d, st, 64);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    if (small) rate_k<true><<<nb, 256>>>(d, st, iters); else rate_k<false><<<nb, 256>>>(d, st, iters);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+    long long cyc; CK(hipMemcpy(&cyc, st, 8, hipMemcpyDeviceToHost));
+    // MACs per instruction: 4x4x4 x 4 blocks = 256; 16x16x4 = 1024
+    const double macs = small ? (double)nb * 4 * iters * 8 * 256 : (double)nb * 4 * iters * 2 * 1024;
+    printf("%s: %.3f ms, %.2f TF (2 flop per MAC), wave0 %.1f cycles per instruction\n",
+           small ? "4x4x4_4b " : "16x16x4  ", ms, 2 * macs / ms / 1e9, (double)cyc / iters / (small ? 8 : 2));
+  }
+  return 0;
+}
