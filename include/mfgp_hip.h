@@ -119,8 +119,9 @@ int mfgp_ctx_reset_timing(mfgp_ctx* ctx);
  * the last reset: out[0..n) = {model runs, bordered appends, one-pass predicts (V stream or
  * lattice step), lattice steps, of them launched with their descriptors by
  * value, of them with the GEMM and cells as a second launch, full refactors, full
- * predicts}; n <= 8. reset != 0 zeroes them after the read. Which step form the
- * Choi iterations took (tools/bench_planner.py). */
+ * predicts, then the batched planner's host time in microseconds before, in and
+ * after its iteration loop}; n <= 11. reset != 0 zeroes them after the read. Which
+ * step form the Choi iterations took and where their time went (tools/bench_planner.py). */
 int mfgp_ctx_planner_stats(mfgp_ctx* ctx, int64_t* out, int n, int reset);
 
 /* SFGP.__init__ (gp:28-64) / MFGP.__init__ (gp:276-327) with the caller's

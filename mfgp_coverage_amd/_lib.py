@@ -214,7 +214,7 @@ class Context:
                 "factor_ms": fm.value, "factor_calls": fn.value}
 
     PLANNER_KEYS = ("runs", "inc_factor", "vstream", "lattice", "lattice_arg", "lattice_g2", "full_factor",
-                    "full_predict")
+                    "full_predict", "batch_setup_us", "batch_loop_us", "batch_finish_us")
 
     def planner_stats(self, reset=False):
         """Path counters of the planners' loops (mfgp_sample_points /

@@ -72,10 +72,10 @@ constexpr size_t F32_SCRATCH = size_t(16) << 30;   // bytes of fp64 V scratch fo
 // and for at most LAT_MAXD consecutive steps before var / mu are recomputed from V
 constexpr double LAT_RMAX = 1e4;
 constexpr int LAT_MAXD = 256;
-// planner working-copy counters (mfgp_ctx_planner_stats): copies, bordered appends,
-// V-stream predicts, lattice steps (of them by value / with k_lat_gemm2), full
-// factors, full predicts
-constexpr int PLAN_NSTATS = 8;
+// planner counters (mfgp_ctx_planner_stats): model runs, bordered appends, V-stream
+// predicts, lattice steps (of them by value / with k_lat_gemm2), full factors, full
+// predicts; then the batched planner's host time (us) before, in and after its loop
+constexpr int PLAN_NSTATS = 11;
 
 struct EvPair {
   hipEvent_t a, b;
@@ -2734,6 +2734,7 @@ int mfgp_sample_points(mfgp_model* model, double threshold, int64_t max_points, 
 // batch step (ties decided by it).
 int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thresholds, int64_t max_points,
                              double* points, int64_t* counts) {
+  const auto tp0 = std::chrono::steady_clock::now();
   const DeviceGuard dg_((models && count > 0 && models[0]) ? models[0]->ctx->device : -1);
   if (const int rc_ = settle((models && count > 0 && models[0]) ? models[0]->ctx : nullptr)) return rc_;
   if (count <= 0 || !models || !thresholds || !counts || (max_points > 0 && !points))
@@ -2827,6 +2828,7 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
   for (int b = 0; b < count; ++b) live[b] = b;
   constexpr int64_t CH = 32;
   int64_t it_done = 0;
+  const auto tp1 = std::chrono::steady_clock::now();
   while (!live.empty() && it_done < max_points) {
     const int64_t C = std::min<int64_t>(CH, max_points - it_done);
     // the live models are the batch step's members, in batch order: their rows at
@@ -2865,6 +2867,7 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
       if ((int)st[2 * b] != 0) keep.push_back(b);
     live.swap(keep);
   }
+  const auto tp2 = std::chrono::steady_clock::now();
   for (int b = 0; b < count; ++b) {
     counts[b] = st[2 * b + 1];
     if (counts[b] > 0 && hipMemcpy(points + 2 * (size_t)b * (size_t)P, pts + 2 * (size_t)b * (size_t)P,
@@ -2875,6 +2878,13 @@ int mfgp_batch_sample_points(mfgp_model** models, int count, const double* thres
   entered = 0;
   const bool sync_ok = hipStreamSynchronize(s) == hipSuccess;   // (the restore copies read ws)
   (void)hipFree(ws);
+  const auto tp3 = std::chrono::steady_clock::now();
+  auto us = [](std::chrono::steady_clock::duration dt) {
+    return (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(dt).count();
+  };
+  c->plan_stats[8] += us(tp1 - tp0);
+  c->plan_stats[9] += us(tp2 - tp1);
+  c->plan_stats[10] += us(tp3 - tp2);
   return sync_ok ? MFGP_OK : set_err(MFGP_ERR_DEVICE, "batch_sample_points: restore failed");
 }
 

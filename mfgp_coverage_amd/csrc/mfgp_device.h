@@ -32,6 +32,13 @@ __device__ __forceinline__ int swz(int k, int i) { return k * NB + (i ^ ((k & 1)
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+// v_mfma_f64_4x4x4_4b_f64: four independent 4 x 4 x 4 blocks; lane l = 16 k + 4 blk + r
+// holds A_blk[r][k] and B_blk[k][r], and C lane 16 i + 4 blk + j holds C_blk[i][j]
+// (tools/probe_mfma4.hip, one-hot products); 1.64x the multiply-adds per cycle of
+// the 16x16x4 form on gfx950
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
 // exact f32 (v_mfma_f32_16x16x4_f32 = an fmaf chain). A/B lane maps as the f64
 // form; C/D: lane (r, g) register v holds row 4g + v, column r (the f64 form:
 // row g + 4v).

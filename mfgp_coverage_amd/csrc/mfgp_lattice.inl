@@ -252,15 +252,27 @@ __device__ __forceinline__ int64_t wst_pos(int64_t nwb, int64_t jb) {
 // is), stores the block of w, counts it into ldone[0] (the Z units wait for all
 // nwb blocks) and writes F's new rows for its columns, -L22^-1 w^T (the top
 // block's also the L22^-1 entries).
-template <class VT>
+template <int KA, class VT>
 __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* sm) {
   // steps in flight per wave: the loop is latency-bound (each step waits for loads
   // issued DEPTH - 1 steps earlier), so fp32 F, whose raw 16-byte rows take half the
   // registers of the widened pairs, keeps more in flight
   constexpr int DEPTH = sizeof(VT) == 4 ? MFGP_W_DEPTH_F : MFGP_W_DEPTH;
+  // M4: appends of k <= 8 rows (KA = 8) take the 4x4x4 f64 MFMA (v_mfma_f64_4x4x4_4b:
+  // four 4 x 4 blocks, K = 4), whose blocks hold exactly the k <= 8 live rows a of w
+  // in two instructions (a = r' + 4 t) where the 16x16x4 form's 16-row A operand
+  // left half its rows zero; and on gfx950 it issues 1.64x the 16x16x4 form's
+  // multiply-adds per cycle (tools/probe_mfma4.hip): the w units' MFMA time / 3.3.
+  // Lane l = 16 q + 4 blk + r' (q: the K row, as before): A = L21c[i][r' + 4 t],
+  // B = the lane's F value s, C lane 16 i + 4 blk + j = w[col_s(4 blk + j)][i + 4 t]
+  constexpr bool M4 = KA == 8;
+  constexpr int NA = M4 ? 2 : 1;   // A values per lane and step
   // a step's F in registers: two widened pairs (fp64 F) or the raw four floats (fp32)
   struct FRow {
     dv2 v[sizeof(VT) == 4 ? 1 : 2];
+  };
+  struct ARow {
+    double v[NA];
   };
   const int64_t n0 = d.n0, ld = d.ld;
   const int nwb = d.nwb;
@@ -366,36 +378,57 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   // of that cell, read here straight from the resident V (rows < n0: not written
   // in this launch): the F stream starts at once instead of after the producers'
   // compact rows (~9 us). Otherwise the compact rows, after the producers' flags.
-  const VT* asrc;
+  // the rows a of w this lane's A values carry: r (16x16x4), r' + 4 t (M4)
+  const int ar0 = M4 ? (lane & 3) : r;
+  const VT* asrc[NA];
   int64_t astr;
   bool selfg;
   {
     const GridLattice L = d.lat;
-    const double* p = row_pt(d, n0 + (r < k ? r : 0));
-    const double px = p[0], py = p[1];
-    const int ix = (int)rint(fmin(fmax((px - L.x0) * L.xinv, 0.0), (double)(L.nx - 1)));
-    const int iy = (int)rint(fmin(fmax((py - L.y0) * L.yinv, 0.0), (double)(L.ny - 1)));
-    const int64_t cr = (px == px && py == py) ? ix * L.sx + iy * L.sy : 0;
-    const dv2 g = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid))[cr];
-    const bool miss = r < k && !(g.x == px && g.y == py);
+    int64_t cr[NA];
+    bool miss = false;
+#pragma unroll
+    for (int t = 0; t < NA; ++t) {
+      const int a = ar0 + 4 * t;
+      const double* p = row_pt(d, n0 + (a < k ? a : 0));
+      const double px = p[0], py = p[1];
+      const int ix = (int)rint(fmin(fmax((px - L.x0) * L.xinv, 0.0), (double)(L.nx - 1)));
+      const int iy = (int)rint(fmin(fmax((py - L.y0) * L.yinv, 0.0), (double)(L.ny - 1)));
+      cr[t] = (px == px && py == py) ? ix * L.sx + iy * L.sy : 0;
+      const dv2 g = reinterpret_cast<const GLOBAL dv2*>(gp(d.grid))[cr[t]];
+      miss = miss || (a < k && !(g.x == px && g.y == py));
+    }
     selfg = d.lat_selfg && L.nx > 0 && d.vres >= n0 && vres_ptr<VT>(d) != nullptr && __ballot(miss) == 0;
-    // (lanes r >= k carry no point: they read lane 0's element, the same line, so the
-    // compact rows' unused half costs no traffic; their MFMA input is zeroed)
-    asrc = selfg ? vres_ptr<VT>(d) + (cr / PBM) * d.vld * PBM + (cr % PBM)
-                 : reinterpret_cast<const VT*>(l21c) + (r < k ? r : 0);
+    // (lanes whose row a >= k carry no point: they read row 0's element, the same
+    // line, so the compact rows' unused part costs no traffic; their MFMA input is zeroed)
+#pragma unroll
+    for (int t = 0; t < NA; ++t) {
+      const int a = ar0 + 4 * t;
+      asrc[t] = selfg ? vres_ptr<VT>(d) + (cr[t] / PBM) * d.vld * PBM + (cr[t] % PBM)
+                      : reinterpret_cast<const VT*>(l21c) + (a < k ? a : 0);
+    }
     astr = selfg ? (int64_t)PBM : (int64_t)KINC;
   }
-  auto load_a = [&](const Cur& c, double& a) {
+  auto load_a = [&](const Cur& c, ARow& a) {
     const int64_t i = row_of(c);
     // L2-served (the compact rows were stored in this launch)
-    a = (double)__hip_atomic_load(gp(asrc) + (i < n0 ? i : n0 - 1) * astr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  d4 acc[4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < NA; ++t)
+      a.v[t] = (double)__hip_atomic_load(gp(asrc[t]) + (i < n0 ? i : n0 - 1) * astr, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // 16x16x4: acc[2 hh + c] (lane (n, g) register v: w[col 32 hh + 2 n + c][a = g + 4 v]);
+  // M4: acc4[s][t] (lane 16 i + 4 blk + j: w[col_s(4 blk + j)][a = i + 4 t])
+  d4 acc[M4 ? 1 : 4];
+  double acc4[M4 ? 4 : 1][NA];
+#pragma unroll
+  for (int c = 0; c < (M4 ? 1 : 4); ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < (M4 ? 4 : 1); ++c)
+#pragma unroll
+    for (int t = 0; t < NA; ++t) acc4[c][t] = 0.0;
   // (columns a >= k of w are never read: zero)
-  auto compute = [&](const FRow& fr, double a, bool live) {
-    const double av = (live && r < k) ? a : 0.0;
+  auto compute = [&](const FRow& fr, const ARow& a, bool live) {
     dv2 f[2];
     if constexpr (sizeof(VT) == 4) {
       const f4 fq = __builtin_bit_cast(f4, fr.v[0]);   // columns 4 r .. 4 r + 3, widened
@@ -405,10 +438,24 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
       f[0] = fr.v[0];
       f[1] = fr.v[sizeof(VT) == 4 ? 0 : 1];
     }
+    if constexpr (M4) {
+      // F value s = 2 hh + c of the lane: column 32 hh + 2 r + c (fp64), 4 r + s (fp32)
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      acc[2 * hh] = mfma(av, f[hh].x, acc[2 * hh]);
-      acc[2 * hh + 1] = mfma(av, f[hh].y, acc[2 * hh + 1]);
+      for (int t = 0; t < NA; ++t) {
+        const double av = (live && ar0 + 4 * t < k) ? a.v[t] : 0.0;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          acc4[2 * hh][t] = mfma4(av, f[hh].x, acc4[2 * hh][t]);
+          acc4[2 * hh + 1][t] = mfma4(av, f[hh].y, acc4[2 * hh + 1][t]);
+        }
+      }
+    } else {
+      const double av = (live && r < k) ? a.v[0] : 0.0;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        acc[2 * hh] = mfma(av, f[hh].x, acc[2 * hh]);
+        acc[2 * hh + 1] = mfma(av, f[hh].y, acc[2 * hh + 1]);
+      }
     }
   };
   int nseg = 0;
@@ -443,21 +490,43 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
     double own[4];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
+      if constexpr (M4) {
+        // half hh: the lane's F values s = 2 hh + c; red [4 w][c][t][64]
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) red[w * 512 + (c * 4 + v) * 64 + lane] = acc[2 * hh + c][v];
-      lds_barrier();
+          for (int t = 0; t < NA; ++t) red[w * 256 + (c * 2 + t) * 64 + lane] = acc4[2 * hh + c][t];
+        lds_barrier();
 #pragma unroll
-      for (int m2 = 0; m2 < 2; ++m2) {
-        const int e = tid + NT * m2, jh = e >> 4, a = e & 15;
-        const int o = ((jh & 1) * 4 + (a >> 2)) * 64 + 16 * (a & 3) + (jh >> 1);
-        own[2 * hh + m2] = (red[o] + red[512 + o]) + (red[1024 + o] + red[1536 + o]);
+        for (int m2 = 0; m2 < 2; ++m2) {
+          // output (local column jh of the half, row a): the lane 16 (a & 3) + (jh >> 1)
+          // (r = 4 blk + j = jh >> 1), value c = jh & 1, t = a >> 2
+          const int e = tid + NT * m2, jh = e >> 4, a = e & 15;
+          const int o = ((jh & 1) * 2 + ((a >> 2) & 1)) * 64 + 16 * (a & 3) + (jh >> 1);
+          own[2 * hh + m2] = a < 8 ? (red[o] + red[256 + o]) + (red[512 + o] + red[768 + o]) : 0.0;
+        }
+        lds_barrier();
+      } else {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) red[w * 512 + (c * 4 + v) * 64 + lane] = acc[2 * hh + c][v];
+        lds_barrier();
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2) {
+          const int e = tid + NT * m2, jh = e >> 4, a = e & 15;
+          const int o = ((jh & 1) * 4 + (a >> 2)) * 64 + 16 * (a & 3) + (jh >> 1);
+          own[2 * hh + m2] = (red[o] + red[512 + o]) + (red[1024 + o] + red[1536 + o]);
+        }
+        lds_barrier();
       }
-      lds_barrier();
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int c = 0; c < (M4 ? 1 : 4); ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < (M4 ? 4 : 1); ++c)
+#pragma unroll
+      for (int t = 0; t < NA; ++t) acc4[c][t] = 0.0;
     // own[2 hh + m2] is output e = 512 hh + tid + 256 m2 of the block
     if (defer && jb_s < 0) {
 #pragma unroll
@@ -474,7 +543,7 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   // load would make the compiler's wait for the current step also wait for the
   // loads behind it.
   FRow fb[DEPTH];
-  double ab[DEPTH];
+  ARow ab[DEPTH];
   Cur cl = cur0;   // the next step to load (clamped to the last)
   int64_t tl = 0;
   auto next_load = [&]() {
@@ -1720,7 +1789,7 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     return;
   }
   if (role < np + d.nwu) {
-    lat_wblock<VT>(d, role - np, sm);
+    lat_wblock<KA, VT>(d, role - np, sm);
     return;
   }
   if (role < np + d.nwu + d.nzu) {

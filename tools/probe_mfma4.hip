@@ -11,11 +11,13 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 // wave p*64+q: a = one-hot at lane p (value 1), b = one-hot at lane q (value 1);
 // out[(p*64+q)*64 + l] = c of lane l
+// BC: the A broadcast (cbsz = 2: every block takes block abid's A)
+template <int BC, int ABID>
 __global__ void onehot_k(double* out) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
   const int p = wv >> 6, q = wv & 63;
   const double a = l == p ? 1.0 : 0.0, b = l == q ? 1.0 : 0.0;
-  const double c = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, 0.0, 0, 0, 0);
+  const double c = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, 0.0, BC, ABID, 0);
   out[(size_t)wv * 64 + l] = c;
 }
 
@@ -23,7 +25,7 @@ template <bool SMALL>
 __global__ __launch_bounds__(256) void rate_k(double* out, long long* st, int iters) {
   const int l = threadIdx.x;
   const double a = 1.0 + 1e-9 * l, b = 1.0 - 1e-9 * l;
-  long long t0 = __builtin_amdgcn_s_memtime();
+  long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   double s = 0.0;
   if constexpr (SMALL) {
     double c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
@@ -43,32 +45,43 @@ __global__ __launch_bounds__(256) void rate_k(double* out, long long* st, int it
     for (int i = 0; i < iters; i++) {
       c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
       c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
     }
-    d4 t = c0 + c1;
+    d4 t = c0 + c1 + c2 + c3;
     s = t[0] + t[1] + t[2] + t[3];
   }
-  long long t1 = __builtin_amdgcn_s_memtime();
+  long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   out[blockIdx.x * 256 + l] = s;
-  if (l == 0 && blockIdx.x == 0) st[0] = t1 - t0;
+  if (l == 0 && blockIdx.x == 0) {
+    st[0] = t1 - t0;
+    st[1] = r1 - r0;
+  }
 }
 
 int main() {
   int dev; CK(hipGetDevice(&dev)); hipDeviceProp_t pr; CK(hipGetDeviceProperties(&pr, dev));
   double* d; CK(hipMalloc(&d, sizeof(double) * 4096 * 64));
   long long* st; CK(hipMalloc(&st, 16));
-  onehot_k<<<1024, 256>>>(d); CK(hipDeviceSynchronize());
   std::vector<double> h(4096 * 64);
-  CK(hipMemcpy(h.data(), d, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
-  // every (a-lane p, b-lane q) whose product lands somewhere: "p q -> l"
-  int n = 0;
-  for (int p = 0; p < 64; ++p)
-    for (int q = 0; q < 64; ++q)
-      for (int l = 0; l < 64; ++l)
-        if (h[(size_t)(p * 64 + q) * 64 + l] != 0.0) {
-          printf("map a%d b%d -> c%d (%g)\n", p, q, l, h[(size_t)(p * 64 + q) * 64 + l]);
-          ++n;
-        }
-  printf("products landing: %d\n", n);
+  for (int v = 0; v < 3; ++v) {
+    if (v == 0) onehot_k<0, 0><<<1024, 256>>>(d);
+    else if (v == 1) onehot_k<2, 1><<<1024, 256>>>(d);
+    else onehot_k<2, 3><<<1024, 256>>>(d);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h.data(), d, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+    // every (a-lane p, b-lane q) whose product lands somewhere: "p q -> l"
+    int n = 0;
+    printf("variant %s\n", v == 0 ? "cbsz 0" : (v == 1 ? "cbsz 2 abid 1" : "cbsz 2 abid 3"));
+    for (int p = 0; p < 64; ++p)
+      for (int q = 0; q < 64; ++q)
+        for (int l = 0; l < 64; ++l)
+          if (h[(size_t)(p * 64 + q) * 64 + l] != 0.0) {
+            printf("map a%d b%d -> c%d (%g)\n", p, q, l, h[(size_t)(p * 64 + q) * 64 + l]);
+            ++n;
+          }
+    printf("products landing: %d\n", n);
+  }
   const int nb = pr.multiProcessorCount * 4, iters = 4096;
   for (int small = 0; small < 2; ++small) {
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); float ms;
@@ -77,11 +90,12 @@ int main() {
     CK(hipEventRecord(e0));
     if (small) rate_k<true><<<nb, 256>>>(d, st, iters); else rate_k<false><<<nb, 256>>>(d, st, iters);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
-    long long cyc; CK(hipMemcpy(&cyc, st, 8, hipMemcpyDeviceToHost));
+    long long cyc[2]; CK(hipMemcpy(cyc, st, 16, hipMemcpyDeviceToHost));
     // MACs per instruction: 4x4x4 x 4 blocks = 256; 16x16x4 = 1024
-    const double macs = small ? (double)nb * 4 * iters * 8 * 256 : (double)nb * 4 * iters * 2 * 1024;
-    printf("%s: %.3f ms, %.2f TF (2 flop per MAC), wave0 %.1f cycles per instruction\n",
-           small ? "4x4x4_4b " : "16x16x4  ", ms, 2 * macs / ms / 1e9, (double)cyc / iters / (small ? 8 : 2));
+    const double macs = small ? (double)nb * 4 * iters * 8 * 256 : (double)nb * 4 * iters * 4 * 1024;
+    printf("%s: %.3f ms, %.2f TF (2 flop per MAC), wave0 %.1f cycles per instruction, clock %.0f MHz\n",
+           small ? "4x4x4_4b " : "16x16x4  ", ms, 2 * macs / ms / 1e9, (double)cyc[0] / iters / (small ? 8 : 4),
+           100.0 * cyc[0] / (double)cyc[1]);
   }
   return 0;
 }
