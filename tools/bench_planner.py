@@ -77,20 +77,37 @@ def batch(a):
     compute_sample_points(ms[0], xs, 0.99 * thr[0] / a.frac, False)
     from mfgp_coverage_amd import _lib
     ctx = _lib.context()
-    ctx.planner_stats(reset=True)
-    t0 = time.perf_counter()
-    pb = compute_sample_points_batch(ms, xs, thr)
-    tb = time.perf_counter() - t0
-    st_b = ctx.planner_stats(reset=True)   # which step form the batched iterations took
-    t0 = time.perf_counter()
-    ps = [compute_sample_points(m, xs, t, False) for m, t in zip(ms, thr)]
-    t1 = time.perf_counter() - t0
-    st_s = ctx.planner_stats(reset=True)
+
+    def timed_batch():
+        ctx.planner_stats(reset=True)
+        t0 = time.perf_counter()
+        pb = compute_sample_points_batch(ms, xs, thr)
+        tb = time.perf_counter() - t0
+        return pb, tb, ctx.planner_stats(reset=True)   # which step form the iterations took
+
+    def timed_single():
+        t0 = time.perf_counter()
+        ps = [compute_sample_points(m, xs, t, False) for m, t in zip(ms, thr)]
+        return ps, time.perf_counter() - t0, ctx.planner_stats(reset=True)
+
+    # cold: the first selection at these thresholds, which grows each model's capacity
+    # (and so rebuilds its F) for the rows it appends -- what the period's own appends
+    # would pay next (the planners work in place and keep the grown capacity); warm: the
+    # same selection again, the models' state as it is between periods of a running
+    # simulation (same capacity, F current)
+    pb_c, tb_c, st_bc = timed_batch()
+    ps_c, t1_c, st_sc = timed_single()
+    pb, tb, st_b = timed_batch()
+    ps, t1, st_s = timed_single()
     same = [int(np.array_equal(x, y)) for x, y in zip(pb, ps)]
+    same_cold = [int(np.array_equal(x, y)) for x, y in zip(pb, pb_c)]
     its = max(p.shape[0] for p in pb)
     out = {"batch": a.batch, "points": [int(p.shape[0]) for p in pb], "batched_s": tb, "one_at_a_time_s": t1,
            "speedup": t1 / tb, "batched_ms_per_iteration": 1e3 * tb / max(1, its),
            "seed_iterations_per_s": sum(p.shape[0] for p in pb) / tb, "equal_to_single": same,
+           "cold": {"batched_s": tb_c, "one_at_a_time_s": t1_c, "speedup": t1_c / tb_c,
+                    "batched_ms_per_iteration": 1e3 * tb_c / max(1, its), "equal_to_warm": same_cold,
+                    "batched_paths": st_bc, "single_paths": st_sc},
            "grid": a.grid, "N_start": a.nl + a.nh, "threshold_frac": a.frac,
            "batched_paths": st_b, "single_paths": st_s}
     print(json.dumps(out), flush=True)

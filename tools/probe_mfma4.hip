@@ -59,6 +59,94 @@ __global__ __launch_bounds__(256) void rate_k(double* out, long long* st, int it
   }
 }
 
+// random operands (per lane, from memory), 4 rotating values: the power / toggling
+// state of a real GEMM (the 16x16x4 form ran faster on random data)
+template <bool SMALL>
+__global__ __launch_bounds__(256) void rate_rand_k(const double* __restrict__ rnd, double* out, int iters) {
+  const int l = threadIdx.x;
+  double a[4], b[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = rnd[(blockIdx.x * 256 + l) * 8 + i];
+    b[i] = rnd[(blockIdx.x * 256 + l) * 8 + 4 + i];
+  }
+  double s = 0.0;
+  if constexpr (SMALL) {
+    double c[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] = 0.0;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[4 * i + j] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[i], b[j], c[4 * i + j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += c[i];
+  } else {
+    d4 c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = d4{0, 0, 0, 0};
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[it & 3], b[j], c[j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s += c[i][0] + c[i][1] + c[i][2] + c[i][3];
+  }
+  out[blockIdx.x * 256 + l] = s;
+}
+
+// LDS-fed: per K4 step a wave reads its operands from LDS (random data) -- the
+// 16x16x4 form one A and four B values per lane for 4 instructions (16 rows x 64
+// columns), the 4x4x4 form four A and four B values for 16 instructions (the same
+// 16 x 64 outputs)
+template <bool SMALL>
+__global__ __launch_bounds__(256) void rate_lds_k(const double* __restrict__ rnd, double* out, int iters) {
+  __shared__ double sh[4096];
+  const int l = threadIdx.x, lane = l & 63, w = l >> 6;
+  for (int e = l; e < 4096; e += 256) sh[e] = rnd[(blockIdx.x * 4096 + e) & ((1 << 20) - 1)];
+  __syncthreads();
+  double s = 0.0;
+  const double* A = sh + w * 1024;
+  const double* B = sh + ((w + 1) & 3) * 1024;
+  if constexpr (SMALL) {
+    double c[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] = 0.0;
+    for (int it = 0; it < iters; it++) {
+      const int kk = ((it & 15) << 2) + (lane >> 4);
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = A[kk * 16 + 4 * i + (lane & 3)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = B[kk * 16 + ((lane + 16 * j) & 15) ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[4 * i + j] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[i], b[j], c[4 * i + j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += c[i];
+  } else {
+    d4 c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = d4{0, 0, 0, 0};
+    for (int it = 0; it < iters; it++) {
+      const int kk = ((it & 15) << 2) + (lane >> 4);
+      const double a = A[kk * 16 + (lane & 15)];
+      double b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = B[kk * 16 + ((lane + 16 * j) & 15)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[j], c[j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s += c[i][0] + c[i][1] + c[i][2] + c[i][3];
+  }
+  out[blockIdx.x * 256 + l] = s;
+}
+
 int main() {
   int dev; CK(hipGetDevice(&dev)); hipDeviceProp_t pr; CK(hipGetDeviceProperties(&pr, dev));
   double* d; CK(hipMalloc(&d, sizeof(double) * 4096 * 64));
@@ -97,5 +185,28 @@ int main() {
            small ? "4x4x4_4b " : "16x16x4  ", ms, 2 * macs / ms / 1e9, (double)cyc[0] / iters / (small ? 8 : 4),
            100.0 * cyc[0] / (double)cyc[1]);
   }
+  // random operands: registers, then LDS-fed
+  double* rnd; CK(hipMalloc(&rnd, sizeof(double) * (1 << 20)));
+  {
+    std::vector<double> hr(1 << 20);
+    unsigned x = 12345;
+    for (auto& v : hr) { x = x * 1664525u + 1013904223u; v = 1.0 + (x >> 8) * (1.0 / 16777216.0); }
+    CK(hipMemcpy(rnd, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice));
+  }
+  for (int kind = 0; kind < 2; ++kind)
+    for (int small = 0; small < 2; ++small) {
+      hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); float ms;
+      auto go = [&](int it) {
+        if (kind == 0) { if (small) rate_rand_k<true><<<nb, 256>>>(rnd, d, it); else rate_rand_k<false><<<nb, 256>>>(rnd, d, it); }
+        else { if (small) rate_lds_k<true><<<nb, 256>>>(rnd, d, it); else rate_lds_k<false><<<nb, 256>>>(rnd, d, it); }
+      };
+      go(64); CK(hipDeviceSynchronize());
+      const int it = 2048;
+      CK(hipEventRecord(e0)); go(it); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      // MACs per wave-iteration: 16 x 256 (4x4x4) or 4 x 1024 (16x16x4): 4096 either way
+      const double macs = (double)nb * 4 * it * 4096;
+      printf("%s %s: %.3f ms, %.2f TF\n", kind == 0 ? "random regs" : "random LDS ", small ? "4x4x4_4b" : "16x16x4 ",
+             ms, 2 * macs / ms / 1e9);
+    }
   return 0;
 }
