@@ -67,8 +67,8 @@ __global__ __launch_bounds__(256) void rate_rand_k(const double* __restrict__ rn
   double a[4], b[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    a[i] = rnd[(blockIdx.x * 256 + l) * 8 + i];
-    b[i] = rnd[(blockIdx.x * 256 + l) * 8 + 4 + i];
+    a[i] = rnd[((blockIdx.x * 256 + l) * 8 + i) & ((1 << 20) - 1)];       // (the buffer holds 2^20)
+    b[i] = rnd[((blockIdx.x * 256 + l) * 8 + 4 + i) & ((1 << 20) - 1)];
   }
   double s = 0.0;
   if constexpr (SMALL) {
