@@ -39,18 +39,6 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
-// The 16 x 16 x 4 product acc += A B on the 4x4x4 form: four instructions, one per
-// 4-row group v of A, each block taking 4 of the 16 columns. a4[v] = A[4 v + (lane & 3)]
-// [lane >> 4] (the 16x16x4 form's a = A[lane & 15][lane >> 4]), b as the 16x16x4 form's
-// (B[lane >> 4][lane & 15]); acc[v] of lane l is C[4 v + (l >> 4)][l & 15] -- the
-// 16x16x4 form's C layout -- so callers keep their accumulator maps. 1.5-1.6x the
-// multiply-adds per cycle of v_mfma_f64_16x16x4 on gfx950 (tools/probe_mfma4.hip:
-// 68 vs 42 TF on random register operands, 63 vs 42 TF LDS-fed).
-__device__ __forceinline__ d4 mfma16x4(const double (&a4)[4], double b, d4 acc) {
-#pragma unroll
-  for (int v = 0; v < 4; ++v) acc[v] = mfma4(a4[v], b, acc[v]);
-  return acc;
-}
 // exact f32 (v_mfma_f32_16x16x4_f32 = an fmaf chain). A/B lane maps as the f64
 // form; C/D: lane (r, g) register v holds row 4g + v, column r (the f64 form:
 // row g + 4v).
@@ -79,23 +67,18 @@ __device__ __forceinline__ void tile_mma(const double* __restrict__ As, const do
 #pragma unroll 4
   for (int k0 = 0; k0 < NB; k0 += 4) {
     const int k = k0 + q;
-    // (the 16 x 16 products on the 4x4x4 MFMA: mfma16x4, the same accumulator map)
-    double a0[4], a1[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      a0[v] = As[swz(k, wm * 32 + 4 * v + (r & 3))];
-      a1[v] = As[swz(k, wm * 32 + 16 + 4 * v + (r & 3))];
-      if (NEG) {
-        a0[v] = -a0[v];
-        a1[v] = -a1[v];
-      }
-    }
+    double a0 = As[swz(k, wm * 32 + r)];
+    double a1 = As[swz(k, wm * 32 + 16 + r)];
     const double b0 = Bs[swz(k, wn * 32 + r)];
     const double b1 = Bs[swz(k, wn * 32 + 16 + r)];
-    acc.c[0][0] = mfma16x4(a0, b0, acc.c[0][0]);
-    acc.c[0][1] = mfma16x4(a0, b1, acc.c[0][1]);
-    acc.c[1][0] = mfma16x4(a1, b0, acc.c[1][0]);
-    acc.c[1][1] = mfma16x4(a1, b1, acc.c[1][1]);
+    if (NEG) {
+      a0 = -a0;
+      a1 = -a1;
+    }
+    acc.c[0][0] = mfma(a0, b0, acc.c[0][0]);
+    acc.c[0][1] = mfma(a0, b1, acc.c[0][1]);
+    acc.c[1][0] = mfma(a1, b0, acc.c[1][0]);
+    acc.c[1][1] = mfma(a1, b1, acc.c[1][1]);
   }
 }
 

@@ -195,13 +195,9 @@ __device__ __forceinline__ d4 mfma16(const double* __restrict__ A, int ars, int 
                                      int brs, int bcs, int K, d4 acc, int lane) {
   const int r = lane & 15, q = lane >> 4;
   for (int k0 = 0; k0 < K; k0 += 4) {
-    double a[4];   // (the 4x4x4 MFMA: mfma16x4)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      a[v] = A[(4 * v + (r & 3)) * ars + (k0 + q) * acs];
-      if (NEG) a[v] = -a[v];
-    }
-    acc = mfma16x4(a, B[(k0 + q) * brs + r * bcs], acc);
+    double a = A[r * ars + (k0 + q) * acs];
+    if (NEG) a = -a;
+    acc = mfma(a, B[(k0 + q) * brs + r * bcs], acc);
   }
   return acc;
 }
@@ -574,18 +570,15 @@ __device__ __forceinline__ void main_mma(const double* __restrict__ As, const do
 #pragma unroll
   for (int k0 = 0; k0 < KS; k0 += 4) {
     const int k = k0 + q;
-    // (the 16 x 16 products on the 4x4x4 MFMA: mfma16x4, the same accumulator map)
-    double a[2][4], b[4];
+    double a[2], b[4];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) a[mt][v] = As[swzp(k, wm * 32 + mt * 16 + 4 * v + (r & 3))];
+    for (int mt = 0; mt < 2; ++mt) a[mt] = As[swzp(k, wm * 32 + mt * 16 + r)];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) b[nt] = Bs[swz(k, nt * 16 + r)];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc.c[mt][nt] = mfma16x4(a[mt], b[nt], acc.c[mt][nt]);
+      for (int nt = 0; nt < 4; ++nt) acc.c[mt][nt] = mfma(a[mt], b[nt], acc.c[mt][nt]);
   }
 }
 
