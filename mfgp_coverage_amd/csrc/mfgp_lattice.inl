@@ -1784,6 +1784,7 @@ __device__ __forceinline__ void inc_lat_wg(const GPDesc& d) {
     role -= P;
   }
   if (role < np) {
+    WTRACE(0);
     inc_producer_role<VT>(d, role, sm, reinterpret_cast<int*>(sm + LAT_LDS),
                           *reinterpret_cast<unsigned*>(sm + LAT_LDS + 8));
     return;
