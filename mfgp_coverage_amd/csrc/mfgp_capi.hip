@@ -246,7 +246,7 @@ struct mfgp_model {
   uint64_t tab_gen = 0;
   double* wv = nullptr;       // w [wv_ld][KINC]
   int64_t wv_ld = 0;
-  unsigned* wflag = nullptr;  // [max(wv_ld / 64 + 2, LAT_WUF_OFF) + LAT_WU_MAX]
+  unsigned* wflag = nullptr;  // [wv_ld / 64 + 2]
   unsigned* wcnt = nullptr;   // [wv_ld / 64 + 2]
   double* wpart = nullptr;    // [LAT_WU_MAX + wv_ld / 64 + 1][1024]
   double* gpart = nullptr;    // split-K partials
@@ -760,10 +760,8 @@ int ensure_lat(mfgp_model* m, int64_t tiles, int ksplit, int ka, int64_t nzu) {
     m->wpart = nullptr;
     HIP_TRY(hipMalloc(&m->wv, sizeof(double) * ld * KINC));
     HIP_TRY(hipMemsetAsync(m->wv, 0, sizeof(double) * ld * KINC, s));
-    // per-block flags, then the w units' (mfgp_internal.h LAT_WUF_OFF)
-    const int64_t nwf = std::max<int64_t>(ld / 64 + 2, LAT_WUF_OFF) + LAT_WU_MAX;
-    HIP_TRY(hipMalloc(&m->wflag, sizeof(unsigned) * nwf));
-    HIP_TRY(hipMemsetAsync(m->wflag, 0, sizeof(unsigned) * nwf, s));   // below every epoch
+    HIP_TRY(hipMalloc(&m->wflag, sizeof(unsigned) * (ld / 64 + 2)));
+    HIP_TRY(hipMemsetAsync(m->wflag, 0, sizeof(unsigned) * (ld / 64 + 2), s));   // below every epoch
     HIP_TRY(hipMalloc(&m->wcnt, sizeof(unsigned) * 2 * (ld / 64 + 2)));
     HIP_TRY(hipMemsetAsync(m->wcnt, 0, sizeof(unsigned) * 2 * (ld / 64 + 2), s));
     HIP_TRY(hipMalloc(&m->wpart, sizeof(double) * 1024 * (LAT_WU_MAX + ld / 64 + 1)));

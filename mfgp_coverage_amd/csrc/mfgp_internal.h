@@ -156,9 +156,6 @@ struct GPDesc {
 // LAT_NWB_MAX blocks of 64 columns
 constexpr int LAT_WU_MAX = 512;
 constexpr int LAT_NWB_MAX = 256;
-// GPDesc::wflag: [LAT_WUF_OFF] per-64-row-block flags (w of the block stored) |
-// [LAT_WU_MAX] per-w-unit flags (the unit's partials stored: the Z units sum them)
-constexpr int LAT_WUF_OFF = LAT_NWB_MAX + 2;
 constexpr int ZKS = 8;   // lattice-axis GEMM: K rows per pipeline stage (Z / axis-table rows)
 // F's column block jb starts at fblk_off(jb, ld): blocks b < jb hold ld - 64 b rows of 64
 inline __host__ __device__ int64_t fblk_off(int64_t jb, int64_t ld) { return 64 * jb * ld - 2048 * jb * (jb - 1); }

@@ -595,11 +595,6 @@ __device__ __forceinline__ void lat_wblock(const GPDesc& d, int64_t u, double* s
   // count the unit's partials in (one arrival per block, all at once)
   drain_stores();
   __syncthreads();
-  // the unit's own flag: its partials are stored (the member-list Z units sum the
-  // partials of their members' blocks themselves, in slot order -- the block
-  // reducers' sums, the same bits -- instead of waiting for the reducers' round
-  // trips: count, load, add, store, drain, flag)
-  if (tid == 0) publish(d.wflag + LAT_WUF_OFF + u, epoch);
   if (tid < nseg) {
     const int64_t jb = segs[tid];
     const unsigned old = __hip_atomic_fetch_add(d.wcnt + jb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1022,42 +1017,8 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
   int* const mj = reinterpret_cast<int*>(sm);        // [ZCH]
   int* const mpx = mj + ZCH;                          // [ZCH]
   double* const cws = sm + ZCH;                       // [ZCH][KA]
-  // per 64-row block of w: its first contributing w unit's partial slot and the
-  // number of contributors (lat_wblock's partition, wst_*): w[j][a] is the sum of
-  // those partials in slot order, the block reducer's sum
-  int* const bslot = reinterpret_cast<int*>(sm + ZCH + ZCH * KA);   // [LAT_NWB_MAX]
-  int* const bcnt = bslot + LAT_NWB_MAX;                            // [LAT_NWB_MAX]
-  static_assert(ZCH + ZCH * KA + LAT_NWB_MAX <= LAT_LDS, "the Z unit's LDS fits");
-  // (the Z rows' staging at the end overwrites the tables: no w is read after it)
+  static_assert(ZCH + ZCH * KA <= LAT_LDS, "the Z unit's LDS fits");
   WTRACE(0);
-  {
-    const int64_t n0 = d.n0, nwb = d.nwb, U = d.nwu;
-    const int64_t C = (n0 + 15) / 16, K2 = 2 * C - 4 * (nwb - 1);
-    const int64_t S = (nwb / 2) * K2 + (nwb & 1) * (C - 4 * (nwb / 2));
-    for (int64_t jb = tid; jb < nwb; jb += NT) {
-      const int64_t f = wst_first(C, nwb, jb);
-      const int64_t ua = wst_unit(f, S, U), ub = wst_unit(f + C - 4 * jb - 1, S, U);
-      bslot[jb] = (int)(ua + wst_pos(nwb, jb));
-      bcnt[jb] = (int)(ub - ua + 1);
-    }
-  }
-  const double* const wpart = d.wpart;
-  // w[j][a] from the partials of j's block, four loads in flight at a time
-  auto w_of = [&](int64_t j, int a) {
-    const int jb = (int)(j >> 6);
-    const double* p = wpart + (int64_t)bslot[jb] * 1024 + (j & 63) * 16 + a;
-    const int R = bcnt[jb];
-    double t = 0.0;
-    for (int r0 = 0; r0 < R; r0 += 4) {
-      double x[4];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) x[rr] = r0 + rr < R ? ldx<true>(p + (r0 + rr) * 1024) : 0.0;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        if (r0 + rr < R) t = (r0 + rr == 0) ? x[rr] : t + x[rr];
-    }
-    return t;
-  };
   // the part's lists (the scan unit was dispatched before any producer)
   wait_flag(d, d.zflag + d.nzu + part, epoch);
   const unsigned* const off = d.csr + (int64_t)part * (tabw + 1 + d.ld);
@@ -1114,7 +1075,7 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
     };
     load_ex(0);
     if (!waited) {
-      wait_flags_all(d, d.wflag + LAT_WUF_OFF, d.nwu, epoch);   // every w unit's partials (a barrier)
+      wait_flags_all(d, d.wflag, d.nwb, epoch);   // w of every block (every wave: a barrier)
       WTRACE(3);
       waited = true;
     }
@@ -1128,7 +1089,7 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
         v[i2] = 0.0;
         if (m < cn) {
           const int64_t j = mj[m];
-          v[i2] = w_of(j, a) * coef(j);   // L2-served: stored in this launch
+          v[i2] = ldx<true>(&wv[j * KINC + a]) * coef(j);   // L2-served: stored in this launch
         }
       }
       __syncthreads();   // (every thread has read mj: cws may be written)
@@ -1152,8 +1113,7 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
     }
   }
   if (!waited) {
-    // (a unit without members still waits: its virtual rows need w)
-    wait_flags_all(d, d.wflag + LAT_WUF_OFF, d.nwu, epoch);
+    wait_flags_all(d, d.wflag, d.nwb, epoch);   // (a unit without members still waits: its virtual rows need w)
     WTRACE(3);
   }
   WTRACE(4);
@@ -1169,7 +1129,7 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
           const int64_t j = __hip_atomic_load(zvl + 1 + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const double e = d.tab[(2 * part) * tstride + j * tabw + ix];
 #pragma unroll
-          for (int a = 0; a < KA; ++a) stx<true>(zr + a, w_of(j, a) * e);
+          for (int a = 0; a < KA; ++a) stx<true>(zr + a, ldx<true>(&wv[j * KINC + a]) * e);
         } else {
 #pragma unroll
           for (int a = 0; a < KA; ++a) stx<true>(zr + a, 0.0);
