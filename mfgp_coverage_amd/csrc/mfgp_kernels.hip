@@ -221,38 +221,23 @@ __device__ void factor_invert_64(double* __restrict__ S, double* __restrict__ R,
       for (int c = 0; c < DB; ++c) d[c] = S[(o + r16) * SP + o + c];
       double rdiag = 1.0;
       int fail = INT_MAX;
-      // The pivot chain, software-pipelined: pivot j's rank-1 update of column j + 1
-      // (the next pivot's input) runs first; its updates of columns k > j + 1 are
-      // issued inside pivot j + 1's chain, between its broadcast and its square
-      // root's dependent steps (the wave issues in order: written after pivot j, they
-      // held pivot j + 1's broadcast behind 14 - j of them, ~460 cycles per pivot).
-      // Every column still takes the pivots' updates in pivot order, with the same
-      // fused operations: the same bits.
-      double lp = 0.0;   // the previous pivot's column entry of this lane
 #pragma unroll
       for (int j = 0; j < DB; ++j) {
         double p = bcast16(d[j], j);
-        // the previous pivot's updates still pending: column j + 1 before this
-        // pivot's own update of it, the rest while the chain below waits
-        if (j > 0 && j + 1 < DB) d[j + 1] = fmac_bcast16<true>(d[j + 1], lp, lp, j + 1);
         const int64_t g = g0 + o + j;
         const bool pad = g >= N;
         const bool bad = !pad && !(p > 0.0);
         fail = bad ? min(fail, (int)(g + 1)) : fail;
         p = (pad || bad) ? 1.0 : p;
-#pragma unroll
-        for (int k = j + 2; k < DB; ++k)
-          if (j > 0) d[k] = fmac_bcast16<true>(d[k], lp, lp, k);
         const double rs = rsqrt(p);
         const double l = (r16 >= j) ? (r16 == j ? p : d[j]) * rs : 0.0;
         rdiag = (r16 == j) ? rs : rdiag;
         d[j] = l;
         // d[k] -= l_r l_k for every row r: rows r > j are the update; rows r < j have
         // l_r = 0; row j's columns k > j are above the diagonal (never read: the
-        // store below and the substitution read columns <= the row). Column j + 1
-        // now; the others in the next pivot's chain (above), the last pivot's none
-        if (j + 1 < DB) d[j + 1] = fmac_bcast16<true>(d[j + 1], l, l, j + 1);
-        lp = l;
+        // store below and the substitution read columns <= the row)
+#pragma unroll
+        for (int k = j + 1; k < DB; ++k) d[k] = fmac_bcast16<true>(d[k], l, l, k);
       }
       if (fail != INT_MAX && lane == 0) atomicMin(status, fail);
       if (lane < DB) {
