@@ -6,7 +6,7 @@ cd $R
 mkdir -p gpurun_out
 for rep in 1 2; do
 for v in "$@"; do
-  L=$R/build/libmfgp_$v.so; [ -f "$L" ] || L=$R/diag/libmfgp_$v.so
+  L=$R/tools/stamps_lib/libmfgp_$v.so; [ -f "$L" ] || L=$R/build/libmfgp_$v.so
   [ "$v" = "default" ] && L=$R/mfgp_coverage_amd/libmfgp_hip.so
   MFGP_LIB=$L timeout -k 10 120 python -u bench.py --diagnostic --no-full --no-cpu-baseline --steps 300 --warmup 30 > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { echo "$v failed rc=$?"; tail -5 gpurun_out/ab_$v.err; exit 1; }
   python - "$v" gpurun_out/ab_$v.json <<'PY'
