@@ -1164,15 +1164,6 @@ __device__ int lattice_cell(const GPDesc& d, double px, double py) {
 // End of a gathering producer chunk: its compact rows (and L21 rows in A) are
 // drained and announced in pflag[chunk] (the cell workgroups wait for these),
 // then the chunk's partials (red, summed over the waves) are stored for the finish.
-__device__ __forceinline__ void inc_chunk_partials(const GPDesc& d, int64_t chunk, double (*red)[ISZ]) {
-  double* __restrict__ part = d.iscr + ISC0 + chunk * ISZ;
-  for (int e = threadIdx.x; e < ISZ; e += NT) {
-    double acc = 0.0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w) acc += red[w][e];
-    stx<true>(part + e, acc);
-  }
-}
 __device__ __forceinline__ bool inc_chunk_done(const GPDesc& d, int64_t chunk, double (*red)[ISZ]) {
   drain_stores();
   __syncthreads();
@@ -1198,8 +1189,7 @@ __device__ __forceinline__ bool inc_chunk_done(const GPDesc& d, int64_t chunk, d
 // chunk's identity padding of newly entered blocks (rows [n0, N) excepted: they
 // are the L21 stores, so no barrier orders the two).
 template <class VT>
-__device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, int64_t j_hi, double (*red)[ISZ],
-                                                double (&akeep)[8]) {
+__device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, int64_t j_hi, double (*red)[ISZ]) {
   constexpr int NW = NT / 64, IU = 8;
   static_assert(4 * NW * IU >= FUSED_CHUNK, "one round of loads covers a chunk");
   const int64_t n0 = d.n0, ld = d.ld, N = d.N;
@@ -1228,8 +1218,7 @@ __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, i
   }
   const bool miss = r < k && !(g.x == px && g.y == py);
   if (__ballot(miss) != 0) return false;
-  (void)A;
-  (void)ld;
+  inc_init_blocks<true>(d, j_lo, j_hi, false, n0, N);
   d4 sacc = {0.0, 0.0, 0.0, 0.0}, uacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int u = 0; u < IU; ++u) {
@@ -1237,9 +1226,7 @@ __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, i
     const bool ok = j < j_hi;
     a[u] = (ok && r < k) ? a[u] : 0.0;
     zz[u] = ok ? zz[u] : 0.0;
-    // (the L21 rows of A and the identity padding come after the compact rows'
-    // announcement: inc_gather_late)
-    akeep[u] = a[u];
+    if (r < k && ok) stx<true>(&A[j * ld + n0 + r], a[u]);
     if (ok) store_l21c<true, VT>(l21c, j, r, k, a[u], zz[u]);
     sacc = mfma(a[u], a[u], sacc);
     uacc = mfma(a[u], zz[u], uacc);
@@ -1250,28 +1237,6 @@ __device__ __forceinline__ bool inc_gather_fast(const GPDesc& d, int64_t j_lo, i
     if (r == 0) red[w][KINC * KINC + q + 4 * v] = uacc[v];
   }
   return true;
-}
-
-// The fast path's stores that no workgroup of the launch reads before the producers'
-// arrival count (the finish reads the last block's L21 rows after it): the L21 rows
-// into A (column n0 + r of row j, as inc_gather_fast's lanes hold them) and the
-// chunk's identity padding of newly entered blocks. Issued after the compact rows
-// are announced, so that the drain in front of the announcement waits for the
-// compact rows only (~128 fewer scattered lines per producer).
-__device__ __forceinline__ void inc_gather_late(const GPDesc& d, int64_t j_lo, int64_t j_hi, const double (&akeep)[8]) {
-  constexpr int NW = NT / 64, IU = 8;
-  const int64_t n0 = d.n0, ld = d.ld, N = d.N;
-  const int k = (int)(N - n0);
-  double* const A = d.A;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 15, q = lane >> 4;
-  inc_init_blocks<true>(d, j_lo, j_hi, false, n0, N);
-#pragma unroll
-  for (int u = 0; u < IU; ++u) {
-    const int64_t j = j_lo + 4 * (w + NW * u) + q;
-    if (r < k && j < j_hi) stx<true>(&A[j * ld + n0 + r], akeep[u]);
-  }
 }
 
 // One producer chunk: land device-resident new rows (chunk 0), find the new
@@ -1310,18 +1275,9 @@ __device__ MFGP_PRODUCE_INLINE bool inc_produce(const GPDesc& d, int64_t chunk, 
   }
   const int64_t j_lo = chunk * ch;
   const int64_t j_hi = j_lo + ch < n0 ? j_lo + ch : n0;
-  double akeep[8];
-  if (d.lat.nx > 0 && j_lo < n0 && ch <= FUSED_CHUNK && inc_gather_fast<VT>(d, j_lo, j_hi, red, akeep)) {
+  if (d.lat.nx > 0 && j_lo < n0 && ch <= FUSED_CHUNK && inc_gather_fast<VT>(d, j_lo, j_hi, red)) {
     if (chunk == 0 && tid == 0) stx<XW>(d.iscr, 1.0);
-    // the compact rows, drained and announced (the consumers wait for them); then
-    // the rest, drained by the caller before it counts the producer in
-    drain_stores();
-    __syncthreads();
-    if (tid == 0) publish(d.pflag + chunk, d.epoch);
-    FSTAMP(39);   // latest producer past its gather
-    inc_gather_late(d, j_lo, j_hi, akeep);
-    inc_chunk_partials(d, chunk, red);
-    return true;
+    return inc_chunk_done(d, chunk, red);
   }
   if (tid < KINC) cell[tid] = INT_MAX;
   __syncthreads();
