@@ -39,18 +39,6 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
-// The 16 x 16 x 4 product acc += A B on the 4x4x4 form: four instructions, one per
-// 4-row group v of A, each block taking 4 of the 16 columns. a4[v] = A[4 v + (lane & 3)]
-// [lane >> 4] (the 16x16x4 form's a = A[lane & 15][lane >> 4]), b as the 16x16x4 form's
-// (B[lane >> 4][lane & 15]); acc[v] of lane l is C[4 v + (l >> 4)][l & 15] -- the
-// 16x16x4 form's C layout -- so callers keep their accumulator maps. 1.5-1.6x the
-// multiply-adds per cycle of v_mfma_f64_16x16x4 on gfx950 (tools/probe_mfma4.hip:
-// 68 vs 42 TF on random register operands, 63 vs 42 TF LDS-fed), for 4x the A reads.
-__device__ __forceinline__ d4 mfma16x4(const double (&a4)[4], double b, d4 acc) {
-#pragma unroll
-  for (int v = 0; v < 4; ++v) acc[v] = mfma4(a4[v], b, acc[v]);
-  return acc;
-}
 // exact f32 (v_mfma_f32_16x16x4_f32 = an fmaf chain). A/B lane maps as the f64
 // form; C/D: lane (r, g) register v holds row 4g + v, column r (the f64 form:
 // row g + 4v).

@@ -1296,25 +1296,22 @@ __device__ __forceinline__ void vm_wait_bar(int n) {
 __device__ __forceinline__ void lat_zcompute(const double* slot, d4 (&acc)[2][4], int w, int r, int q) {
   const double* As = slot;
   const double* Bs = slot + ZKS * 128;
-  // the 16 x 16 products on the 4x4x4 MFMA (mfma16x4: the same accumulator map, so
-  // the split-K partials and the cells read them as before), one 4-row k-step's
-  // operands live at a time (both at once spilled the kernel's other roles);
-  // k_lat_gemm2 issues the same products in the same order: the two forms stay
-  // bit-equal
+  double a[2][2], b[2][4];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int k = 4 * e + q;
-    double a[2][4], b[4];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < 2; ++m) a[e][m] = As[k * 128 + ((32 * w + 16 * m + r) ^ ((k & 1) << 4))];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) a[m][v] = As[k * 128 + ((32 * w + 16 * m + 4 * v + (r & 3)) ^ ((k & 1) << 4))];
+    for (int n = 0; n < 4; ++n) b[e][n] = Bs[swz(k, 16 * n + r)];
+  }
+  __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
 #pragma unroll
-    for (int n = 0; n < 4; ++n) b[n] = Bs[swz(k, 16 * n + r)];
+  for (int e = 0; e < 2; ++e) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      acc[0][n] = mfma16x4(a[0], b[n], acc[0][n]);
-      acc[1][n] = mfma16x4(a[1], b[n], acc[1][n]);
+      acc[0][n] = mfma(a[e][0], b[e][n], acc[0][n]);
+      acc[1][n] = mfma(a[e][1], b[e][n], acc[1][n]);
     }
   }
 }
@@ -2000,13 +1997,11 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
         const double* slot = ring + ((slot0 + t) % G2NST) * G2STG;
         const double* As = slot;
         const double* Bs = slot + ZKS * G2R;
-        // (the 16 x 16 products on the 4x4x4 MFMA, as lat_zcompute: mfma16x4)
-        double a[2][4], b[2][4];
+        double a[2], b[2][4];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int kk = 4 * e + q;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) a[e][v] = As[kk * G2R + ((16 * w + 4 * v + (r & 3)) ^ ((kk & 3) << 4))];
+          a[e] = As[kk * G2R + ((16 * w + r) ^ ((kk & 3) << 4))];
 #pragma unroll
           for (int n = 0; n < 4; ++n) b[e][n] = Bs[swz(kk, 16 * n + r)];
         }
@@ -2014,7 +2009,7 @@ __device__ __forceinline__ void lat_gemm2(const GPDesc& d, int64_t tile) {
 #pragma unroll
         for (int e = 0; e < 2; ++e)
 #pragma unroll
-          for (int n = 0; n < 4; ++n) acc[n] = mfma16x4(a[e], b[e][n], acc[n]);
+          for (int n = 0; n < 4; ++n) acc[n] = mfma(a[e], b[e][n], acc[n]);
         if (t + D < hi) issue(s + (t + D) * G2S, virt, slot0 + t + D);
       }
     }
