@@ -140,3 +140,27 @@ def test_hand_off_polls_read_device_scope_and_wait(hand_offs):
         for it in its:
             assert it["loads"] and it["sc1"], (name, it)
             assert it["waited"], (name, it)
+
+
+def test_poll_check_catches_plain_and_unwaited_polls(report):
+    """The poll check itself: in a real spin loop of k_inc_lat, a flag load without
+    sc1 or a missing s_waitcnt vmcnt(0) before the loop's exit branch is reported."""
+    import tempfile
+    import check_codeobj
+    with tempfile.TemporaryDirectory() as td:
+        dis = check_codeobj.disassembly(check_codeobj.code_object(
+            os.path.join(ROOT, "mfgp_coverage_amd", "libmfgp_hip.so"), td))
+    name = next(n for n in dis if "k_inc_lat_arg" in n)
+    ins = dis[name]
+    its = check_codeobj.poll_iterations(ins)
+    assert its and all(it["loads"] and it["sc1"] and it["waited"] for it in its)
+    # the first spin's first load: drop its sc1; separately, drop the waits after it
+    i = next(k for k, x in enumerate(ins) if x[1] == "s_sleep")
+    first = check_codeobj.poll_iterations(ins[:i + 400])[0]
+    assert first["loads"], first
+    plain = [(a, op, args.replace(" sc1", ""), t) if op.startswith(check_codeobj.VMEM_LOAD) else (a, op, args, t)
+             for a, op, args, t in ins]
+    assert not check_codeobj.poll_iterations(plain)[0]["sc1"]
+    unwaited = [(a, "s_nop", "0", t) if op == "s_waitcnt" and "vmcnt(0)" in args else (a, op, args, t)
+                for a, op, args, t in ins]
+    assert not check_codeobj.poll_iterations(unwaited)[0]["waited"]

@@ -77,38 +77,38 @@ VMEM_LOAD = ("global_load", "buffer_load", "flat_load")
 
 def poll_iterations(ins):
     """The hand-off waits' poll iterations of one kernel. Every bounded spin sleeps
-    (s_sleep) between polls, so each s_sleep starts one iteration: its flag loads,
-    up to the first conditional branch after them, the one that decides whether to
-    poll again (a branch before them is the spin bound's), following unconditional
-    branches. Returns one record per iteration: the iteration's vector loads;
-    whether all carry sc1 (device scope, L2-coherent across the XCDs: a flag is
-    never served from a stale line); and whether an s_waitcnt vmcnt(0) lies
-    between the last of them and the branch (the branch reads the flag's value, so
-    nothing after the exit is issued before the flag was seen)."""
+    (s_sleep) between polls, so each s_sleep marks one spin loop: the instructions
+    from the target of the first branch after the s_sleep that jumps back to it or
+    above (the loop's back edge; the compiler may put the bound's test on it) up to
+    that branch. Returns one record per s_sleep: the loop's vector loads (its polls
+    of the hand-off words); whether all carry sc1 (device scope, L2-coherent across
+    the XCDs: a flag is never served from a stale line); and whether every one of
+    them is followed by an s_waitcnt vmcnt(0) before the next conditional branch
+    (the branch reads the flag's value, so nothing after the exit is issued before
+    the flag was seen)."""
     at = {a: i for i, (a, _, _, _) in enumerate(ins)}
     out = []
-    for i, (_, op, _, _) in enumerate(ins):
+    for i, (addr, op, _, _) in enumerate(ins):
         if op != "s_sleep":
             continue
-        loads, pending, waited, j = [], False, False, i + 1
-        for _ in range(300):
-            if j >= len(ins):
+        head = br = None
+        for j in range(i + 1, min(len(ins), i + 400)):
+            _, op2, _, tgt = ins[j]
+            if op2.startswith(("s_branch", "s_cbranch")) and tgt is not None and tgt <= addr and tgt in at:
+                head, br = at[tgt], j
                 break
-            _, op2, args, tgt = ins[j]
+        body = ins[head:br + 1] if head is not None else []
+        loads, waited, pending = [], True, False
+        for _, op2, args, _ in body:
             if op2.startswith(VMEM_LOAD):
                 loads.append((op2, args))
                 pending = True
             elif op2 == "s_waitcnt" and "vmcnt(0)" in args:
                 pending = False
-            elif op2.startswith("s_cbranch") and loads:
-                waited = not pending
-                break
-            elif op2 == "s_branch" and tgt in at:
-                j = at[tgt]
-                continue
-            j += 1
+            elif op2.startswith("s_cbranch") and pending:
+                waited = False
         out.append({"loads": loads, "sc1": bool(loads) and all(re.search(r"\bsc1\b", a) for _, a in loads),
-                    "waited": waited})
+                    "waited": waited and bool(loads)})
     return out
 
 
