@@ -755,6 +755,9 @@ __device__ __forceinline__ void lat_zunit(const GPDesc& d, int64_t zu, double* s
   // ~16 members per row) rather than 16, whose axis values held 64 VGPRs and made
   // the kernel spill 16 (2 now); the same FMAs in the same order, 0.5-2 % faster
   // (tools/ab_variants.sh zmb8 zmb12, round 4)
+#ifndef MFGP_ZST
+#define MFGP_ZST 6   // member-list Z units: members staged per row in LDS before the w wait
+#endif
 #ifndef MFGP_ZMB8
 #define MFGP_ZMB8 8
 #endif
@@ -1012,12 +1015,18 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
   const double cL = h.kind == 0 ? h.sL : h.rho * h.sL, cLH = h.rho2 * h.sL;
   auto coef = [&](int64_t j) { return part == 1 ? h.sH : (j < NL ? cL : cLH); };
   // LDS: the unit's members in chunks of ZCH (their rows' lists are contiguous in the
-  // CSR): training row j and axis column px, then (after the w wait) the c w rows
-  constexpr int ZCH = 256;
+  // CSR): training row j and axis column px, then (after the w wait) the c w rows;
+  // then the stash: each row's members ZMB .. ZMB + ZST - 1 of the first chunk, their
+  // axis rows ex(px, .) DMA'd before the w wait (MFGP_ZST; tabw a multiple of 128),
+  // so that a row of up to ZMB + ZST members loads nothing after the wait
+  constexpr int ZST = KA == 8 ? MFGP_ZST : 0;
+  constexpr int ZCH = ZST > 0 ? 128 : 256;
   int* const mj = reinterpret_cast<int*>(sm);        // [ZCH]
   int* const mpx = mj + ZCH;                          // [ZCH]
   double* const cws = sm + ZCH;                       // [ZCH][KA]
-  static_assert(ZCH + ZCH * KA <= LAT_LDS, "the Z unit's LDS fits");
+  double* const stash = cws + ZCH * KA;               // [ZQ rows][ZST][tabw] = [2 NT][ZST]
+  static_assert(ZCH + ZCH * KA + 2 * NT * ZST <= LAT_LDS, "the Z unit's LDS fits");
+  const bool use_st = ZST > 0 && tabw % 128 == 0 && ZQ * tabw == 2 * NT;
   WTRACE(0);
   // the part's lists (the scan unit was dispatched before any producer)
   wait_flag(d, d.zflag + d.nzu + part, epoch);
@@ -1074,6 +1083,23 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
         }
     };
     load_ex(0);
+    if (use_st && c0 == 0) {
+      // the stash: one LDS-DMA per (row, slot, 128 columns), 16 bytes a lane (the wave
+      // takes instructions w, w + 4, ...); no registers held across the wait
+      const int NHf = (int)(tabw / 128);
+      const int lane = tid & 63, wv4 = tid >> 6;
+      const double* const axb = d.axt + (2 * part) * (tabw + 1) * tabw;
+      for (int pi = wv4; pi < ZQ * ZST * NHf; pi += NT / 64) {
+        const int r = pi / (ZST * NHf), sl = (pi / NHf) % ZST, hf = pi % NHf;
+        const int64_t q = qa + r;
+        if (q >= ny) continue;
+        const int e = (int)ldu(off + q) - u_lo + ZMB + sl;   // the member (chunk 0)
+        if (e >= (int)ldu(off + q + 1) - u_lo || e >= cn) continue;
+        const double* src = axb + (int64_t)mpx[e] * tabw + hf * 128 + 2 * lane;
+        __builtin_amdgcn_global_load_lds((const GLOBAL void*)src, (lds_vptr)(stash + ((int64_t)r * ZST + sl) * tabw + hf * 128),
+                                         16, 0, 0);
+      }
+    }
     if (!waited) {
       wait_flags_all(d, d.wflag, d.nwb, epoch);   // w of every block (every wave: a barrier)
       WTRACE(3);
@@ -1096,20 +1122,34 @@ __device__ __forceinline__ void lat_zunit_csr(const GPDesc& d, int64_t zu, doubl
 #pragma unroll
       for (int i2 = 0; i2 < NE; ++i2)
         if (tid + NT * i2 < ZCH * KA) cws[tid + NT * i2] = v[i2];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the stash's DMAs: every wave's, at the barrier)
       __syncthreads();
     }
-    for (int m0 = 0; m0 < mmax; m0 += ZMB) {
-      if (m0 > 0) load_ex(m0);
+    // the members in order: batch 0 (registers), then the stash (ZST), then batches
+    // of ZMB from memory -- the same FMAs in the same order as without the stash
+    for (int m0 = 0; m0 < mmax;) {
+      const bool st = use_st && c0 == 0 && m0 == ZMB;
+      if (st) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int m = 0; m < ZMB; ++m)
+            ex[hh][m] = m < ZST && b0[hh] + m0 + m < b1[hh] ? stash[((ql + hh * ZH) * ZST + m) * tabw + ix] : 0.0;
+      } else if (m0 > 0) {
+        load_ex(m0);
+      }
+      const int mn = st ? ZST : ZMB;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
         for (int m = 0; m < ZMB; ++m) {
           const int e = b0[hh] + m0 + m;
-          if (e < b1[hh]) {
+          if (m < mn && e < b1[hh]) {
 #pragma unroll
             for (int a = 0; a < KA; ++a) acc[hh][a] = __builtin_fma(cws[e * KA + a], ex[hh][m], acc[hh][a]);
           }
         }
+      m0 += mn;
     }
   }
   if (!waited) {
